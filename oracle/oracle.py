@@ -1,0 +1,274 @@
+"""ctypes wrapper over oracle/_build/libsb_oracle.so.
+
+TEST INFRASTRUCTURE ONLY: the CPU restatement of the strawboat (b41sh/pa)
+codec path used as the parity checker and as bench.py's cpu_baseline leg.
+The product package (pa_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libsb_oracle.so")
+
+# codec ids (compression/mod.rs:64-82)
+NONE, LZ4, ZSTD, SNAPPY = 0, 1, 2, 3
+RLE, DICT, ONE_VALUE, FREQ, BITPACKING, DELTA_BITPACKING, PATAS = 10, 11, 12, 13, 14, 15, 16
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what}: oracle status {code}")
+        self.code = code
+
+
+class _Buf(ctypes.Structure):
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8)), ("len", ctypes.c_size_t), ("cap", ctypes.c_size_t)]
+
+
+class WriteOptions(ctypes.Structure):
+    """write::WriteOptions (write/common.rs:37-45) + forced codec + sampler seed."""
+
+    _fields_ = [
+        ("default_codec", ctypes.c_int32),
+        ("has_ratio", ctypes.c_int32),
+        ("ratio", ctypes.c_double),
+        ("forbidden_mask", ctypes.c_uint32),
+        ("forced_codec", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+    @classmethod
+    def make(cls, default_codec=NONE, ratio=None, forbidden=(), forced=-1, seed=42):
+        m = 0
+        for c in forbidden:
+            m |= 1 << c
+        return cls(default_codec, ratio is not None, float(ratio or 0.0), m, forced, seed)
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        PS = ctypes.POINTER(ctypes.c_size_t)
+        L.orc_buf_free.argtypes = [ctypes.POINTER(_Buf)]
+        L.orc_bp4x_num_bits.argtypes = [P]
+        L.orc_bp4x_num_bits.restype = ctypes.c_uint32
+        for f in ("orc_bp4x_pack", "orc_bp4x_unpack"):
+            getattr(L, f).argtypes = [P, ctypes.c_uint32, P]
+            getattr(L, f).restype = S
+        for f in ("orc_bp4x_pack_sorted", "orc_bp4x_unpack_sorted"):
+            getattr(L, f).argtypes = [ctypes.c_uint32, P, ctypes.c_uint32, P]
+            getattr(L, f).restype = S
+        for f in ("orc_decompress_integer", "orc_decompress_double"):
+            getattr(L, f).argtypes = [P, S, PS, I, S, P]
+            getattr(L, f).restype = I
+        L.orc_compress_integer.argtypes = [P, P, S, I, I, ctypes.POINTER(WriteOptions), ctypes.POINTER(_Buf)]
+        L.orc_compress_double.argtypes = [P, P, S, I, ctypes.POINTER(WriteOptions), ctypes.POINTER(_Buf)]
+        L.orc_patas_pack.argtypes = [ctypes.c_uint32] * 3
+        L.orc_patas_pack.restype = ctypes.c_uint16
+        L.orc_patas_unpack.argtypes = [ctypes.c_uint16] + [ctypes.POINTER(ctypes.c_uint32)] * 3
+        L.orc_read_validity.argtypes = [P, S, PS, S, P]
+        L.orc_write_validity.argtypes = [P, S, ctypes.POINTER(_Buf)]
+        L.orc_read_flat_page.argtypes = [P, S, S, I, I, I, P, P]
+        L.orc_write_flat_page.argtypes = [P, P, S, I, I, I, I, ctypes.POINTER(WriteOptions), ctypes.POINTER(_Buf)]
+        L.orc_roaring_decode.argtypes = [P, S, P, S, PS]
+        L.orc_roaring_encode.argtypes = [P, S, ctypes.POINTER(_Buf)]
+        L.orc_hybrid_decode.argtypes = [P, S, ctypes.c_uint32, S, P]
+        L.orc_common_decompress.argtypes = [I, P, S, P, S]
+        L.orc_common_compress.argtypes = [I, P, S, ctypes.POINTER(_Buf)]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _take(buf: _Buf) -> bytes:
+    out = ctypes.string_at(buf.data, buf.len) if buf.len else b""
+    lib().orc_buf_free(ctypes.byref(buf))
+    return out
+
+
+def _check(rc, what):
+    if rc:
+        raise OracleError(rc, what)
+
+
+def _bytes_arr(b: bytes) -> np.ndarray:
+    return np.frombuffer(b, dtype=np.uint8).copy() if b else np.zeros(1, np.uint8)
+
+
+# ---- BitPacker4x ----------------------------------------------------------
+def bp4x_num_bits(block: np.ndarray) -> int:
+    block = np.ascontiguousarray(block, dtype=np.uint32)
+    return lib().orc_bp4x_num_bits(_ptr(block))
+
+
+def bp4x_pack(block: np.ndarray, b: int, sorted_initial=None) -> bytes:
+    block = np.ascontiguousarray(block, dtype=np.uint32)
+    out = np.zeros(512, np.uint8)
+    if sorted_initial is None:
+        n = lib().orc_bp4x_pack(_ptr(block), b, _ptr(out))
+    else:
+        n = lib().orc_bp4x_pack_sorted(sorted_initial, _ptr(block), b, _ptr(out))
+    return out[:n].tobytes()
+
+
+def bp4x_unpack(data: bytes, b: int, sorted_initial=None) -> np.ndarray:
+    src = np.zeros(512 + 16, np.uint8)
+    src[: len(data)] = np.frombuffer(data, np.uint8)
+    out = np.zeros(128, np.uint32)
+    if sorted_initial is None:
+        lib().orc_bp4x_unpack(_ptr(src), b, _ptr(out))
+    else:
+        lib().orc_bp4x_unpack_sorted(sorted_initial, _ptr(src), b, _ptr(out))
+    return out
+
+
+# ---- value streams ----------------------------------------------------------
+def compress(values: np.ndarray, validity=None, opts: WriteOptions | None = None) -> bytes:
+    """compress_integer / compress_double on one page's values."""
+    values = np.ascontiguousarray(values)
+    opts = opts or WriteOptions.make()
+    buf = _Buf()
+    vb = None if validity is None else np.packbits(np.asarray(validity, bool), bitorder="little")
+    if values.dtype.kind == "f":
+        rc = lib().orc_compress_double(_ptr(values), _ptr(vb), len(values), values.itemsize, ctypes.byref(opts), ctypes.byref(buf))
+    else:
+        rc = lib().orc_compress_integer(
+            _ptr(values), _ptr(vb), len(values), values.itemsize, int(values.dtype.kind == "i"), ctypes.byref(opts), ctypes.byref(buf)
+        )
+    data = _take(buf)
+    _check(rc, "compress")
+    return data
+
+
+def decompress(data: bytes, dtype, length: int, pos: int = 0):
+    """decompress_integer / decompress_double; returns (values, new_pos)."""
+    dtype = np.dtype(dtype)
+    src = _bytes_arr(data)
+    out = np.zeros(max(length, 1), dtype)
+    p = ctypes.c_size_t(pos)
+    f = lib().orc_decompress_double if dtype.kind == "f" else lib().orc_decompress_integer
+    rc = f(_ptr(src), len(data), ctypes.byref(p), dtype.itemsize, length, _ptr(out))
+    _check(rc, "decompress")
+    return out[:length], p.value
+
+
+def write_validity(validity) -> bytes:
+    v = np.packbits(np.asarray(validity, bool), bitorder="little")
+    buf = _Buf()
+    _check(lib().orc_write_validity(_ptr(v), len(validity), ctypes.byref(buf)), "write_validity")
+    return _take(buf)
+
+
+def read_validity(data: bytes, length: int, pos: int = 0):
+    src = _bytes_arr(data)
+    out = np.zeros((length + 7) // 8 + 1, np.uint8)
+    p = ctypes.c_size_t(pos)
+    _check(lib().orc_read_validity(_ptr(src), len(data), ctypes.byref(p), length, _ptr(out)), "read_validity")
+    return np.unpackbits(out, bitorder="little")[:length].astype(bool), p.value
+
+
+def write_page(values: np.ndarray, validity=None, nullable=False, opts: WriteOptions | None = None) -> bytes:
+    """One flat page as serialize::write_simple emits it (serialize.rs:52-132)."""
+    values = np.ascontiguousarray(values)
+    opts = opts or WriteOptions.make()
+    vb = None
+    if validity is not None:
+        vb = np.packbits(np.asarray(validity, bool), bitorder="little")
+    buf = _Buf()
+    kind = 1 if values.dtype.kind == "f" else 0
+    rc = lib().orc_write_flat_page(
+        _ptr(values), _ptr(vb), len(values), kind, values.itemsize, int(values.dtype.kind == "i"), int(nullable), ctypes.byref(opts), ctypes.byref(buf)
+    )
+    data = _take(buf)
+    _check(rc, "write_page")
+    return data
+
+
+def read_page(page: bytes, num_values: int, dtype, nullable=False):
+    """IntegerIter / DoubleIter::deserialize on one page -> (values, validity|None)."""
+    dtype = np.dtype(dtype)
+    src = _bytes_arr(page)
+    out = np.zeros(max(num_values, 1), dtype)
+    bits = np.zeros((num_values + 7) // 8 + 1, np.uint8)
+    kind = 1 if dtype.kind == "f" else 0
+    rc = lib().orc_read_flat_page(_ptr(src), len(page), num_values, kind, dtype.itemsize, int(nullable), _ptr(out), _ptr(bits))
+    _check(rc, "read_page")
+    validity = np.unpackbits(bits, bitorder="little")[:num_values].astype(bool) if nullable else None
+    return out[:num_values], validity
+
+
+def roaring_encode(positions) -> bytes:
+    p = np.ascontiguousarray(positions, dtype=np.uint32)
+    buf = _Buf()
+    _check(lib().orc_roaring_encode(_ptr(p), len(p), ctypes.byref(buf)), "roaring_encode")
+    return _take(buf)
+
+
+def roaring_decode(data: bytes) -> np.ndarray:
+    src = _bytes_arr(data)
+    cnt = ctypes.c_size_t(0)
+    _check(lib().orc_roaring_decode(_ptr(src), len(data), None, 0, ctypes.byref(cnt)), "roaring_decode")
+    out = np.zeros(max(cnt.value, 1), np.uint32)
+    _check(lib().orc_roaring_decode(_ptr(src), len(data), _ptr(out), cnt.value, ctypes.byref(cnt)), "roaring_decode")
+    return out[: cnt.value]
+
+
+def hybrid_decode(data: bytes, bit_width: int, n: int) -> np.ndarray:
+    src = _bytes_arr(data)
+    out = np.zeros(max(n, 1), np.uint32)
+    _check(lib().orc_hybrid_decode(_ptr(src), len(data), bit_width, n, _ptr(out)), "hybrid_decode")
+    return out[:n]
+
+
+def common_compress(codec: int, data: bytes) -> bytes:
+    src = _bytes_arr(data)
+    buf = _Buf()
+    rc = lib().orc_common_compress(codec, _ptr(src), len(data), ctypes.byref(buf))
+    out = _take(buf)
+    _check(rc, "common_compress")
+    return out
+
+
+def common_decompress(codec: int, data: bytes, out_len: int) -> bytes:
+    src = _bytes_arr(data)
+    out = np.zeros(max(out_len, 1), np.uint8)
+    _check(lib().orc_common_decompress(codec, _ptr(src), len(data), _ptr(out), out_len), "common_decompress")
+    return out[:out_len].tobytes()
+
+
+def patas_pack(r, s, t) -> int:
+    return lib().orc_patas_pack(r, s, t)
+
+
+def patas_unpack(p: int):
+    a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    lib().orc_patas_unpack(p, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    return a.value, b.value, c.value
+
+
+def page_codec(page: bytes, nullable: bool) -> int:
+    """Codec byte of a flat page's value stream (after the validity prefix)."""
+    pos = 0
+    if nullable:
+        pos = 4 + int.from_bytes(page[:4], "little")
+    return page[pos]
