@@ -1,0 +1,161 @@
+/*
+ * strawboat_gpu.h -- C ABI of the MI355X strawboat page decode/encode engine.
+ *
+ * This is the drop-in boundary for the reference's codec path (b41sh/pa,
+ * crate strawboat 0.2.6).  Every entry point names the reference interface it
+ * replaces.  Plain pointers and sizes only; a Rust crate binds it 1:1
+ * (INTEGRATION.md shows the extern "C" block).
+ *
+ * Memory: "d_" pointers are device (HBM) pointers, "h_" pointers host memory.
+ * Calls are asynchronous on the context's HIP stream unless stated; sb_sync()
+ * waits.  Decode errors are per page (a status word written by the kernel) and
+ * are surfaced by sb_plan_status() / sb_decode_column(), never by aborting.
+ */
+#ifndef STRAWBOAT_GPU_H
+#define STRAWBOAT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error convention: arrow2::error::Error variants the reference returns
+ * (src/errors.rs:19-31; OutOfSpec for malformed pages e.g.
+ * compression/mod.rs:78-80, NotYetImplemented, Io for short reads, External
+ * for codec failures basic.rs:115-116).  Reference panics on malformed pages
+ * (array/integer.rs:81, read_basic.rs:59) map to SB_E_OUT_OF_SPEC here. */
+typedef enum {
+  SB_OK = 0,
+  SB_E_OUT_OF_SPEC = 1,
+  SB_E_NYI = 2,
+  SB_E_IO = 3,
+  SB_E_CODEC = 4,
+  SB_E_DEVICE = 5,
+  SB_E_ARG = 6,
+} sb_status;
+
+/* Codec ids of the 9-byte value-stream header (compression/mod.rs:64-82). */
+typedef enum {
+  SB_CODEC_NONE = 0,
+  SB_CODEC_LZ4 = 1,
+  SB_CODEC_ZSTD = 2,
+  SB_CODEC_SNAPPY = 3,
+  SB_CODEC_RLE = 10,
+  SB_CODEC_DICT = 11,
+  SB_CODEC_ONE_VALUE = 12,
+  SB_CODEC_FREQ = 13,
+  SB_CODEC_BITPACKING = 14,
+  SB_CODEC_DELTA_BITPACKING = 15,
+  SB_CODEC_PATAS = 16,
+} sb_codec;
+
+/* Arrow physical types handled by the page deserializers
+ * (read/deserialize.rs:100-135 dispatch). */
+typedef enum {
+  SB_T_INT8 = 1,
+  SB_T_INT16 = 2,
+  SB_T_INT32 = 3,
+  SB_T_INT64 = 4,
+  SB_T_UINT8 = 5,
+  SB_T_UINT16 = 6,
+  SB_T_UINT32 = 7,
+  SB_T_UINT64 = 8,
+  SB_T_FLOAT32 = 9,
+  SB_T_FLOAT64 = 10,
+} sb_physical_type;
+
+/* PageMeta (src/lib.rs:75-80): compressed page length and num_values. */
+typedef struct {
+  uint64_t length;
+  uint64_t num_values;
+} sb_page_meta;
+
+/* Leaf column descriptor: the parts of arrow2 Field + parquet2
+ * ColumnDescriptor the flat page readers use (array/integer.rs:28-60:
+ * is_nullable, data_type). */
+typedef struct {
+  int32_t physical_type; /* sb_physical_type */
+  int32_t nullable;      /* Field::is_nullable */
+} sb_column_desc;
+
+/* Output buffers of a primitive column (caller-allocated, device):
+ * values: sum(num_values) * sizeof(T) bytes;
+ * validity: 4*ceil(sum(num_values)/32) bytes (LSB-first Arrow bitmap, written
+ * as 32-bit words; bits past the last row are zero) or NULL when the column is
+ * not nullable.  Both 16-byte aligned for vector stores. */
+typedef struct {
+  void* d_values;
+  uint8_t* d_validity;
+} sb_primitive_out;
+
+typedef struct sb_ctx sb_ctx;
+typedef struct sb_plan sb_plan;
+
+/* ---- context ---------------------------------------------------------- */
+/* One context binds one device and one HIP stream; not thread-safe (the
+ * reference's readers are single-consumer iterators, read/reader.rs:51). */
+sb_status sb_ctx_create(int device, sb_ctx** out);
+void sb_ctx_destroy(sb_ctx* ctx);
+/* Launch on an external hipStream_t (e.g. torch.cuda.current_stream()).  The
+ * handle is used as given: NULL means the legacy default stream.  A fresh
+ * context uses a non-blocking stream of its own. */
+sb_status sb_ctx_set_stream(sb_ctx* ctx, void* hip_stream);
+void* sb_ctx_stream(sb_ctx* ctx);
+sb_status sb_sync(sb_ctx* ctx);
+const char* sb_last_error(const sb_ctx* ctx);
+const char* sb_status_str(int status);
+
+/* ---- column decode ----------------------------------------------------- */
+/* Builds the device page table for one leaf column chunk: the pages are the
+ * back-to-back page bytes starting at ColumnMeta.offset (d_chunk, chunk_len
+ * bytes, already in HBM), described by h_metas (ColumnMeta.pages).  Replaces
+ * the per-page NativeReader::next (read/reader.rs:119-131) walk; the row
+ * offsets are the running sum of num_values.  Uploads asynchronously. */
+sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk,
+                         uint64_t chunk_len, const sb_page_meta* h_metas, uint64_t n_pages,
+                         sb_plan** out);
+void sb_plan_destroy(sb_plan* plan);
+uint64_t sb_plan_num_rows(const sb_plan* plan);
+uint64_t sb_plan_num_pages(const sb_plan* plan);
+
+/* Launches the batched page decode of a planned column (asynchronous).
+ * Replaces read_integer / read_double (read/array/integer.rs:210-238,
+ * read/array/double.rs:210-238) as driven by batch_read_array
+ * (read/batch_read.rs:190-209): validity + values of every page, appended. */
+sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* plan, const sb_primitive_out* out);
+
+/* Waits for the plan's last decode and returns the first failing page's
+ * status (SB_OK if every page decoded); *h_bad_page = its index or -1. */
+sb_status sb_plan_status(sb_ctx* ctx, sb_plan* plan, int64_t* h_bad_page);
+
+/* One-shot: plan + decode + wait + status.  The batch_read_array
+ * equivalent for one flat primitive leaf. */
+sb_status sb_decode_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk,
+                           uint64_t chunk_len, const sb_page_meta* h_metas, uint64_t n_pages,
+                           const sb_primitive_out* out);
+
+/* Device kernel time of the plan's last decode, in milliseconds (HIP events
+ * recorded on the launch stream around the decode kernels). */
+sb_status sb_plan_last_kernel_ms(sb_ctx* ctx, sb_plan* plan, float* ms);
+
+/* ---- value-stream level (unit parity) ---------------------------------- */
+/* decompress_integer / decompress_double for ONE page's values, no validity
+ * prefix (compression/integer/mod.rs:72-117, double/mod.rs:69-114):
+ * d_stream = [codec][csize][usize][body], length values out. Synchronous. */
+sb_status sb_decompress_values(sb_ctx* ctx, int32_t physical_type, const uint8_t* d_stream,
+                               uint64_t stream_len, uint64_t length, void* d_out);
+
+/* ---- host-side format helpers ------------------------------------------ */
+/* read_meta (read/reader.rs:148-178) over the tail of a file held in host
+ * memory: fills up to cap column metas.  Returns the number of columns in
+ * *n_cols; pages of column i are written to h_pages[page_start[i]..]. */
+sb_status sb_read_meta(const uint8_t* h_file, uint64_t file_len, uint64_t* h_col_offsets,
+                       uint64_t* h_col_page_start, uint64_t cols_cap, sb_page_meta* h_pages,
+                       uint64_t pages_cap, uint64_t* n_cols, uint64_t* n_pages);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,15 @@
+"""pa_amd: MI355X-native page encode/decode engine for the strawboat format
+(drop-in for the codec path of b41sh/pa).  See DESIGN.md."""
+from ._native import StrawboatError, build, lib  # noqa: F401
+from .read import (  # noqa: F401
+    ColumnDecoder,
+    ColumnMeta,
+    Context,
+    NativeReader,
+    PageMeta,
+    batch_read_array,
+    column_iter_to_arrays,
+    default_context,
+    read_meta,
+    unpack_bitmap,
+)

@@ -1,0 +1,322 @@
+// sb_api.cpp -- host side of the C ABI (include/strawboat_gpu.h).
+//
+// Plays the role of the reference's NativeReader + read_* drivers
+// (read/reader.rs:51-146, read/array/integer.rs:210-238): it turns
+// ColumnMeta.pages into a device page table and launches the batched page
+// kernels on the context's HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/strawboat_gpu.h"
+#include "sb_internal.h"
+
+struct sb_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+};
+
+struct sb_plan {
+  sb_column_desc desc{};
+  const uint8_t* d_chunk = nullptr;
+  uint64_t chunk_len = 0;
+  uint64_t n_pages = 0, n_rows = 0;
+  int width = 0;
+  bool is_float = false;
+  sb::PageDesc* d_pages = nullptr;
+  uint32_t* d_status = nullptr;
+  uint32_t* d_lists = nullptr;  // [staged list | global list]
+  uint32_t n_staged = 0, n_global = 0;
+  bool staged_identity = false;  // every page staged: no index list
+  uint32_t stage_bytes = 0;
+  bool validity_needs_zero = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+};
+
+static sb_status fail(sb_ctx* ctx, sb_status st, const char* fmt, ...) {
+  if (ctx) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    ctx->err = buf;
+  }
+  return st;
+}
+
+#define HIP_TRY(ctx, expr)                                                                  \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return fail(ctx, SB_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+static int type_width(int t, bool* is_float) {
+  *is_float = false;
+  switch (t) {
+    case SB_T_INT8: case SB_T_UINT8: return 1;
+    case SB_T_INT16: case SB_T_UINT16: return 2;
+    case SB_T_INT32: case SB_T_UINT32: return 4;
+    case SB_T_INT64: case SB_T_UINT64: return 8;
+    case SB_T_FLOAT32: *is_float = true; return 4;
+    case SB_T_FLOAT64: *is_float = true; return 8;
+  }
+  return 0;
+}
+
+extern "C" {
+
+const char* sb_status_str(int st) {
+  switch (st) {
+    case SB_OK: return "ok";
+    case SB_E_OUT_OF_SPEC: return "out of spec";
+    case SB_E_NYI: return "not yet implemented";
+    case SB_E_IO: return "io (short read)";
+    case SB_E_CODEC: return "codec error";
+    case SB_E_DEVICE: return "device error";
+    case SB_E_ARG: return "invalid argument";
+  }
+  return "unknown";
+}
+
+sb_status sb_ctx_create(int device, sb_ctx** out) {
+  if (!out) return SB_E_ARG;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return SB_E_DEVICE;
+  if (device < 0 || device >= n) return SB_E_ARG;
+  sb_ctx* c = new sb_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SB_E_DEVICE;
+  }
+  c->stream = c->own;
+  *out = c;
+  return SB_OK;
+}
+
+void sb_ctx_destroy(sb_ctx* ctx) {
+  if (!ctx) return;
+  if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  delete ctx;
+}
+
+sb_status sb_ctx_set_stream(sb_ctx* ctx, void* s) {
+  if (!ctx) return SB_E_ARG;
+  ctx->stream = (hipStream_t)s;  // taken literally: NULL is the legacy default stream
+  return SB_OK;
+}
+
+void* sb_ctx_stream(sb_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+sb_status sb_sync(sb_ctx* ctx) {
+  if (!ctx) return SB_E_ARG;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return SB_OK;
+}
+
+const char* sb_last_error(const sb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void sb_plan_destroy(sb_plan* p) {
+  if (!p) return;
+  if (p->d_pages) (void)hipFree(p->d_pages);
+  if (p->d_status) (void)hipFree(p->d_status);
+  if (p->d_lists) (void)hipFree(p->d_lists);
+  if (p->ev0) (void)hipEventDestroy(p->ev0);
+  if (p->ev1) (void)hipEventDestroy(p->ev1);
+  delete p;
+}
+
+uint64_t sb_plan_num_rows(const sb_plan* p) { return p ? p->n_rows : 0; }
+uint64_t sb_plan_num_pages(const sb_plan* p) { return p ? p->n_pages : 0; }
+
+sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                         const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out) {
+  if (!ctx || !desc || !out || (!h_metas && n_pages)) return fail(ctx, SB_E_ARG, "null argument");
+  bool is_float;
+  int width = type_width(desc->physical_type, &is_float);
+  if (!width) return fail(ctx, SB_E_NYI, "physical type %d not supported", desc->physical_type);
+  if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+
+  std::vector<sb::PageDesc> pages(n_pages);
+  std::vector<uint32_t> staged, global;
+  uint64_t off = 0, rows = 0;
+  uint32_t max_stage = 0;
+  bool needs_zero = false;
+  for (uint64_t i = 0; i < n_pages; i++) {
+    const sb_page_meta& m = h_metas[i];
+    if (m.length > 0xFFFFFFFFull || m.num_values > 0xFFFFFFFFull)
+      return fail(ctx, SB_E_ARG, "page %llu exceeds u32 sizes", (unsigned long long)i);
+    if (off + m.length > chunk_len)
+      return fail(ctx, SB_E_ARG, "page %llu overruns the column chunk", (unsigned long long)i);
+    pages[i] = sb::PageDesc{off, rows, (uint32_t)m.length, (uint32_t)m.num_values, 0};
+    // a 32-bit validity word shared by two pages is merged with atomics
+    if ((rows & 31) || (m.num_values & 31)) needs_zero = true;
+    if (m.length + 16 <= sb::kStageMaxBytes) {
+      staged.push_back((uint32_t)i);
+      max_stage = std::max<uint32_t>(max_stage, (uint32_t)m.length);
+    } else {
+      global.push_back((uint32_t)i);
+    }
+    off += m.length;
+    rows += m.num_values;
+  }
+
+  sb_plan* p = new sb_plan();
+  p->desc = *desc;
+  p->d_chunk = d_chunk;
+  p->chunk_len = chunk_len;
+  p->n_pages = n_pages;
+  p->n_rows = rows;
+  p->width = width;
+  p->is_float = is_float;
+  p->n_staged = (uint32_t)staged.size();
+  p->n_global = (uint32_t)global.size();
+  p->staged_identity = global.empty();
+  p->stage_bytes = ((max_stage + 16 + 15) & ~15u) + sb::kStagePad;
+  p->validity_needs_zero = needs_zero;
+  size_t np = n_pages ? n_pages : 1;
+  hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
+  if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&p->d_lists, np * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipEventCreate(&p->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&p->ev1);
+  if (e == hipSuccess && n_pages) {
+    std::vector<uint32_t> lists(staged);
+    lists.insert(lists.end(), global.begin(), global.end());
+    e = hipMemcpyAsync(p->d_pages, pages.data(), n_pages * sizeof(sb::PageDesc), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(p->d_lists, lists.data(), n_pages * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(p->d_status, 0, n_pages * sizeof(uint32_t), ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);  // host vectors go out of scope
+  }
+  if (e != hipSuccess) {
+    sb_plan_destroy(p);
+    return fail(ctx, SB_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
+  }
+  *out = p;
+  return SB_OK;
+}
+
+sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out) {
+  if (!ctx || !p || !out) return fail(ctx, SB_E_ARG, "null argument");
+  if (p->n_rows && !out->d_values) return fail(ctx, SB_E_ARG, "values buffer is null");
+  if (p->desc.nullable && p->n_rows && !out->d_validity) return fail(ctx, SB_E_ARG, "validity buffer is null");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (p->desc.nullable && p->validity_needs_zero)
+    HIP_TRY(ctx, hipMemsetAsync(out->d_validity, 0, (p->n_rows + 31) / 32 * 4, ctx->stream));
+  HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
+  sb::LaunchArgs a{};
+  a.chunk = p->d_chunk;
+  a.pages = p->d_pages;
+  a.out_values = (uint8_t*)out->d_values;
+  a.out_validity = (uint32_t*)out->d_validity;
+  a.nullable = p->desc.nullable;
+  a.status = p->d_status;
+  a.stage_bytes = p->stage_bytes;
+  a.list = p->staged_identity ? nullptr : p->d_lists;
+  a.n_list = p->n_staged;
+  if (sb::launch_decode_fixed(p->width, p->is_float, true, a, ctx->stream))
+    return fail(ctx, SB_E_DEVICE, "staged decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  a.list = p->d_lists + p->n_staged;
+  a.n_list = p->n_global;
+  if (sb::launch_decode_fixed(p->width, p->is_float, false, a, ctx->stream))
+    return fail(ctx, SB_E_DEVICE, "global decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
+  p->timed = true;
+  return SB_OK;
+}
+
+sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
+  if (!ctx || !p) return fail(ctx, SB_E_ARG, "null argument");
+  if (bad) *bad = -1;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (!p->n_pages) return SB_OK;
+  std::vector<uint32_t> st(p->n_pages);
+  HIP_TRY(ctx, hipMemcpy(st.data(), p->d_status, p->n_pages * 4, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < p->n_pages; i++) {
+    if (st[i]) {
+      if (bad) *bad = (int64_t)i;
+      return fail(ctx, (sb_status)st[i], "page %llu: %s", (unsigned long long)i, sb_status_str((int)st[i]));
+    }
+  }
+  return SB_OK;
+}
+
+sb_status sb_plan_last_kernel_ms(sb_ctx* ctx, sb_plan* p, float* ms) {
+  if (!ctx || !p || !ms || !p->timed) return fail(ctx, SB_E_ARG, "no timed decode");
+  HIP_TRY(ctx, hipEventSynchronize(p->ev1));
+  HIP_TRY(ctx, hipEventElapsedTime(ms, p->ev0, p->ev1));
+  return SB_OK;
+}
+
+sb_status sb_decode_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                           const sb_page_meta* h_metas, uint64_t n_pages, const sb_primitive_out* out) {
+  sb_plan* p = nullptr;
+  sb_status st = sb_plan_column(ctx, desc, d_chunk, chunk_len, h_metas, n_pages, &p);
+  if (st) return st;
+  st = sb_decode_planned(ctx, p, out);
+  if (!st) st = sb_plan_status(ctx, p, nullptr);
+  sb_plan_destroy(p);
+  return st;
+}
+
+sb_status sb_decompress_values(sb_ctx* ctx, int32_t physical_type, const uint8_t* d_stream, uint64_t stream_len,
+                               uint64_t length, void* d_out) {
+  // one non-nullable page whose bytes are exactly the value stream
+  sb_column_desc d{physical_type, 0};
+  sb_page_meta m{stream_len, length};
+  sb_primitive_out o{d_out, nullptr};
+  return sb_decode_column(ctx, &d, d_stream, stream_len, &m, 1, &o);
+}
+
+// read_meta (read/reader.rs:148-178): footer = ... meta | u32 schema_size |
+// u32 meta_size | FF FF FF FF 00 00 00 00; meta = u64 n_cols, per column
+// (u64 offset, u64 n_pages, n_pages * (u64 length, u64 num_values)).
+sb_status sb_read_meta(const uint8_t* f, uint64_t flen, uint64_t* col_off, uint64_t* col_start, uint64_t cols_cap,
+                       sb_page_meta* pages, uint64_t pages_cap, uint64_t* n_cols, uint64_t* n_pages) {
+  if (!f || !n_cols || !n_pages || flen < 16) return SB_E_ARG;
+  uint32_t meta_size;
+  memcpy(&meta_size, f + flen - 12, 4);
+  if ((uint64_t)meta_size + 16 > flen) return SB_E_OUT_OF_SPEC;
+  const uint8_t* m = f + flen - 16 - meta_size;
+  uint64_t pos = 0;
+  auto rd = [&](uint64_t* v) {
+    if (pos + 8 > meta_size) return false;
+    memcpy(v, m + pos, 8);
+    pos += 8;
+    return true;
+  };
+  uint64_t nc;
+  if (!rd(&nc)) return SB_E_IO;
+  uint64_t total = 0;
+  for (uint64_t c = 0; c < nc; c++) {
+    uint64_t off, np;
+    if (!rd(&off) || !rd(&np)) return SB_E_IO;
+    if (c < cols_cap) {
+      if (col_off) col_off[c] = off;
+      if (col_start) col_start[c] = total;
+    }
+    for (uint64_t i = 0; i < np; i++) {
+      uint64_t len, nv;
+      if (!rd(&len) || !rd(&nv)) return SB_E_IO;
+      if (pages && total < pages_cap) pages[total] = sb_page_meta{len, nv};
+      total++;
+    }
+  }
+  *n_cols = nc;
+  *n_pages = total;
+  return SB_OK;
+}
+
+}  // extern "C"

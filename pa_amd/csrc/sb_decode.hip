@@ -1,0 +1,760 @@
+// sb_decode.hip -- batched page decode of fixed-width strawboat columns on
+// MI355X (gfx950).
+//
+// One 256-thread workgroup decodes one page: the page bytes are staged into
+// LDS with 16-byte loads, the validity prefix and the value stream header are
+// parsed from LDS, and the codec body is expanded straight into the Arrow
+// buffers in HBM.  Restates, per page:
+//   IntegerIter::deserialize / read_integer   read/array/integer.rs:68-88, 210-238
+//   DoubleIter::deserialize / read_double     read/array/double.rs:68-88, 210-238
+//   read_validity                             read/read_basic.rs:36-63
+//   decompress_integer / decompress_double    compression/integer/mod.rs:72-117,
+//                                             compression/double/mod.rs:69-114
+//   Bitpacking / DeltaBitpacking              compression/integer/bp.rs:67-86,
+//                                             compression/integer/delta_bp.rs:69-92
+//   RLE                                       compression/integer/rle.rs:106-134
+//   OneValue                                  compression/integer/one_value.rs:77-94
+//   Dict                                      compression/integer/dict.rs:75-103
+//   Freq                                      compression/integer/freq.rs:88-123
+// Integer/byte work only: no MFMA.  Bound: HBM bandwidth.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sb_internal.h"
+
+namespace sbk {
+
+using namespace sb;
+
+constexpr int NT = 256;
+constexpr int NW = NT / 64;
+constexpr uint32_t kWinBlocks = 64;  // bitpack blocks per header walk window
+constexpr uint32_t kMaxConts = 16;   // roaring containers handled per page
+constexpr uint32_t kMaxBitmapConts = 4;  // of which bitmap containers (card > 4096)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int W> struct VT { using T = uint32_t; };
+template <> struct VT<8> { using T = uint64_t; };
+
+// ---------------------------------------------------------------------------
+// byte sources
+// ---------------------------------------------------------------------------
+// Page staged in LDS at byte `base` of the dynamic LDS words.  The staging
+// buffer carries kStagePad bytes of slack so word-granular over-reads are safe.
+struct LdsSrc {
+  const uint32_t* w;
+  uint32_t base;
+  __device__ __forceinline__ uint32_t u8(uint32_t p) const {
+    p += base;
+    return (w[p >> 2] >> ((p & 3) * 8)) & 0xFFu;
+  }
+  __device__ __forceinline__ uint32_t u32(uint32_t p) const {
+    p += base;
+    uint32_t i = p >> 2;
+    return __builtin_amdgcn_alignbyte(w[i + 1], w[i], p & 3);
+  }
+  __device__ __forceinline__ uint64_t u64(uint32_t p) const {
+    p += base;
+    uint32_t i = p >> 2, sh = p & 3;
+    uint32_t a = w[i], b = w[i + 1], c = w[i + 2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(b, a, sh) |
+           ((uint64_t)__builtin_amdgcn_alignbyte(c, b, sh) << 32);
+  }
+  // the 4 lane words at p and (if need_hi) the 4 at p + 16, unaligned
+  __device__ __forceinline__ void quad_words(uint32_t p, bool need_hi, uint32_t* d8) const {
+    p += base;
+    uint32_t i = p >> 2, sh = p & 3;
+    uint32_t d[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) d[k] = w[i + k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) d8[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+  }
+};
+
+// Page read straight from HBM (pages larger than the LDS stage).  Unaligned
+// words are assembled from the aligned dwords that contain them, so no read
+// leaves the bytes the page owns.
+struct GlbSrc {
+  const uint8_t* p;
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
+  __device__ __forceinline__ uint32_t u32(uint32_t i) const {
+    uintptr_t a = (uintptr_t)(p + i);
+    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    uint32_t sh = (uint32_t)(a & 3);
+    if (sh == 0) return q[0];
+    return __builtin_amdgcn_alignbyte(q[1], q[0], sh);
+  }
+  __device__ __forceinline__ uint64_t u64(uint32_t i) const {
+    return (uint64_t)u32(i) | ((uint64_t)u32(i + 4) << 32);
+  }
+  __device__ __forceinline__ void quad_words(uint32_t pos, bool need_hi, uint32_t* d8) const {
+#pragma unroll
+    for (int k = 0; k < 4; k++) d8[k] = u32(pos + 4 * k);
+    if (need_hi) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) d8[4 + k] = u32(pos + 16 + 4 * k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) d8[4 + k] = 0;
+    }
+  }
+};
+
+template <int W, class Src>
+__device__ __forceinline__ typename VT<W>::T ldv(const Src& s, uint32_t p) {
+  if constexpr (W == 8) return s.u64(p);
+  else if constexpr (W == 4) return s.u32(p);
+  else if constexpr (W == 2) return s.u32(p) & 0xFFFFu;
+  else return s.u8(p);
+}
+
+// ---------------------------------------------------------------------------
+// per-workgroup shared state
+// ---------------------------------------------------------------------------
+struct Stream {
+  uint32_t codec, body, csize, n;
+};
+
+struct Shared {
+  uint32_t err;
+  uint32_t walk_off;
+  uint32_t blk_off[kWinBlocks];
+  uint32_t blk_bits[kWinBlocks];
+  uint64_t wsum[NW];
+  uint32_t rle_start[NT + 1];
+  uint32_t rle_c;
+  uint32_t rle_R;
+  uint32_t rle_flags;  // bit0 = a run ends exactly at n, bit1 = a run overshoots n
+  // page header
+  uint32_t has_valid, vb_pos, vb_bytes;
+  Stream top;
+  Stream sub;  // the leaf stream at the bottom of the cascade
+  uint32_t chain;
+  // Dict
+  uint32_t dict_k, dict_off;
+  // Freq
+  uint64_t freq_top;
+  uint32_t n_conts;
+  uint32_t cont_key[kMaxConts];
+  uint32_t cont_data[kMaxConts];
+  uint32_t cont_prefix[kMaxConts + 1];
+  uint32_t cont_bm[kMaxConts];            // index into cont_cp, or ~0u for array containers
+  uint16_t cont_cp[kMaxBitmapConts][64];  // set bits before each 16-word group
+};
+
+__device__ __forceinline__ void set_err(Shared& sh, uint32_t code) { atomicMax(&sh.err, code); }
+
+// Block-wide exclusive scan (sum) of one value per thread; *total = block sum.
+template <class T>
+__device__ __forceinline__ T block_excl_scan(T v, Shared& sh, T* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    T y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) sh.wsum[wv] = (uint64_t)x;
+  __syncthreads();
+  T pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    T s = (T)sh.wsum[k];
+    if (k < wv) pre += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+// ---------------------------------------------------------------------------
+// output sinks
+// ---------------------------------------------------------------------------
+template <int W>
+struct GSink {
+  uint8_t* base;  // page row 0
+  bool vec;       // page row 0 is 4*W aligned: quads store as one vector
+  using T = typename VT<W>::T;
+  __device__ __forceinline__ void put(uint32_t row, T v) const {
+    if constexpr (W == 8) ((uint64_t*)base)[row] = v;
+    else if constexpr (W == 4) ((uint32_t*)base)[row] = v;
+    else if constexpr (W == 2) ((uint16_t*)base)[row] = (uint16_t)v;
+    else base[row] = (uint8_t)v;
+  }
+  __device__ __forceinline__ void put4(uint32_t row, const T* v, uint32_t nvalid) const {
+    if (nvalid == 4 && vec) {
+      if constexpr (W == 8) {
+        uint4* p = (uint4*)(base + (size_t)row * 8);
+        p[0] = make_uint4((uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32));
+        p[1] = make_uint4((uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32));
+      } else if constexpr (W == 4) {
+        *(uint4*)(base + (size_t)row * 4) = make_uint4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (W == 2) {
+        *(uint2*)(base + (size_t)row * 2) = make_uint2((v[0] & 0xFFFF) | (v[1] << 16), (v[2] & 0xFFFF) | (v[3] << 16));
+      } else {
+        *(uint32_t*)(base + row) = (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | (v[3] << 24);
+      }
+    } else {
+      for (uint32_t l = 0; l < nvalid; l++) put(row + l, v[l]);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Bitpacking (BitPacker4x layout, bitpacking 0.8.0): header walk
+// ---------------------------------------------------------------------------
+// Block k of a stream is [u8 b][16*b bytes]; its header offset depends on
+// every earlier b.  Wave 0 walks `cnt` headers speculatively: lane j guesses
+// block (done + j) sits (j * (1 + 16*b0)) bytes on, i.e. that b stays b0.
+// The first lane that reads a different b ends the confirmed prefix (its own
+// offset is still right); the next round restarts there.  Constant-width
+// pages need one round per 64 blocks; the worst case is one block per round.
+template <class Src>
+__device__ void bp_walk(const Src& s, Shared& sh, uint32_t end, uint32_t cnt) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t off = sh.walk_off, done = 0;
+  while (done < cnt) {
+    if (off >= end) { if (lane == 0) set_err(sh, ST_IO); return; }
+    uint32_t b0 = s.u8(off);
+    if (b0 > 32) { if (lane == 0) set_err(sh, ST_OUT_OF_SPEC); return; }
+    uint32_t step = 1 + 16 * b0;
+    uint32_t k = done + lane;
+    uint32_t g = off + lane * step;
+    bool inb = k < cnt;
+    uint32_t bj = (inb && g < end) ? s.u8(g) : 0xFFFFFFFFu;
+    unsigned long long mism = __ballot(inb && bj != b0);
+    uint32_t m = mism ? (uint32_t)__builtin_ctzll(mism) : min(64u, cnt - done);
+    if (lane < m) {
+      sh.blk_off[k] = g + 1;
+      sh.blk_bits[k] = b0;
+    }
+    done += m;
+    off += m * step;
+  }
+  if (off > end) { if (lane == 0) set_err(sh, ST_IO); return; }
+  if (lane == 0) sh.walk_off = off;
+}
+
+// 4 values of quad i of a block whose payload starts at P with width b.
+template <class Src>
+__device__ __forceinline__ void bp_quad(const Src& s, uint32_t P, uint32_t b, uint32_t i, uint32_t* v) {
+  if (b == 0) { v[0] = v[1] = v[2] = v[3] = 0; return; }
+  uint32_t bit = i * b, w = bit >> 5, sft = bit & 31;
+  uint32_t mask = b == 32 ? 0xFFFFFFFFu : ((1u << b) - 1);
+  uint32_t d[8];
+  s.quad_words(P + 16 * w, sft + b > 32, d);
+#pragma unroll
+  for (int l = 0; l < 4; l++) v[l] = __builtin_amdgcn_alignbit(d[4 + l], d[l], sft) & mask;
+}
+
+// ---------------------------------------------------------------------------
+// RLE: runs of (u32 count, T value)
+// ---------------------------------------------------------------------------
+// Preparation: thread t owns runs [t*c, (t+1)*c); an exclusive scan of the
+// per-thread count sums gives each thread chunk's first row.  Validity
+// follows rle.rs:115-132: decoding stops at the first run whose end reaches
+// n; it must land exactly on n (array/integer.rs:81 assert).
+template <int SW, class Src>
+__device__ void rle_prepare(const Src& s, Shared& sh, const Stream& st) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t runsz = 4 + SW;
+  const uint32_t R = st.csize / runsz;
+  const uint32_t c = (R + NT - 1) / NT;
+  uint32_t r0 = min(R, tid * c), r1 = min(R, r0 + c);
+  uint64_t sum = 0;
+  for (uint32_t r = r0; r < r1; r++) sum += s.u32(st.body + r * runsz);
+  uint64_t tot;
+  uint64_t start = block_excl_scan<uint64_t>(sum, sh, &tot);
+  uint32_t flags = 0;
+  uint64_t acc = start;
+  if (start < st.n) {
+    for (uint32_t r = r0; r < r1; r++) {
+      uint64_t b = acc;
+      acc += s.u32(st.body + r * runsz);
+      if (b < st.n && acc == st.n) flags |= 1;
+      if (b < st.n && acc > st.n) flags |= 2;
+      if (acc >= st.n) break;
+    }
+  }
+  sh.rle_start[tid] = (uint32_t)min<uint64_t>(start, 0xFFFFFFFFull);
+  if (tid == 0) {
+    sh.rle_start[NT] = (uint32_t)min<uint64_t>(tot, 0xFFFFFFFFull);
+    sh.rle_c = c;
+    sh.rle_R = R;
+    sh.rle_flags = 0;
+  }
+  __syncthreads();
+  if (flags) atomicOr(&sh.rle_flags, flags);
+  __syncthreads();
+  if (tid == 0 && st.n > 0) {
+    uint32_t f = sh.rle_flags;
+    if ((f & 2) || !(f & 1)) set_err(sh, (f & 2) ? ST_OUT_OF_SPEC : ST_IO);
+  }
+  __syncthreads();
+}
+
+// Run containing row `row` (row < n): binary search over the thread-chunk
+// starts, then a linear walk inside the chunk.  Returns run index and fills
+// [rs, re) = its row span.
+template <int SW, class Src>
+__device__ __forceinline__ uint32_t rle_find(const Src& s, const Shared& sh, const Stream& st, uint32_t row,
+                                             uint32_t* rs, uint32_t* re) {
+  uint32_t lo = 0, hi = NT;  // largest t with rle_start[t] <= row
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (sh.rle_start[mid] <= row) lo = mid; else hi = mid;
+  }
+  const uint32_t runsz = 4 + SW;
+  uint32_t r = lo * sh.rle_c;
+  uint32_t acc = sh.rle_start[lo];
+  for (;;) {
+    uint32_t cnt = s.u32(st.body + r * runsz);
+    if (row < acc + cnt || r + 1 >= sh.rle_R) { *rs = acc; *re = acc + cnt; return r; }
+    acc += cnt;
+    r++;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Stream driver: expands one leaf value stream (None, OneValue, RLE,
+// Bitpacking, DeltaBitpacking) of n values of width SW and hands every quad
+// of consecutive values to fn(first_index, v[4], nvalid).  All threads of the
+// workgroup call this uniformly.  Dict and Freq are handled one level up.
+// ---------------------------------------------------------------------------
+template <int SW, class Src, class Fn>
+__device__ void run_leaf(const Src& s, Shared& sh, const Stream st, Fn&& fn) {
+  using T = typename VT<SW>::T;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nq = (st.n + 3) >> 2;
+  switch (st.codec) {
+    case 0: {  // None: raw LE values (basic.rs:68-71 copy_from_slice)
+      if (st.csize != st.n * SW) { if (tid == 0) set_err(sh, ST_OUT_OF_SPEC); return; }
+      for (uint32_t q = tid; q < nq; q += NT) {
+        T v[4];
+        uint32_t nv = min(4u, st.n - 4 * q);
+#pragma unroll
+        for (uint32_t l = 0; l < 4; l++) v[l] = l < nv ? ldv<SW>(s, st.body + (4 * q + l) * SW) : (T)0;
+        fn(4 * q, v, nv);
+      }
+      return;
+    }
+    case 12: {  // OneValue
+      if (st.csize < SW) { if (tid == 0) set_err(sh, ST_IO); return; }
+      T x = ldv<SW>(s, st.body);
+      for (uint32_t q = tid; q < nq; q += NT) {
+        T v[4] = {x, x, x, x};
+        fn(4 * q, v, min(4u, st.n - 4 * q));
+      }
+      return;
+    }
+    case 10: {  // RLE
+      rle_prepare<SW>(s, sh, st);
+      if (sh.err) return;
+      const uint32_t runsz = 4 + SW;
+      for (uint32_t q = tid; q < nq; q += NT) {
+        uint32_t row = 4 * q, nv = min(4u, st.n - row);
+        uint32_t rs, re;
+        uint32_t r = rle_find<SW>(s, sh, st, row, &rs, &re);
+        T x = ldv<SW>(s, st.body + r * runsz + 4);
+        T v[4];
+#pragma unroll
+        for (uint32_t l = 0; l < 4; l++) {
+          if (l < nv && row + l >= re) {
+            // advance to the run covering row + l (zero-count runs skipped)
+            do {
+              r++;
+              rs = re;
+              re = rs + s.u32(st.body + r * runsz);
+            } while (row + l >= re && r + 1 < sh.rle_R);
+            x = ldv<SW>(s, st.body + r * runsz + 4);
+          }
+          v[l] = x;
+        }
+        fn(row, v, nv);
+      }
+      return;
+    }
+    case 14:
+    case 15: {  // Bitpacking / DeltaBitpacking (T must be 4 bytes, n % 128 == 0)
+      if (SW != 4 || (st.n & 127)) { if (tid == 0) set_err(sh, ST_OUT_OF_SPEC); return; }
+      const bool delta = st.codec == 15;
+      const uint32_t nblk = st.n >> 7;
+      const uint32_t end = st.body + st.csize;
+      if (tid == 0) sh.walk_off = st.body;
+      __syncthreads();
+      uint32_t carry = 0;
+      for (uint32_t kb = 0; kb < nblk; kb += kWinBlocks) {
+        const uint32_t cnt = min(kWinBlocks, nblk - kb);
+        if (tid < 64) bp_walk(s, sh, end, cnt);
+        __syncthreads();
+        if (sh.err) return;
+        const uint32_t nqw = cnt * 32;
+        for (uint32_t j = 0; j < (nqw + NT - 1) / NT; j++) {
+          const uint32_t q = j * NT + tid;
+          uint32_t v[4] = {0, 0, 0, 0};
+          const bool act = q < nqw;
+          if (act) bp_quad(s, sh.blk_off[q >> 5], sh.blk_bits[q >> 5], q & 31, v);
+          if (delta) {
+            // wrapping inclusive prefix over the whole page (delta_bp.rs:76-90:
+            // each block starts from the previous block's last value)
+            v[1] += v[0];
+            v[2] += v[1];
+            v[3] += v[2];
+            uint32_t tot;
+            uint32_t pre = block_excl_scan<uint32_t>(act ? v[3] : 0u, sh, &tot) + carry;
+#pragma unroll
+            for (int l = 0; l < 4; l++) v[l] += pre;
+            carry += tot;
+          }
+          if (act) {
+            T tv[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+            fn(kb * 128 + 4 * q, tv, 4u);
+          }
+        }
+        __syncthreads();
+      }
+      return;
+    }
+    case 1:
+    case 2:
+    case 3:   // LZ4 / Zstd / Snappy general codecs: not yet on device
+    case 11:  // Dict / Freq nested below another Dict / Freq
+    case 13:
+    case 16:  // Patas (float streams)
+      if (tid == 0) set_err(sh, ST_NYI);
+      return;
+    default:
+      if (tid == 0) set_err(sh, ST_OUT_OF_SPEC);
+      return;
+  }
+}
+
+// Parse a nested [codec][csize][usize] header at p (bounded by end).
+template <class Src>
+__device__ bool parse_stream(const Src& s, uint32_t p, uint32_t end, uint32_t n, Stream* st) {
+  if (p + 9 > end) return false;
+  st->codec = s.u8(p);
+  st->csize = s.u32(p + 1);
+  st->body = p + 9;
+  st->n = n;
+  return st->csize <= end - st->body;
+}
+
+// Roaring select: row of exception i.  Array containers index directly;
+// bitmap containers find the 16-word group by its checkpoint, then the word by
+// popcounts, then the bit.
+template <class Src>
+__device__ __forceinline__ uint32_t roaring_select(const Src& s, const Shared& sh, uint32_t i) {
+  uint32_t c = 0;
+  while (c + 1 < sh.n_conts && sh.cont_prefix[c + 1] <= i) c++;
+  uint32_t j = i - sh.cont_prefix[c];
+  const uint32_t bmi = sh.cont_bm[c];
+  if (bmi == ~0u) return (sh.cont_key[c] << 16) | (s.u32(sh.cont_data[c] + 2 * j) & 0xFFFFu);
+  uint32_t g = 0;
+  for (uint32_t step = 32; step; step >>= 1)
+    if (g + step < 64 && sh.cont_cp[bmi][g + step] <= j) g += step;
+  j -= sh.cont_cp[bmi][g];
+  uint32_t w = 16 * g;
+  uint64_t word = s.u64(sh.cont_data[c] + 8 * w);
+  for (uint32_t pc = __popcll(word); pc <= j && w + 1 < 1024; pc = __popcll(word)) {
+    j -= pc;
+    word = s.u64(sh.cont_data[c] + 8 * (++w));
+  }
+  for (uint32_t t = 0; t < j; t++) word &= word - 1;  // drop the j lowest set bits
+  return (sh.cont_key[c] << 16) | (w * 64 + (uint32_t)__builtin_ctzll(word));
+}
+
+// ---------------------------------------------------------------------------
+// validity: copy the page's def-level bitmap to bit offset row_off
+// ---------------------------------------------------------------------------
+template <class Src>
+__device__ void write_validity(const Src& s, uint32_t vb, uint32_t n, uint64_t row_off, uint32_t* out) {
+  if (n == 0) return;
+  const uint64_t fw = row_off >> 5, lw = (row_off + n - 1) >> 5;
+  for (uint64_t w = fw + threadIdx.x; w <= lw; w += NT) {
+    int64_t pb = (int64_t)(w * 32) - (int64_t)row_off;  // page bit of word bit 0
+    uint32_t v;
+    if (pb >= 0) v = (uint32_t)(s.u64(vb + (uint32_t)(pb >> 3)) >> (pb & 7));
+    else v = s.u32(vb) << (uint32_t)(-pb);
+    // keep word bits k with 0 <= pb + k < n
+    uint32_t lo = pb < 0 ? (uint32_t)(-pb) : 0u;
+    int64_t hi_ex = (int64_t)n - pb;  // word bits < hi_ex are inside the page
+    uint32_t hi = hi_ex >= 32 ? 32u : (uint32_t)hi_ex;
+    uint32_t m = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1)) & (0xFFFFFFFFu << lo);
+    if (m == 0xFFFFFFFFu) out[w] = v;
+    else atomicOr(&out[w], v & m);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// the page kernel
+// ---------------------------------------------------------------------------
+// Parses a Freq body [T top][u32 bm][roaring][exceptions stream] whose value
+// width is `vw` (integer/freq.rs:88-123).  Thread 0 only.
+template <class Src>
+__device__ bool parse_freq(const Src& s, Shared& sh, const Stream& st, uint32_t vw, Stream* ex) {
+  const uint32_t e = st.body + st.csize;
+  if (st.body + vw + 4 > e) { set_err(sh, ST_IO); return false; }
+  sh.freq_top = vw == 8 ? s.u64(st.body) : vw == 4 ? s.u32(st.body) : vw == 2 ? (s.u32(st.body) & 0xFFFFu) : s.u8(st.body);
+  const uint32_t bm = s.u32(st.body + vw), r = st.body + vw + 4;
+  if (bm > e - r || bm < 8) { set_err(sh, ST_IO); return false; }
+  if (s.u32(r) != 12346) { set_err(sh, ST_NYI); return false; }  // run containers (cookie 12347)
+  const uint32_t nc = s.u32(r + 4);
+  if (nc > kMaxConts || 8 + 8 * (uint64_t)nc > bm) { set_err(sh, ST_NYI); return false; }
+  uint32_t tot = 0, nbm = 0;
+  sh.n_conts = nc;
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint32_t kc = s.u32(r + 8 + 4 * c);
+    const uint32_t card = (kc >> 16) + 1;
+    const uint32_t off = s.u32(r + 8 + 4 * nc + 4 * c);
+    const uint32_t dbytes = card > 4096 ? 8192u : 2 * card;  // bitmap : array container
+    if (off > bm || dbytes > bm - off) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+    sh.cont_key[c] = kc & 0xFFFF;
+    sh.cont_data[c] = r + off;
+    sh.cont_prefix[c] = tot;
+    sh.cont_bm[c] = ~0u;
+    if (card > 4096) {
+      if (nbm == kMaxBitmapConts) { set_err(sh, ST_NYI); return false; }
+      uint32_t acc = 0;
+      for (uint32_t g = 0; g < 64; g++) {
+        sh.cont_cp[nbm][g] = (uint16_t)acc;
+        for (uint32_t w = 0; w < 16; w++) acc += __popcll(s.u64(r + off + 8 * (16 * g + w)));
+      }
+      if (acc != card) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      sh.cont_bm[c] = nbm++;
+    }
+    tot += card;
+  }
+  sh.cont_prefix[nc] = tot;
+  if (!parse_stream(s, r + bm, e, tot, ex)) { set_err(sh, ST_IO); return false; }
+  return true;
+}
+
+// Parses a Dict body [u32 indices stream][u32 k][k * T] (integer/dict.rs:75-103).
+template <class Src>
+__device__ bool parse_dict(const Src& s, Shared& sh, const Stream& st, uint32_t vw, Stream* ix) {
+  const uint32_t end = st.body + st.csize;
+  if (!parse_stream(s, st.body, end, st.n, ix)) { set_err(sh, ST_IO); return false; }
+  const uint32_t e = ix->body + ix->csize;
+  if (e + 4 > end) { set_err(sh, ST_IO); return false; }
+  const uint32_t k = s.u32(e);
+  if ((uint64_t)k * vw > end - (e + 4)) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+  sh.dict_k = k;
+  sh.dict_off = e + 4;
+  return true;
+}
+
+// Cascade shapes the writer produces (Dict forbids Dict below it, Freq forbids
+// Freq: dict.rs:60-62, freq.rs:79-83).
+enum : uint32_t { CH_LEAF = 0, CH_DICT = 1, CH_FREQ = 2, CH_DICT_FREQ = 3, CH_FREQ_DICT = 4 };
+
+template <int W, bool FLT, class Src>
+__device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const LaunchArgs& a) {
+  using T = typename VT<W>::T;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t len = pd.byte_len, n = pd.num_values;
+
+  if (tid == 0) {
+    uint32_t p = 0;
+    sh.has_valid = 0;
+    do {
+      if (a.nullable) {
+        // read_validity: [def_len u32][ULEB128 h: h&1 = bit-packed, h>>1 groups][bitmap]
+        if (p + 4 > len) { set_err(sh, ST_IO); break; }
+        uint32_t def_len = s.u32(p);
+        p += 4;
+        if (def_len == 0) {  // nothing pushed: validity length mismatch
+          if (n) set_err(sh, ST_OUT_OF_SPEC);
+        } else {
+          if (def_len > len - p) { set_err(sh, ST_IO); break; }
+          uint32_t q = p, h = 0, sft = 0;
+          for (;;) {
+            if (q >= p + def_len || sft > 28) { set_err(sh, ST_OUT_OF_SPEC); break; }
+            uint32_t c = s.u8(q++);
+            h |= (c & 0x7Fu) << sft;
+            if (!(c & 0x80)) break;
+            sft += 7;
+          }
+          if (sh.err) break;
+          if (!(h & 1)) { set_err(sh, ST_OUT_OF_SPEC); break; }  // Rle run: unreachable!()
+          uint32_t groups = min(h >> 1, p + def_len - q);
+          if ((uint64_t)groups * 8 < n) { set_err(sh, ST_OUT_OF_SPEC); break; }
+          sh.has_valid = 1;
+          sh.vb_pos = q;
+          p += def_len;
+        }
+      }
+      Stream st;
+      if (!parse_stream(s, p, len, n, &st)) { set_err(sh, ST_IO); break; }
+      uint32_t chain = CH_LEAF;
+      Stream inner;
+      if (st.codec == 11) {
+        if (!parse_dict(s, sh, st, W, &inner)) break;
+        chain = CH_DICT;
+        if (inner.codec == 13) {
+          Stream ex;
+          if (!parse_freq(s, sh, inner, 4, &ex)) break;
+          chain = CH_DICT_FREQ;
+          inner = ex;
+        }
+      } else if (st.codec == 13) {
+        if (!parse_freq(s, sh, st, W, &inner)) break;
+        chain = CH_FREQ;
+        if (inner.codec == 11) {
+          Stream ix;
+          if (!parse_dict(s, sh, inner, W, &ix)) break;
+          chain = CH_FREQ_DICT;
+          inner = ix;
+        }
+      } else {
+        inner = st;
+      }
+      if (inner.codec == 11 || inner.codec == 13) { set_err(sh, ST_OUT_OF_SPEC); break; }
+      if (FLT && (inner.codec == 14 || inner.codec == 15) && (chain == CH_LEAF || chain == CH_FREQ)) {
+        set_err(sh, ST_OUT_OF_SPEC);  // no Bitpacking in decompress_double
+        break;
+      }
+      sh.top = st;
+      sh.sub = inner;
+      sh.chain = chain;
+    } while (0);
+  }
+  __syncthreads();
+  if (sh.err) return;
+
+  if (sh.has_valid) write_validity(s, sh.vb_pos, n, pd.row_off, a.out_validity);
+
+  uint8_t* obase = a.out_values + pd.row_off * W;
+  GSink<W> out{obase, ((uintptr_t)obase & (uintptr_t)(W == 8 ? 15 : 4 * W - 1)) == 0};
+  const uint32_t chain = sh.chain;
+  const Stream leaf = sh.sub;
+  const uint32_t k = sh.dict_k, doff = sh.dict_off;
+
+  if (chain == CH_LEAF) {
+    run_leaf<W>(s, sh, leaf, [&](uint32_t row, const T* v, uint32_t nv) { out.put4(row, v, nv); });
+    return;
+  }
+  if (chain == CH_DICT) {
+    // Dict: u32 index leaf stream -> gather from the plain dictionary
+    run_leaf<4>(s, sh, leaf, [&](uint32_t row, const uint32_t* idx, uint32_t nv) {
+      T v[4];
+      bool bad = false;
+#pragma unroll
+      for (uint32_t l = 0; l < 4; l++) {
+        const bool ok = l < nv && idx[l] < k;
+        bad |= (l < nv && !ok);
+        v[l] = ok ? ldv<W>(s, doff + idx[l] * W) : (T)0;
+      }
+      if (bad) set_err(sh, ST_OUT_OF_SPEC);  // data[i] out of range panics
+      out.put4(row, v, nv);
+    });
+    return;
+  }
+  // Freq at the top (CH_FREQ, CH_FREQ_DICT) or under the Dict (CH_DICT_FREQ):
+  // fill every row, then scatter the exceptions at their roaring rows.
+  T fill;
+  if (chain == CH_DICT_FREQ) {
+    const uint32_t ti = (uint32_t)sh.freq_top;
+    if (ti >= k && leaf.n < n) { if (tid == 0) set_err(sh, ST_OUT_OF_SPEC); return; }
+    fill = ti < k ? ldv<W>(s, doff + ti * W) : (T)0;
+  } else {
+    fill = (T)sh.freq_top;
+  }
+  for (uint32_t q = tid; q < (n + 3) / 4; q += NT) {
+    T v[4] = {fill, fill, fill, fill};
+    out.put4(4 * q, v, min(4u, n - 4 * q));
+  }
+  __syncthreads();  // the scatter below overwrites rows of the fill
+  auto scatter = [&](uint32_t i0, const T* x, uint32_t nv) {
+    for (uint32_t l = 0; l < nv; l++) {
+      const uint32_t row = roaring_select(s, sh, i0 + l);
+      if (row < n) out.put(row, x[l]);
+      else set_err(sh, ST_OUT_OF_SPEC);  // output[begin + val] out of range panics
+    }
+  };
+  if (chain == CH_FREQ) {
+    run_leaf<W>(s, sh, leaf, scatter);
+  } else {
+    run_leaf<4>(s, sh, leaf, [&](uint32_t i0, const uint32_t* idx, uint32_t nv) {
+      T v[4];
+      bool bad = false;
+#pragma unroll
+      for (uint32_t l = 0; l < 4; l++) {
+        const bool ok = l < nv && idx[l] < k;
+        bad |= (l < nv && !ok);
+        v[l] = ok ? ldv<W>(s, doff + idx[l] * W) : (T)0;
+      }
+      if (bad) set_err(sh, ST_OUT_OF_SPEC);
+      scatter(i0, v, nv);
+    });
+  }
+}
+
+template <int W, bool FLT>
+__global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
+  extern __shared__ u32x4 stage[];
+  __shared__ Shared sh;
+  const uint32_t page = a.list ? a.list[blockIdx.x] : blockIdx.x;
+  const PageDesc pd = a.pages[page];
+  if (threadIdx.x == 0) sh.err = 0;
+  // stage the page: aligned 16-byte loads covering [pg, pg + len)
+  const uint8_t* pg = a.chunk + pd.byte_off;
+  const uintptr_t a0 = (uintptr_t)pg & ~(uintptr_t)15;
+  const uint32_t base = (uint32_t)((uintptr_t)pg & 15);
+  const uint32_t nchunks = (base + pd.byte_len + 15) >> 4;
+  const u32x4* gsrc = (const u32x4*)a0;
+  for (uint32_t c = threadIdx.x; c < nchunks; c += NT) stage[c] = __builtin_nontemporal_load(gsrc + c);
+  __syncthreads();
+  LdsSrc s{(const uint32_t*)stage, base};
+  decode_page<W, FLT>(s, sh, pd, a);
+  __syncthreads();
+  if (threadIdx.x == 0) a.status[page] = sh.err;
+}
+
+template <int W, bool FLT>
+__global__ __launch_bounds__(NT) void k_decode_global(LaunchArgs a) {
+  __shared__ Shared sh;
+  const uint32_t page = a.list ? a.list[blockIdx.x] : blockIdx.x;
+  const PageDesc pd = a.pages[page];
+  if (threadIdx.x == 0) sh.err = 0;
+  __syncthreads();
+  GlbSrc s{a.chunk + pd.byte_off};
+  decode_page<W, FLT>(s, sh, pd, a);
+  __syncthreads();
+  if (threadIdx.x == 0) a.status[page] = sh.err;
+}
+
+template <int W, bool FLT>
+static int launch(bool staged, const LaunchArgs& a, hipStream_t stream) {
+  if (a.n_list == 0) return 0;
+  dim3 grid(a.n_list), block(NT);
+  if (staged) {
+    hipLaunchKernelGGL((k_decode_staged<W, FLT>), grid, block, a.stage_bytes, stream, a);
+  } else {
+    hipLaunchKernelGGL((k_decode_global<W, FLT>), grid, block, 0, stream, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace sbk
+
+namespace sb {
+int launch_decode_fixed(int width, bool is_float, bool staged, const LaunchArgs& a, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (is_float) {
+    if (width == 4) return sbk::launch<4, true>(staged, a, s);
+    if (width == 8) return sbk::launch<8, true>(staged, a, s);
+    return -2;
+  }
+  switch (width) {
+    case 1: return sbk::launch<1, false>(staged, a, s);
+    case 2: return sbk::launch<2, false>(staged, a, s);
+    case 4: return sbk::launch<4, false>(staged, a, s);
+    case 8: return sbk::launch<8, false>(staged, a, s);
+  }
+  return -2;
+}
+}  // namespace sb

@@ -1,0 +1,50 @@
+// sb_internal.h -- host/device shared layout of the MI355X strawboat engine.
+#pragma once
+#include <stdint.h>
+
+namespace sb {
+
+// One entry of the device page table.  Built on the host from
+// ColumnMeta.pages (src/lib.rs:40-80): byte_off is the running sum of
+// PageMeta.length from the column chunk start, row_off the running sum of
+// PageMeta.num_values (the position read_integer appends at,
+// read/array/integer.rs:225-231).
+struct PageDesc {
+  uint64_t byte_off;
+  uint64_t row_off;
+  uint32_t byte_len;
+  uint32_t num_values;
+  uint64_t reserved;
+};
+static_assert(sizeof(PageDesc) == 32, "page table entry is 32 bytes");
+
+// Per-page kernel status word (the kernel never traps).
+enum : uint32_t {
+  ST_OK = 0,
+  ST_OUT_OF_SPEC = 1,
+  ST_NYI = 2,
+  ST_IO = 3,
+  ST_CODEC = 4,
+};
+
+// Pages whose bytes fit this bound are staged whole into LDS; larger pages
+// are decoded straight from HBM by the global-source instantiation.
+constexpr uint32_t kStageMaxBytes = 48 * 1024;
+constexpr uint32_t kStagePad = 64;  // LDS slack for unaligned over-reads
+
+// Launch entry points (sb_decode.hip).
+struct LaunchArgs {
+  const uint8_t* chunk;
+  const PageDesc* pages;
+  const uint32_t* list;  // page indices for this launch, or nullptr = identity
+  uint32_t n_list;
+  uint8_t* out_values;
+  uint32_t* out_validity;  // 32-bit words of the Arrow bitmap
+  int nullable;
+  uint32_t* status;
+  uint32_t stage_bytes;  // dynamic LDS (staged launch only)
+};
+
+int launch_decode_fixed(int width, bool is_float, bool staged, const LaunchArgs& a, void* stream);
+
+}  // namespace sb
