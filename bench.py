@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""bench.py -- decoded GB/s of the MI355X strawboat page decoder.
+
+Workload (BASELINE.json configs[1]): a non-nullable
+Int32 column of 100M rows in 8192-row pages, written by the engine's writer
+with the reference's adaptive codec choice at default_compress_ratio 1.2
+(write/common.rs:49-119, compression/integer/mod.rs:231-308).  Page data
+is shaped so the adaptive choice lands on the two codecs the config names:
+80 % of pages uniform in [0, 2^b) with b cycling 12..24 (-> Bitpacking),
+20 % runs of length 2-3 of random 31-bit values (-> RLE).  The codec of
+every page is read back and reported.
+
+A "step" = one batched decode of the whole column (compressed pages resident
+in HBM -> Arrow values buffer in HBM).  value = decoded bytes of all ranks /
+max-over-ranks wall time of the timed steps.  Weak scaling: each rank owns a
+100M-row shard (its own page queue, no collectives on the data path).
+
+Also reported: the all-Bitpacking b=12 variant (the north star's >=60 %
+roofline target), the roofline of the decode kernel from HIP events on the
+launch stream, and the CPU restatement (oracle, 1 thread) on the same column.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "decoded GB/s (uncompressed) per node at 1/2/4/8 GPUs; bit-exact vs CPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PAGE_ROWS = 8192
+
+
+def gen_c2(rows: int, seed: int, variant: str) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    v = np.empty(rows, np.int32)
+    npg = (rows + PAGE_ROWS - 1) // PAGE_ROWS
+    for p in range(npg):
+        n = min(PAGE_ROWS, rows - p * PAGE_ROWS)
+        s = slice(p * PAGE_ROWS, p * PAGE_ROWS + n)
+        if variant == "b12":
+            v[s] = rng.integers(0, 1 << 12, n)
+        elif p % 5 == 4:
+            lens = rng.choice(np.array([2, 3]), size=n // 2 + 2, p=[0.3, 0.7])
+            v[s] = np.repeat(rng.integers(0, 2**31, len(lens)), lens)[:n]
+        else:
+            v[s] = rng.integers(0, 1 << (12 + (p * 7) % 13), n)
+    return v
+
+
+def codec_mix(chunk: bytes, metas) -> dict:
+    names = {0: "none", 1: "lz4", 10: "rle", 11: "dict", 12: "one_value", 13: "freq", 14: "bitpacking",
+             15: "delta_bitpacking"}
+    mix, pos = {}, 0
+    for m in metas:
+        k = names.get(chunk[pos], str(chunk[pos]))
+        mix[k] = mix.get(k, 0) + 1
+        pos += m.length
+    return mix
+
+
+class Workload:
+    """One encoded column resident in HBM twice (two input copies and two
+    output buffers, alternated per step so the 256 MiB Infinity Cache cannot
+    serve a step from the previous one)."""
+
+    def __init__(self, torch, pa, rows, seed, variant, device, threads):
+        t0 = time.time()
+        self.values = gen_c2(rows, seed, variant)
+        opts = pa.WriteOptions(default_compress_ratio=1.2, max_page_size=PAGE_ROWS, seed=seed)
+        self.chunk, self.metas = pa.encode_column(self.values, None, False, opts, n_threads=threads)
+        self.encode_s = time.time() - t0
+        self.mix = codec_mix(self.chunk, self.metas)
+        self.rows = rows
+        self.in_bytes = len(self.chunk)
+        self.out_bytes = rows * 4
+        dev = f"cuda:{device}"
+        host = torch.from_numpy(np.frombuffer(self.chunk, dtype=np.uint8).copy())
+        self.decs, self.outs = [], []
+        for _ in range(2):
+            d = pa.ColumnDecoder(host.to(dev), self.metas, np.int32, False)
+            self.decs.append(d)
+            self.outs.append(d.alloc_outputs())
+        self.expect = torch.from_numpy(self.values).to(dev)
+        torch.cuda.synchronize()
+
+    def step(self, k):
+        d = self.decs[k & 1]
+        d.decode_async(*self.outs[k & 1])
+
+    def verify(self, torch) -> bool:
+        ok = True
+        for d, (v, _) in zip(self.decs, self.outs):
+            d.check()
+            ok &= bool(torch.equal(v[: self.rows], self.expect))
+        return ok
+
+
+def timed(torch, dist, wl: Workload, steps: int, warmup: int):
+    for k in range(warmup):
+        wl.step(k)
+    torch.cuda.synchronize()
+    ok = wl.verify(torch)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        evs[k][0].record()
+        wl.step(k)
+        evs[k][1].record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    for d in wl.decs:
+        d.check()
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    return t1 - t0, kern_ms, ok
+
+
+def cpu_baseline(wl: Workload, budget_s: float = 10.0) -> dict:
+    from oracle import oracle as O
+
+    metas = [(m.length, m.num_values) for m in wl.metas]
+    t0 = time.perf_counter()
+    out, _ = O.read_column(wl.chunk, metas, np.int32)
+    first = time.perf_counter() - t0
+    assert np.array_equal(out, wl.values), "oracle decode mismatch"
+    passes = max(1, min(50, int(math.ceil(budget_s / max(first, 1e-3))) - 1))
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        O.read_column(wl.chunk, metas, np.int32)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(wl.out_bytes * passes / dt / 1e9, 3),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle/ C restatement of read_integer over the full {wl.rows}-row column, {passes} passes "
+                  f"({dt:.1f} s), 1 thread, compressed pages in host RAM -> values in host RAM",
+    }
+
+
+def load_traffic(workload: str):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get(workload)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-b12", action="store_true", help="skip the all-bitpack b=12 variant")
+    args = ap.parse_args()
+
+    import torch
+
+    import pa_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+
+        tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dist = tdist
+    threads = max(1, min(16, (os.cpu_count() or 8) // max(world, 1)))
+    pa_amd.default_context(local)
+
+    wl = Workload(torch, pa_amd, args.rows, 42 + rank, "mix", local, threads)
+    wall, kern_ms, ok = timed(torch, dist, wl, args.steps, args.warmup)
+    t = torch.tensor([wall, 0.0 if ok else 1.0], device=f"cuda:{local}", dtype=torch.float64)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max, any_bad = float(t[0]), bool(t[1] > 0)
+    kavg = float(np.mean(kern_ms))
+    achieved = (wl.in_bytes + wl.out_bytes) / (kavg / 1e3) / 1e9
+    value = world * wl.out_bytes * args.steps / wall_max / 1e9
+
+    extra = {}
+    if not args.no_b12:
+        wl12 = Workload(torch, pa_amd, args.rows, 4242 + rank, "b12", local, threads)
+        w12, k12, ok12 = timed(torch, dist, wl12, args.steps, args.warmup)
+        k12avg = float(np.mean(k12))
+        a12 = (wl12.in_bytes + wl12.out_bytes) / (k12avg / 1e3) / 1e9
+        extra["bitpack_b12"] = {
+            "decoded_GBps": round(wl12.out_bytes * args.steps / w12 / 1e9, 1),
+            "kernel_ms": round(k12avg, 4),
+            "kernel_traffic_GBps": round(a12, 1),
+            "roofline_frac": round(a12 / HBM_PEAK_GBPS, 4),
+            "compressed_bytes": wl12.in_bytes,
+            "bit_exact": bool(ok12),
+        }
+        del wl12
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (seeded numpy; pages encoded by the engine's writer)",
+            "config": {
+                "workload": "c2_int32_adaptive_bitpack_rle",
+                "rows_per_gpu": args.rows,
+                "page_rows": PAGE_ROWS,
+                "pages_per_gpu": len(wl.metas),
+                "codec_mix": wl.mix,
+                "compress_ratio_option": 1.2,
+                "compressed_bytes_per_gpu": wl.in_bytes,
+                "decoded_bytes_per_gpu": wl.out_bytes,
+                "parallelism": f"page-shard x{world}",
+            },
+            "bit_exact": (not any_bad),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": load_traffic("c2_int32_adaptive_bitpack_rle"),
+                "kernel": "k_decode_staged<4,false>",
+                "kernel_ms": round(kavg, 4),
+                "bytes_per_launch": wl.in_bytes + wl.out_bytes,
+            },
+        }
+        line.update(extra)
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(wl)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -155,6 +155,40 @@ sb_status sb_read_meta(const uint8_t* h_file, uint64_t file_len, uint64_t* h_col
                        uint64_t* h_col_page_start, uint64_t cols_cap, sb_page_meta* h_pages,
                        uint64_t pages_cap, uint64_t* n_cols, uint64_t* n_pages);
 
+/* ---- writer side ------------------------------------------------------- */
+/* write::WriteOptions (write/common.rs:37-45) + the debug-build forced codec
+ * of util/env.rs (STRAWBOAT_*_COMPRESSION; -1 = none) + the seed of the
+ * deterministic trial-window sampler that replaces thread_rng
+ * (compression/integer/mod.rs:316). */
+typedef struct {
+  int32_t default_codec;   /* CommonCompression: SB_CODEC_NONE..SB_CODEC_SNAPPY */
+  int32_t has_ratio;       /* default_compress_ratio.is_some() */
+  double ratio;            /* default_compress_ratio */
+  uint32_t forbidden_mask; /* forbidden_compressions: bit (1u << codec id) */
+  int32_t forced_codec;
+  uint64_t seed;
+} sb_write_options;
+
+/* One flat page (write::write_simple, write/serialize.rs:52-132): optional
+ * validity prefix + compress_integer / compress_double value stream.  Host
+ * memory in and out; *h_out is freed with sb_free. */
+sb_status sb_encode_page(int32_t physical_type, const void* h_values, const uint8_t* h_validity, uint64_t n,
+                         int32_t nullable, const sb_write_options* opts, uint64_t seed, uint8_t** h_out,
+                         uint64_t* out_len);
+/* NativeWriter::encode_chunk (write/common.rs:49-119) for one flat leaf:
+ * pages of max_page_rows rows (0 = one page), encoded on n_threads host
+ * threads (0 = all).  Page p samples with sb_page_seed(opts->seed, p). */
+sb_status sb_encode_column(int32_t physical_type, const void* h_values, const uint8_t* h_validity,
+                           uint64_t n_rows, int32_t nullable, const sb_write_options* opts,
+                           uint64_t max_page_rows, int32_t n_threads, uint8_t** h_out, uint64_t* out_len,
+                           sb_page_meta** h_metas, uint64_t* n_pages);
+uint64_t sb_page_seed(uint64_t seed, uint64_t page);
+/* NativeWriter::finish (write/writer.rs:128-167) footer bytes. */
+sb_status sb_write_footer(const uint8_t* h_schema, uint64_t schema_len, const uint64_t* h_col_offsets,
+                          const uint64_t* h_col_npages, uint64_t n_cols, const sb_page_meta* h_pages,
+                          uint8_t** h_out, uint64_t* out_len);
+void sb_free(void* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -87,6 +87,7 @@ def lib():
         L.orc_write_validity.argtypes = [P, S, ctypes.POINTER(_Buf)]
         L.orc_read_flat_page.argtypes = [P, S, S, I, I, I, P, P]
         L.orc_write_flat_page.argtypes = [P, P, S, I, I, I, I, ctypes.POINTER(WriteOptions), ctypes.POINTER(_Buf)]
+        L.orc_read_column.argtypes = [P, S, P, S, I, I, I, P, P]
         L.orc_roaring_decode.argtypes = [P, S, P, S, PS]
         L.orc_roaring_encode.argtypes = [P, S, ctypes.POINTER(_Buf)]
         L.orc_hybrid_decode.argtypes = [P, S, ctypes.c_uint32, S, P]
@@ -272,3 +273,17 @@ def page_codec(page: bytes, nullable: bool) -> int:
     if nullable:
         pos = 4 + int.from_bytes(page[:4], "little")
     return page[pos]
+
+
+def read_column(chunk: bytes, metas, dtype, nullable=False):
+    """read_integer / read_double over a whole column chunk (one C call)."""
+    dtype = np.dtype(dtype)
+    n = sum(int(nv) for _, nv in metas)
+    m = np.asarray([(int(l), int(nv)) for l, nv in metas], dtype=np.uint64).reshape(-1)
+    src = np.frombuffer(chunk, dtype=np.uint8)
+    out = np.zeros(max(n, 1), dtype)
+    bits = np.zeros((n + 7) // 8 + 1, np.uint8)
+    kind = 1 if dtype.kind == "f" else 0
+    rc = lib().orc_read_column(_ptr(src), len(chunk), _ptr(m), len(metas), kind, dtype.itemsize, int(nullable), _ptr(out), _ptr(bits))
+    _check(rc, "read_column")
+    return out[:n], (np.unpackbits(bits, bitorder="little")[:n].astype(bool) if nullable else None)

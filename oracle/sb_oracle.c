@@ -1257,3 +1257,41 @@ int orc_write_flat_page(const uint8_t* values, const uint8_t* validity, size_t n
   return kind ? orc_compress_double(values, validity, n, width, opt, out)
               : orc_compress_integer(values, validity, n, width, is_signed, opt, out);
 }
+
+/* read_integer / read_double (read/array/integer.rs:210-238,
+ * read/array/double.rs:210-238): every page of a column chunk appended.
+ * metas = n_pages pairs (length, num_values).  Single-threaded, like the
+ * reference's batch reader. */
+int orc_read_column(const uint8_t* chunk, size_t len, const uint64_t* metas, size_t n_pages, int kind, int width,
+                    int nullable, uint8_t* out_values, uint8_t* out_bits) {
+  size_t pos = 0, row = 0;
+  uint8_t* tmp = NULL;
+  size_t tmp_cap = 0;
+  for (size_t p = 0; p < n_pages; p++) {
+    size_t plen = (size_t)metas[2 * p], nv = (size_t)metas[2 * p + 1];
+    if (pos + plen > len) { free(tmp); return ORC_E_IO; }
+    uint8_t* bits = NULL;
+    if (nullable) {
+      size_t need = (nv + 7) / 8 + 1;
+      if (need > tmp_cap) { free(tmp); tmp = (uint8_t*)malloc(need); tmp_cap = need; }
+      bits = tmp;
+    }
+    int rc = orc_read_flat_page(chunk + pos, plen, nv, kind, width, nullable, out_values + row * (size_t)width, bits);
+    if (rc) { free(tmp); return rc; }
+    if (nullable) {
+      if ((row & 7) == 0) {
+        memcpy(out_bits + row / 8, bits, (nv + 7) / 8);
+      } else {
+        for (size_t i = 0; i < nv; i++) {
+          size_t r = row + i;
+          if (get_bit(bits, i)) out_bits[r >> 3] |= (uint8_t)(1u << (r & 7));
+          else out_bits[r >> 3] &= (uint8_t)~(1u << (r & 7));
+        }
+      }
+    }
+    pos += plen;
+    row += nv;
+  }
+  free(tmp);
+  return ORC_OK;
+}

@@ -101,6 +101,10 @@ int orc_write_flat_page(const uint8_t* values, const uint8_t* validity, size_t n
                         int width, int is_signed, int nullable, const orc_write_options* opt,
                         orc_buf* out);
 
+/* whole column chunk (read_integer / read_double): metas = (length, num_values) pairs */
+int orc_read_column(const uint8_t* chunk, size_t len, const uint64_t* metas, size_t n_pages, int kind, int width,
+                    int nullable, uint8_t* out_values, uint8_t* out_bits);
+
 /* ---- roaring portable format (roaring 0.10.1) ---- */
 /* Deserializes into ascending positions.  *count set; positions may be NULL to
  * size.  cap = capacity of positions. */

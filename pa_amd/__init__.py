@@ -13,3 +13,4 @@ from .read import (  # noqa: F401
     read_meta,
     unpack_bitmap,
 )
+from .write import NativeWriter, WriteOptions, encode_column, encode_page, page_seed  # noqa: F401,E402

@@ -23,7 +23,8 @@ EXPORTED = [
     "sb_ctx_create", "sb_ctx_destroy", "sb_ctx_set_stream", "sb_ctx_stream", "sb_sync", "sb_last_error",
     "sb_status_str", "sb_plan_column", "sb_plan_destroy", "sb_plan_num_rows", "sb_plan_num_pages",
     "sb_decode_planned", "sb_plan_status", "sb_decode_column", "sb_plan_last_kernel_ms",
-    "sb_decompress_values", "sb_read_meta",
+    "sb_decompress_values", "sb_read_meta", "sb_encode_page", "sb_encode_column", "sb_page_seed",
+    "sb_write_footer", "sb_free",
 ]
 
 
@@ -41,6 +42,17 @@ class PageMetaC(ctypes.Structure):
 
 class ColumnDescC(ctypes.Structure):
     _fields_ = [("physical_type", ctypes.c_int32), ("nullable", ctypes.c_int32)]
+
+
+class WriteOptionsC(ctypes.Structure):
+    _fields_ = [
+        ("default_codec", ctypes.c_int32),
+        ("has_ratio", ctypes.c_int32),
+        ("ratio", ctypes.c_double),
+        ("forbidden_mask", ctypes.c_uint32),
+        ("forced_codec", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
 
 
 class PrimitiveOutC(ctypes.Structure):
@@ -101,5 +113,17 @@ def lib():
     L.sb_decompress_values.restype = I32
     L.sb_read_meta.argtypes = [P, U64, P, P, U64, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]
     L.sb_read_meta.restype = I32
+    PU8 = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))
+    L.sb_encode_page.argtypes = [I32, P, P, U64, I32, ctypes.POINTER(WriteOptionsC), U64, PU8, ctypes.POINTER(U64)]
+    L.sb_encode_page.restype = I32
+    L.sb_encode_column.argtypes = [I32, P, P, U64, I32, ctypes.POINTER(WriteOptionsC), U64, I32, PU8,
+                                   ctypes.POINTER(U64), ctypes.POINTER(ctypes.POINTER(PageMetaC)), ctypes.POINTER(U64)]
+    L.sb_encode_column.restype = I32
+    L.sb_page_seed.argtypes = [U64, U64]
+    L.sb_page_seed.restype = U64
+    L.sb_write_footer.argtypes = [P, U64, P, P, U64, P, PU8, ctypes.POINTER(U64)]
+    L.sb_write_footer.restype = I32
+    L.sb_free.argtypes = [P]
+    L.sb_free.restype = None
     _lib = L
     return L

@@ -1,0 +1,27 @@
+// sb_encode.h -- host page encoder (writer side), see sb_encode.cpp.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace sb {
+namespace enc {
+
+// write::WriteOptions (write/common.rs:37-45) + forced codec (util/env.rs)
+struct Opts {
+  int32_t default_codec = 0;
+  bool has_ratio = false;
+  double ratio = 0.0;
+  uint32_t forbidden = 0;  // bit (1 << codec id)
+  int32_t forced = -1;
+};
+
+// One flat page of n rows (serialize.rs:52-132) appended to out.
+int encode_page(int phys, const void* values, const uint8_t* validity, size_t n, bool nullable, const Opts& opt,
+                uint64_t seed, std::vector<uint8_t>& out);
+// Sampler seed of page `page` of a column written with `seed`.
+uint64_t page_seed(uint64_t seed, uint64_t page);
+int type_size(int phys);
+
+}  // namespace enc
+}  // namespace sb

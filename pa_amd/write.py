@@ -1,0 +1,150 @@
+"""Write side, mirroring the reference's NativeWriter / WriteOptions.
+
+Reference (b41sh/pa @ 2025-01-17):
+  WriteOptions                  src/write/common.rs:37-45
+  NativeWriter::{new, start, write, finish}   src/write/writer.rs:42-167
+  encode_chunk (paging)         src/write/common.rs:49-119
+
+Encoding runs in the engine's host encoder (libstrawboat_gpu.so,
+sb_encode_column); pages are encoded in parallel on the host's cores.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .read import ColumnMeta, PageMeta, physical_type
+
+# CommonCompression / Compression codec ids (compression/mod.rs:64-82)
+NONE, LZ4, ZSTD, SNAPPY = 0, 1, 2, 3
+RLE, DICT, ONE_VALUE, FREQ, BITPACKING, DELTA_BITPACKING, PATAS = 10, 11, 12, 13, 14, 15, 16
+
+ARROW_MAGIC = b"ARROW2"
+
+
+@dataclass
+class WriteOptions:
+    """write::WriteOptions (common.rs:37-45).  forced_codec mirrors the
+    debug-build STRAWBOAT_*_COMPRESSION switches (util/env.rs); seed drives
+    the deterministic trial-window sampler."""
+
+    default_compression: int = NONE
+    default_compress_ratio: Optional[float] = None
+    max_page_size: Optional[int] = None
+    forbidden_compressions: Sequence[int] = field(default_factory=tuple)
+    forced_codec: int = -1
+    seed: int = 42
+
+    def c(self) -> N.WriteOptionsC:
+        m = 0
+        for c in self.forbidden_compressions:
+            m |= 1 << c
+        r = self.default_compress_ratio
+        return N.WriteOptionsC(self.default_compression, r is not None, float(r or 0.0), m, self.forced_codec, self.seed)
+
+
+def _take(ptr, n) -> bytes:
+    b = ctypes.string_at(ptr, n) if n else b""
+    N.lib().sb_free(ptr)
+    return b
+
+
+def encode_column(values: np.ndarray, validity=None, nullable: bool = False,
+                  options: Optional[WriteOptions] = None, n_threads: int = 0) -> Tuple[bytes, List[PageMeta]]:
+    """encode_chunk for one flat leaf -> (column chunk bytes, page metas)."""
+    options = options or WriteOptions()
+    values = np.ascontiguousarray(values)
+    vb = None
+    if validity is not None:
+        vb = np.packbits(np.asarray(validity, bool), bitorder="little")
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_uint64()
+    metas = ctypes.POINTER(N.PageMetaC)()
+    npg = ctypes.c_uint64()
+    opts = options.c()
+    st = N.lib().sb_encode_column(
+        physical_type(values.dtype), values.ctypes.data_as(ctypes.c_void_p),
+        None if vb is None else vb.ctypes.data_as(ctypes.c_void_p), len(values), int(nullable),
+        ctypes.byref(opts), options.max_page_size or 0, n_threads, ctypes.byref(out), ctypes.byref(olen),
+        ctypes.byref(metas), ctypes.byref(npg))
+    if st:
+        raise N.StrawboatError(st, "encode_column")
+    pm = [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
+    N.lib().sb_free(metas)
+    return _take(out, olen.value), pm
+
+
+def encode_page(values: np.ndarray, validity=None, nullable: bool = False,
+                options: Optional[WriteOptions] = None, seed: Optional[int] = None) -> bytes:
+    options = options or WriteOptions()
+    values = np.ascontiguousarray(values)
+    vb = None if validity is None else np.packbits(np.asarray(validity, bool), bitorder="little")
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_uint64()
+    opts = options.c()
+    st = N.lib().sb_encode_page(physical_type(values.dtype), values.ctypes.data_as(ctypes.c_void_p),
+                                None if vb is None else vb.ctypes.data_as(ctypes.c_void_p), len(values), int(nullable),
+                                ctypes.byref(opts), options.seed if seed is None else seed, ctypes.byref(out),
+                                ctypes.byref(olen))
+    if st:
+        raise N.StrawboatError(st, "encode_page")
+    return _take(out, olen.value)
+
+
+def page_seed(seed: int, page: int) -> int:
+    return N.lib().sb_page_seed(seed, page)
+
+
+class NativeWriter:
+    """NativeWriter (writer.rs:42-167) over an in-memory buffer for flat
+    primitive columns: start() -> write(columns) once -> finish()."""
+
+    def __init__(self, options: Optional[WriteOptions] = None, schema_bytes: bytes = b""):
+        self.options = options or WriteOptions()
+        self.schema_bytes = schema_bytes
+        self.buf = bytearray()
+        self.metas: List[ColumnMeta] = []
+        self.state = "none"
+
+    def start(self):
+        if self.state != "none":
+            raise N.StrawboatError(N.E_OUT_OF_SPEC, "The strawboat file can only be started once")
+        self.buf += ARROW_MAGIC + b"\x00\x00"
+        self.state = "started"
+
+    def write(self, columns: Sequence[Tuple[np.ndarray, Optional[np.ndarray], bool]]):
+        """columns: (values, validity|None, nullable) per leaf, equal lengths."""
+        if self.state == "written":
+            raise N.StrawboatError(N.E_OUT_OF_SPEC, "The strawboat file can only accept one RowGroup in a single file")
+        if self.state != "started":
+            raise N.StrawboatError(N.E_OUT_OF_SPEC, "The strawboat file must be started before it can be written to")
+        for values, validity, nullable in columns:
+            chunk, pages = encode_column(values, validity, nullable, self.options)
+            self.metas.append(ColumnMeta(len(self.buf), pages))
+            self.buf += chunk
+        self.state = "written"
+
+    def finish(self) -> bytes:
+        if self.state != "written":
+            raise N.StrawboatError(N.E_OUT_OF_SPEC, "The strawboat file must be written before it can be finished")
+        offs = (ctypes.c_uint64 * max(1, len(self.metas)))(*[m.offset for m in self.metas])
+        nps = (ctypes.c_uint64 * max(1, len(self.metas)))(*[len(m.pages) for m in self.metas])
+        allp = [p for m in self.metas for p in m.pages]
+        pages = (N.PageMetaC * max(1, len(allp)))(*[N.PageMetaC(p.length, p.num_values) for p in allp])
+        sch = (ctypes.c_uint8 * max(1, len(self.schema_bytes))).from_buffer_copy(self.schema_bytes or b"\x00")
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        olen = ctypes.c_uint64()
+        st = N.lib().sb_write_footer(sch, len(self.schema_bytes), offs, nps, len(self.metas), pages,
+                                     ctypes.byref(out), ctypes.byref(olen))
+        if st:
+            raise N.StrawboatError(st, "finish")
+        self.buf += _take(out, olen.value)
+        self.state = "finished"
+        return bytes(self.buf)
+
+    def total_size(self) -> int:
+        return len(self.buf)
