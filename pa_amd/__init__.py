@@ -14,3 +14,4 @@ from .read import (  # noqa: F401
     unpack_bitmap,
 )
 from .write import NativeWriter, WriteOptions, encode_column, encode_page, page_seed  # noqa: F401,E402
+from .shard import Shard, shard_pages  # noqa: F401,E402

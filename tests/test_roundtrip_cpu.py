@@ -1,0 +1,124 @@
+"""The reference's integration matrix (tests/it/io.rs:72-278 via
+test_write_read :417-438) restated for flat primitive columns: every chunk is
+written under None / LZ4 / Zstd / Snappy with 2048-row pages and
+default_compress_ratio 2.0, read back, and compared with Arrow logical
+equality (values under null slots are not compared, like assert_eq!).
+Writer = the product's host encoder; reader = the oracle (CPU).  The GPU
+reader is held to the same pages, bit-exact, in test_gpu_*.py."""
+import numpy as np
+import pytest
+
+import pa_amd
+from oracle import oracle as O
+
+WRITE_PAGE = 2048
+CODECS = [0, 1, 2, 3]
+
+
+def write_read(values, validity, nullable):
+    for dc in CODECS:
+        opts = pa_amd.WriteOptions(default_compression=dc, default_compress_ratio=2.0, max_page_size=WRITE_PAGE,
+                                   forbidden_compressions=(O.PATAS,) if values.dtype == np.float32 else ())
+        chunk, metas = pa_amd.encode_column(values, validity, nullable, opts)
+        assert sum(m.num_values for m in metas) == len(values)
+        out, vv = O.read_column(chunk, [(m.length, m.num_values) for m in metas], values.dtype, nullable)
+        if nullable:
+            assert (vv == validity).all()
+            m = validity
+            assert (out[m].view(np.uint8) if out.dtype.itemsize == 1 else out[m]).tobytes() == values[m].tobytes()
+        else:
+            assert out.tobytes() == values.tobytes()
+
+
+def create_random_index(size, null_density, uniq, rng, dtype=np.int32):
+    v = rng.integers(0, uniq, size).astype(dtype)
+    valid = rng.random(size) >= null_density
+    return v, valid
+
+
+def test_basic():
+    for dt in [np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16, np.int32, np.int64, np.float32, np.float64]:
+        v = np.array([1, 2, 3, 4, 5, 6], dtype=dt) if np.dtype(dt).kind != "f" else np.array([1.1, 2.2, 3.3, 4.4, 5.5, 6.6], dt)
+        write_read(v, None, False)
+
+
+@pytest.mark.parametrize("null_density", [0.0, 0.1, 0.2, 0.3, 0.4, 0.5])
+def test_random(null_density):
+    rng = np.random.default_rng(42)
+    for dt in [np.int32, np.int64, np.float64]:
+        v, valid = create_random_index(10000, null_density, 10000, rng, dt)
+        write_read(v, valid, True)
+        write_read(v, None, False)
+
+
+def test_dict():
+    rng = np.random.default_rng(42)
+    for nd in [0.1, 0.2, 0.3, 0.4]:
+        v, valid = create_random_index(10000, nd, 8, rng)
+        write_read(v, valid, True)
+    v, valid = create_random_index(10000, 0.5, 8, rng, np.float64)
+    write_read(v, valid, True)
+
+
+def test_freq():
+    # io.rs:120-132: per page 2045 x 20 + 3 x 10000
+    page = np.concatenate([np.full(2045, 20, np.uint32), np.full(3, 10000, np.uint32)])
+    v = np.tile(page, 5)
+    write_read(v, None, False)
+    opts = pa_amd.WriteOptions(default_compress_ratio=2.0, max_page_size=WRITE_PAGE)
+    chunk, metas = pa_amd.encode_column(v, None, False, opts)
+    assert chunk[0] == O.FREQ
+
+
+def test_bitpacking():
+    rng = np.random.default_rng(42)
+    v, _ = create_random_index(10240, 0.0, 8, rng)
+    write_read(v, None, False)
+
+
+def test_delta_bitpacking():
+    # io.rs:146-152: 0..10240 as u32 and i32
+    for dt in (np.uint32, np.int32):
+        v = np.arange(10240, dtype=dt)
+        write_read(v, None, False)
+        chunk, metas = pa_amd.encode_column(v, None, False, pa_amd.WriteOptions(default_compress_ratio=2.0, max_page_size=WRITE_PAGE))
+        assert chunk[0] == O.DELTA_BITPACKING
+
+
+def test_onevalue():
+    write_read(np.full(10000, 3, np.int32), None, False)
+    write_read(np.full(10000, 3.5, np.float64), None, False)
+
+
+def test_float():
+    rng = np.random.default_rng(42)
+    for nd in [0.0, 0.1, 0.5]:
+        v = rng.integers(0, 10000, 10000).astype(np.float64)
+        write_read(v, rng.random(10000) >= nd, True)
+        v32 = np.round(rng.standard_normal(10000), 3).astype(np.float32)
+        write_read(v32, None, False)
+
+
+def test_encoder_matches_oracle_encoder():
+    """Product host encoder == oracle restatement of compress_integer /
+    compress_double, byte for byte, per page (same sampler seed)."""
+    from tests.colgen import gen_values
+
+    rng = np.random.default_rng(1)
+    for dt in [np.int32, np.uint32, np.int64, np.uint8, np.int16, np.float64]:
+        for kind in ["index", "full", "sorted", "one", "runs", "short_runs", "freq", "bits12"]:
+            v = gen_values(kind, 9000, dt, rng)
+            for nullable in (False, True):
+                val = rng.random(9000) > 0.2 if nullable else None
+                for ratio, forced, dc in [(None, -1, 0), (1.2, -1, 0), (2.0, O.DICT, 0), (2.0, O.FREQ, 0), (1.1, -1, 1)]:
+                    wo = pa_amd.WriteOptions(default_compression=dc, default_compress_ratio=ratio, max_page_size=4096,
+                                             forced_codec=forced, seed=11)
+                    chunk, metas = pa_amd.encode_column(v, val, nullable, wo)
+                    pos = 0
+                    for i, m in enumerate(metas):
+                        sl = slice(i * 4096, i * 4096 + m.num_values)
+                        ob = O.write_page(v[sl], None if val is None else val[sl], nullable,
+                                          O.WriteOptions.make(default_codec=dc, ratio=ratio, forced=forced,
+                                                              seed=pa_amd.page_seed(11, i)))
+                        assert chunk[pos:pos + m.length] == ob, (np.dtype(dt).name, kind, nullable, ratio, forced, i)
+                        pos += m.length
