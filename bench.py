@@ -108,22 +108,24 @@ def timed(torch, dist, wl: Workload, steps: int, warmup: int):
         wl.step(k)
     torch.cuda.synchronize()
     ok = wl.verify(torch)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # HIP events on the launch stream (the context launches on torch's current
+    # stream) bracket the whole timed region: per-launch average = span / steps
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()
     for k in range(steps):
-        evs[k][0].record()
         wl.step(k)
-        evs[k][1].record()
+    ev1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
     for d in wl.decs:
         d.check()
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    kern_ms = [ev0.elapsed_time(ev1) / steps]
     return t1 - t0, kern_ms, ok
 
 

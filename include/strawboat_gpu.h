@@ -136,8 +136,11 @@ sb_status sb_decode_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_
                            uint64_t chunk_len, const sb_page_meta* h_metas, uint64_t n_pages,
                            const sb_primitive_out* out);
 
-/* Device kernel time of the plan's last decode, in milliseconds (HIP events
- * recorded on the launch stream around the decode kernels). */
+/* Opt-in per-decode timing: when on, sb_decode_planned records HIP events on
+ * the launch stream around the decode kernels (off by default: an event
+ * record between back-to-back decodes costs a gap on the stream). */
+sb_status sb_plan_enable_timing(sb_plan* plan, int32_t on);
+/* Device time of the plan's last timed decode, in milliseconds. */
 sb_status sb_plan_last_kernel_ms(sb_ctx* ctx, sb_plan* plan, float* ms);
 
 /* ---- value-stream level (unit parity) ---------------------------------- */

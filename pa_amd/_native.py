@@ -11,7 +11,7 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstrawboat_gpu.so")
+LIB_PATH = os.environ.get("PA_AMD_LIB") or os.path.join(_HERE, "libstrawboat_gpu.so")
 
 # sb_status
 OK, E_OUT_OF_SPEC, E_NYI, E_IO, E_CODEC, E_DEVICE, E_ARG = 0, 1, 2, 3, 4, 5, 6
@@ -22,7 +22,7 @@ INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = ran
 EXPORTED = [
     "sb_ctx_create", "sb_ctx_destroy", "sb_ctx_set_stream", "sb_ctx_stream", "sb_sync", "sb_last_error",
     "sb_status_str", "sb_plan_column", "sb_plan_destroy", "sb_plan_num_rows", "sb_plan_num_pages",
-    "sb_decode_planned", "sb_plan_status", "sb_decode_column", "sb_plan_last_kernel_ms",
+    "sb_decode_planned", "sb_plan_status", "sb_decode_column", "sb_plan_last_kernel_ms", "sb_plan_enable_timing",
     "sb_decompress_values", "sb_read_meta", "sb_encode_page", "sb_encode_column", "sb_page_seed",
     "sb_write_footer", "sb_free",
 ]
@@ -107,6 +107,8 @@ def lib():
     L.sb_decode_column.argtypes = [P, ctypes.POINTER(ColumnDescC), P, U64, ctypes.POINTER(PageMetaC), U64,
                                    ctypes.POINTER(PrimitiveOutC)]
     L.sb_decode_column.restype = I32
+    L.sb_plan_enable_timing.argtypes = [P, I32]
+    L.sb_plan_enable_timing.restype = I32
     L.sb_plan_last_kernel_ms.argtypes = [P, P, ctypes.POINTER(ctypes.c_float)]
     L.sb_plan_last_kernel_ms.restype = I32
     L.sb_decompress_values.argtypes = [P, I32, P, U64, U64, P]

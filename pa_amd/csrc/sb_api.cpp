@@ -37,6 +37,7 @@ struct sb_plan {
   uint32_t stage_bytes = 0;
   bool validity_needs_zero = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timing = false;  // record HIP events around each decode (sb_plan_enable_timing)
   bool timed = false;
 };
 
@@ -214,7 +215,7 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   if (p->desc.nullable && p->validity_needs_zero)
     HIP_TRY(ctx, hipMemsetAsync(out->d_validity, 0, (p->n_rows + 31) / 32 * 4, ctx->stream));
-  HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
+  if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
   sb::LaunchArgs a{};
   a.chunk = p->d_chunk;
   a.pages = p->d_pages;
@@ -231,8 +232,10 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   a.n_list = p->n_global;
   if (sb::launch_decode_fixed(p->width, p->is_float, false, a, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "global decode launch failed: %s", hipGetErrorString(hipGetLastError()));
-  HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
-  p->timed = true;
+  if (p->timing) {
+    HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
+    p->timed = true;
+  }
   return SB_OK;
 }
 
@@ -250,6 +253,12 @@ sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
       return fail(ctx, (sb_status)st[i], "page %llu: %s", (unsigned long long)i, sb_status_str((int)st[i]));
     }
   }
+  return SB_OK;
+}
+
+sb_status sb_plan_enable_timing(sb_plan* p, int32_t on) {
+  if (!p) return SB_E_ARG;
+  p->timing = on != 0;
   return SB_OK;
 }
 

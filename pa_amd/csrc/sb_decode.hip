@@ -26,11 +26,24 @@ namespace sbk {
 
 using namespace sb;
 
-constexpr int NT = 256;
+#ifndef SB_BLOCK
+#define SB_BLOCK 256
+#endif
+#ifndef SB_LOAD_NT
+#define SB_LOAD_NT 1
+#endif
+#ifndef SB_STORE_NT
+#define SB_STORE_NT 1
+#endif
+#ifndef SB_LDS_DMA
+#define SB_LDS_DMA 1
+#endif
+constexpr int NT = SB_BLOCK;
 constexpr int NW = NT / 64;
 constexpr uint32_t kWinBlocks = 64;  // bitpack blocks per header walk window
 constexpr uint32_t kMaxConts = 16;   // roaring containers handled per page
 constexpr uint32_t kMaxBitmapConts = 4;  // of which bitmap containers (card > 4096)
+constexpr uint32_t kRleFastRows = 8192;  // RLE pages up to this many rows use the run-start bitmap
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -126,7 +139,9 @@ struct Shared {
   uint32_t rle_start[NT + 1];
   uint32_t rle_c;
   uint32_t rle_R;
-  uint32_t rle_flags;  // bit0 = a run ends exactly at n, bit1 = a run overshoots n
+  uint32_t rle_flags;  // bit0 = a run ends exactly at n, bit1 = a run overshoots n, bit2 = zero-count run
+  uint32_t rle_bits[kRleFastRows / 32];  // bit r set <=> a run starts at row r
+  uint16_t rle_pref[kRleFastRows / 32];  // set bits before word w
   // page header
   uint32_t has_valid, vb_pos, vb_bytes;
   Stream top;
@@ -173,6 +188,15 @@ __device__ __forceinline__ T block_excl_scan(T v, Shared& sh, T* total) {
 // ---------------------------------------------------------------------------
 // output sinks
 // ---------------------------------------------------------------------------
+template <class V>
+__device__ __forceinline__ void st_out(V* p, V v) {
+#if SB_STORE_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 template <int W>
 struct GSink {
   uint8_t* base;  // page row 0
@@ -187,11 +211,11 @@ struct GSink {
   __device__ __forceinline__ void put4(uint32_t row, const T* v, uint32_t nvalid) const {
     if (nvalid == 4 && vec) {
       if constexpr (W == 8) {
-        uint4* p = (uint4*)(base + (size_t)row * 8);
-        p[0] = make_uint4((uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32));
-        p[1] = make_uint4((uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32));
+        u32x4* p = (u32x4*)(base + (size_t)row * 8);
+        st_out(p, u32x4{(uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32)});
+        st_out(p + 1, u32x4{(uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32)});
       } else if constexpr (W == 4) {
-        *(uint4*)(base + (size_t)row * 4) = make_uint4(v[0], v[1], v[2], v[3]);
+        st_out((u32x4*)(base + (size_t)row * 4), u32x4{v[0], v[1], v[2], v[3]});
       } else if constexpr (W == 2) {
         *(uint2*)(base + (size_t)row * 2) = make_uint2((v[0] & 0xFFFF) | (v[1] << 16), (v[2] & 0xFFFF) | (v[3] << 16));
       } else {
@@ -263,19 +287,25 @@ __device__ void rle_prepare(const Src& s, Shared& sh, const Stream& st) {
   const uint32_t runsz = 4 + SW;
   const uint32_t R = st.csize / runsz;
   const uint32_t c = (R + NT - 1) / NT;
+  const bool small = st.n <= kRleFastRows;
+  if (small)
+    for (uint32_t w = tid; w < kRleFastRows / 32; w += NT) sh.rle_bits[w] = 0;
   uint32_t r0 = min(R, tid * c), r1 = min(R, r0 + c);
   uint64_t sum = 0;
   for (uint32_t r = r0; r < r1; r++) sum += s.u32(st.body + r * runsz);
   uint64_t tot;
-  uint64_t start = block_excl_scan<uint64_t>(sum, sh, &tot);
+  uint64_t start = block_excl_scan<uint64_t>(sum, sh, &tot);  // (syncs: the zeroing above is visible)
   uint32_t flags = 0;
   uint64_t acc = start;
   if (start < st.n) {
     for (uint32_t r = r0; r < r1; r++) {
-      uint64_t b = acc;
-      acc += s.u32(st.body + r * runsz);
-      if (b < st.n && acc == st.n) flags |= 1;
-      if (b < st.n && acc > st.n) flags |= 2;
+      const uint64_t b = acc;
+      const uint32_t cnt = s.u32(st.body + r * runsz);
+      acc += cnt;
+      if (cnt == 0) flags |= 4;
+      if (acc == st.n) flags |= 1;
+      if (acc > st.n) flags |= 2;
+      if (small) atomicOr(&sh.rle_bits[b >> 5], 1u << (b & 31));
       if (acc >= st.n) break;
     }
   }
@@ -290,8 +320,26 @@ __device__ void rle_prepare(const Src& s, Shared& sh, const Stream& st) {
   if (flags) atomicOr(&sh.rle_flags, flags);
   __syncthreads();
   if (tid == 0 && st.n > 0) {
-    uint32_t f = sh.rle_flags;
+    const uint32_t f = sh.rle_flags;
     if ((f & 2) || !(f & 1)) set_err(sh, (f & 2) ? ST_OUT_OF_SPEC : ST_IO);
+  }
+  if (small) {  // prefix popcount of the run-start bitmap (kRleFastRows/32 words)
+    constexpr uint32_t kWords = kRleFastRows / 32;
+    constexpr uint32_t kPer = kWords >= (uint32_t)NT ? kWords / NT : 1;
+    const uint32_t w0 = tid * kPer;
+    uint32_t pc[kPer], tsum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+      pc[k] = w0 + k < kWords ? __popc(sh.rle_bits[w0 + k]) : 0u;
+      tsum += pc[k];
+    }
+    uint32_t t;
+    uint32_t pre = block_excl_scan<uint32_t>(tsum, sh, &t);
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+      if (w0 + k < kWords) sh.rle_pref[w0 + k] = (uint16_t)pre;
+      pre += pc[k];
+    }
   }
   __syncthreads();
 }
@@ -354,6 +402,24 @@ __device__ void run_leaf(const Src& s, Shared& sh, const Stream st, Fn&& fn) {
       rle_prepare<SW>(s, sh, st);
       if (sh.err) return;
       const uint32_t runsz = 4 + SW;
+      if (st.n <= kRleFastRows && !(sh.rle_flags & 4)) {
+        // run of row r = (run starts at rows <= r) - 1: one bitmap word and one
+        // prefix per quad, no search
+        for (uint32_t q = tid; q < nq; q += NT) {
+          const uint32_t row = 4 * q, nv = min(4u, st.n - row);
+          const uint32_t word = sh.rle_bits[row >> 5], base = sh.rle_pref[row >> 5];
+          T v[4];
+#pragma unroll
+          for (uint32_t l = 0; l < 4; l++) {
+            const uint32_t b = (row + l) & 31;
+            const uint32_t m = b == 31 ? 0xFFFFFFFFu : ((2u << b) - 1);
+            const uint32_t r = base + __popc(word & m) - 1;
+            v[l] = ldv<SW>(s, st.body + r * runsz + 4);
+          }
+          fn(row, v, nv);
+        }
+        return;
+      }
       for (uint32_t q = tid; q < nq; q += NT) {
         uint32_t row = 4 * q, nv = min(4u, st.n - row);
         uint32_t rs, re;
@@ -706,7 +772,25 @@ __global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
   const uint32_t base = (uint32_t)((uintptr_t)pg & 15);
   const uint32_t nchunks = (base + pd.byte_len + 15) >> 4;
   const u32x4* gsrc = (const u32x4*)a0;
-  for (uint32_t c = threadIdx.x; c < nchunks; c += NT) stage[c] = __builtin_nontemporal_load(gsrc + c);
+#if SB_LDS_DMA
+  {  // LDS-DMA: each wave instruction lands 64 x 16 B contiguously at the wave's LDS base
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t c0 = wv * 64; c0 < nchunks; c0 += NT) {
+      if (c0 + lane < nchunks)
+        __builtin_amdgcn_global_load_lds((const void*)(gsrc + c0 + lane), (__attribute__((address_space(3))) void*)(stage + c0),
+                                         16, 0, SB_LOAD_NT ? 2 : 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#else
+  for (uint32_t c = threadIdx.x; c < nchunks; c += NT) {
+#if SB_LOAD_NT
+    stage[c] = __builtin_nontemporal_load(gsrc + c);
+#else
+    stage[c] = gsrc[c];
+#endif
+  }
+#endif
   __syncthreads();
   LdsSrc s{(const uint32_t*)stage, base};
   decode_page<W, FLT>(s, sh, pd, a);

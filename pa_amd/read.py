@@ -174,7 +174,8 @@ class ColumnDecoder:
     decode() is the batch_read_array path for one flat primitive leaf
     (batch_read.rs:27-60 -> read_integer / read_double)."""
 
-    def __init__(self, chunk, page_metas: Sequence[PageMeta], dtype, nullable: bool, ctx: Optional[Context] = None):
+    def __init__(self, chunk, page_metas: Sequence[PageMeta], dtype, nullable: bool, ctx: Optional[Context] = None,
+                 timing: bool = False):
         import torch
 
         self.ctx = ctx or default_context()
@@ -190,6 +191,8 @@ class ColumnDecoder:
         if st:
             raise N.StrawboatError(st, self.ctx.error())
         self._h = h
+        if timing:
+            N.lib().sb_plan_enable_timing(h, 1)
         self.num_rows = int(N.lib().sb_plan_num_rows(h))
         self._torch = torch
 

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Builds decode-kernel variants as separate libraries for A/B timing
+# (select one with PA_AMD_LIB=pa_amd/variants/libsb_<name>.so).
+set -e
+cd "$(dirname "$0")/../pa_amd"
+make -s
+mkdir -p variants _build/variants
+build() {
+  name=$1; shift
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" -x hip -c csrc/sb_decode.hip -o _build/variants/$name.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o variants/libsb_$name.so _build/variants/$name.o _build/sb_api.cpp.o _build/sb_encode.cpp.o _build/sb_write_api.cpp.o -l:liblz4.so.1 -l:libzstd.so.1 -lpthread
+}
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  build $name $flags &
+done
+wait
+ls variants
