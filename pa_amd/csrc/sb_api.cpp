@@ -8,6 +8,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -32,6 +33,9 @@ struct sb_plan {
   sb::PageDesc* d_pages = nullptr;
   uint32_t* d_status = nullptr;
   uint32_t* d_lists = nullptr;  // [staged list | global list]
+  uint32_t* d_defer = nullptr;  // [count parity 0, count parity 1, work list...]
+  uint64_t decodes = 0;
+  int deferred_state = -1;  // -1 unknown, 0 no deferred pages, 1 some
   uint32_t n_staged = 0, n_global = 0;
   bool staged_identity = false;  // every page staged: no index list
   uint32_t stage_bytes = 0;
@@ -131,6 +135,7 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_pages) (void)hipFree(p->d_pages);
   if (p->d_status) (void)hipFree(p->d_status);
   if (p->d_lists) (void)hipFree(p->d_lists);
+  if (p->d_defer) (void)hipFree(p->d_defer);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   delete p;
@@ -189,6 +194,8 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
   if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&p->d_lists, np * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&p->d_defer, (np + 2) * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(p->d_defer, 0, 2 * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipEventCreate(&p->ev0);
   if (e == hipSuccess) e = hipEventCreate(&p->ev1);
   if (e == hipSuccess && n_pages) {
@@ -224,14 +231,26 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   a.nullable = p->desc.nullable;
   a.status = p->d_status;
   a.stage_bytes = p->stage_bytes;
+  a.defer_count = p->d_defer;
+  a.defer_list = p->d_defer + 2;
+  a.parity = (uint32_t)(p->decodes & 1);
+  p->decodes++;
   a.list = p->staged_identity ? nullptr : p->d_lists;
   a.n_list = p->n_staged;
-  if (sb::launch_decode_fixed(p->width, p->is_float, true, a, ctx->stream))
+  if (sb::launch_decode_fixed(p->width, p->is_float, 0, a, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "staged decode launch failed: %s", hipGetErrorString(hipGetLastError()));
   a.list = p->d_lists + p->n_staged;
   a.n_list = p->n_global;
-  if (sb::launch_decode_fixed(p->width, p->is_float, false, a, ctx->stream))
+  if (sb::launch_decode_fixed(p->width, p->is_float, 1, a, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "global decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (p->deferred_state != 0 && p->n_pages) {
+    // pages whose leaf stream is LZ4 / Zstd / Snappy / Patas, listed by the pass above
+    a.list = nullptr;
+    a.n_list = (uint32_t)std::min<uint64_t>(p->n_pages, sb::kDeferredGrid);
+    a.stage_bytes = sb::kDeferredLds;
+    if (sb::launch_decode_fixed(p->width, p->is_float, 2, a, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "deferred decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
   if (p->timing) {
     HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
     p->timed = true;
@@ -247,6 +266,11 @@ sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
   if (!p->n_pages) return SB_OK;
   std::vector<uint32_t> st(p->n_pages);
   HIP_TRY(ctx, hipMemcpy(st.data(), p->d_status, p->n_pages * 4, hipMemcpyDeviceToHost));
+  if (p->decodes && p->deferred_state == -1) {  // the plan's pages are fixed: learn once
+    uint32_t cnt = 0;
+    HIP_TRY(ctx, hipMemcpy(&cnt, p->d_defer + ((p->decodes - 1) & 1), 4, hipMemcpyDeviceToHost));
+    p->deferred_state = cnt ? 1 : 0;
+  }
   for (uint64_t i = 0; i < p->n_pages; i++) {
     if (st[i]) {
       if (bad) *bad = (int64_t)i;

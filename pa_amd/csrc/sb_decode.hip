@@ -147,6 +147,7 @@ struct Shared {
   Stream top;
   Stream sub;  // the leaf stream at the bottom of the cascade
   uint32_t chain;
+  uint32_t defer;
   // Dict
   uint32_t dict_k, dict_off;
   // Freq
@@ -613,12 +614,164 @@ __device__ bool parse_dict(const Src& s, Shared& sh, const Stream& st, uint32_t 
   return true;
 }
 
+
+// ---------------------------------------------------------------------------
+// general codecs and Patas, expanded into LDS by wave 0 (deferred pages)
+// ---------------------------------------------------------------------------
+// LZ4 raw block (basic.rs:87-91 -> liblz4 LZ4_decompress_safe with the exact
+// output size).  Tokens are parsed by every lane of the wave (uniform LDS
+// reads); literal and match bytes are copied lane-parallel.  A match copy
+// reads only bytes before `op`: byte i of a match is out[op - off + i % off].
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+__device__ uint32_t lz4_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, uint32_t olen) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t ip = 0, op = 0;
+  if (ilen == 0) return olen == 0 ? ST_OK : ST_CODEC;
+  for (;;) {
+    if (ip >= ilen) return ST_CODEC;
+    const uint32_t token = in[ip++];
+    uint32_t lit = token >> 4;
+    if (lit == 15) {
+      uint32_t b;
+      do {
+        if (ip >= ilen) return ST_CODEC;
+        b = in[ip++];
+        lit += b;
+      } while (b == 255);
+    }
+    if (lit > ilen - ip || lit > olen - op) return ST_CODEC;
+    for (uint32_t i = lane; i < lit; i += 64) out[op + i] = in[ip + i];
+    ip += lit;
+    op += lit;
+    if (ip == ilen) break;  // the last sequence carries literals only
+    if (ip + 2 > ilen) return ST_CODEC;
+    const uint32_t off = in[ip] | ((uint32_t)in[ip + 1] << 8);
+    ip += 2;
+    if (off == 0 || off > op) return ST_CODEC;
+    uint32_t ml = (token & 15) + 4;
+    if ((token & 15) == 15) {
+      uint32_t b;
+      do {
+        if (ip >= ilen) return ST_CODEC;
+        b = in[ip++];
+        ml += b;
+      } while (b == 255);
+    }
+    if (ml > olen - op) return ST_CODEC;
+    if (off >= ml) {
+      for (uint32_t i = lane; i < ml; i += 64) out[op + i] = out[op - off + i];
+    } else {
+      for (uint32_t i = lane; i < ml; i += 64) out[op + i] = out[op - off + i % off];
+    }
+    op += ml;
+  }
+  return op == olen ? ST_OK : ST_CODEC;
+}
+
+// Snappy raw (basic.rs:99-106, snap 1.1 raw::Decoder): varint length, then
+// literal / copy-1 / copy-2 / copy-4 elements.
+__device__ uint32_t snappy_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, uint32_t olen) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t ip = 0, op = 0;
+  uint64_t ulen = 0;
+  for (uint32_t sft = 0;; sft += 7) {
+    if (ip >= ilen || sft > 35) return ST_CODEC;
+    const uint32_t c = in[ip++];
+    ulen |= (uint64_t)(c & 0x7F) << sft;
+    if (!(c & 0x80)) break;
+  }
+  if (ulen != olen) return ST_CODEC;
+  while (ip < ilen) {
+    const uint32_t tag = in[ip++];
+    const uint32_t type = tag & 3;
+    if (type == 0) {
+      uint32_t len = (tag >> 2) + 1;
+      if (len > 60) {
+        const uint32_t nb = len - 60;
+        if (ip + nb > ilen) return ST_CODEC;
+        len = 0;
+        for (uint32_t i = 0; i < nb; i++) len |= (uint32_t)in[ip + i] << (8 * i);
+        len += 1;
+        ip += nb;
+      }
+      if (len > ilen - ip || len > olen - op) return ST_CODEC;
+      for (uint32_t i = lane; i < len; i += 64) out[op + i] = in[ip + i];
+      ip += len;
+      op += len;
+    } else {
+      uint32_t len, off;
+      if (type == 1) {
+        if (ip + 1 > ilen) return ST_CODEC;
+        len = ((tag >> 2) & 7) + 4;
+        off = ((tag >> 5) << 8) | in[ip];
+        ip += 1;
+      } else if (type == 2) {
+        if (ip + 2 > ilen) return ST_CODEC;
+        len = (tag >> 2) + 1;
+        off = in[ip] | ((uint32_t)in[ip + 1] << 8);
+        ip += 2;
+      } else {
+        if (ip + 4 > ilen) return ST_CODEC;
+        len = (tag >> 2) + 1;
+        off = in[ip] | ((uint32_t)in[ip + 1] << 8) | ((uint32_t)in[ip + 2] << 16) | ((uint32_t)in[ip + 3] << 24);
+        ip += 4;
+      }
+      if (off == 0 || off > op || len > olen - op) return ST_CODEC;
+      if (off >= len) {
+        for (uint32_t i = lane; i < len; i += 64) out[op + i] = out[op - off + i];
+      } else {
+        for (uint32_t i = lane; i < len; i += 64) out[op + i] = out[op - off + i % off];
+      }
+      op += len;
+    }
+  }
+  return op == olen ? ST_OK : ST_CODEC;
+}
+
+// Patas (double/patas.rs:107-132): first value raw, then per value a u16
+// (ref_diff 7b | sig_bytes 3b | tz 6b; sig 0 => 8 when tz < 63) and sig
+// bytes; value = (v << tz) ^ out[i - ref_diff].  Serial (lane 0).
+template <int W>
+__device__ uint32_t patas_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, uint32_t n) {
+  using T = typename VT<W>::T;
+  if ((threadIdx.x & 63) != 0) return ST_OK;
+  if (n == 0) return ST_OUT_OF_SPEC;  // `length - 1` underflows (patas.rs:117)
+  if (ilen < W) return ST_IO;
+  __attribute__((address_space(3))) T* o = (__attribute__((address_space(3))) T*)out;
+  T first = 0;
+  for (int b = 0; b < W; b++) first |= (T)in[b] << (8 * b);
+  o[0] = first;
+  uint32_t p = W;
+  for (uint32_t i = 1; i < n; i++) {
+    if (p + 2 > ilen) return ST_IO;
+    const uint32_t packed = in[p] | ((uint32_t)in[p + 1] << 8);
+    p += 2;
+    const uint32_t rd = (packed >> 9) & 0x7F, tz = packed & 0x3F;
+    uint32_t sb = (packed >> 6) & 7;
+    if (tz < 63 && sb == 0) sb = 8;
+    if (sb > (uint32_t)W) return ST_OUT_OF_SPEC;  // the f32 desync (patas.rs:154-160)
+    if (p + sb > ilen) return ST_IO;
+    uint64_t v = 0;
+    for (uint32_t b = 0; b < sb; b++) v |= (uint64_t)in[p + b] << (8 * b);
+    p += sb;
+    if (rd == 0 || rd > i) return ST_OUT_OF_SPEC;
+    const T sh = tz >= 8 * W ? (T)0 : (T)((T)v << tz);
+    o[i] = sh ^ o[i - rd];
+  }
+  return ST_OK;
+}
+
 // Cascade shapes the writer produces (Dict forbids Dict below it, Freq forbids
 // Freq: dict.rs:60-62, freq.rs:79-83).
 enum : uint32_t { CH_LEAF = 0, CH_DICT = 1, CH_FREQ = 2, CH_DICT_FREQ = 3, CH_FREQ_DICT = 4 };
 
-template <int W, bool FLT, class Src>
-__device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const LaunchArgs& a) {
+// MODE 0: main pass (general-codec / Patas leaves are deferred to a work
+// list); MODE 1: deferred pass (the leaf is expanded into LDS at `xpos`,
+// xcap bytes available, then decoded as a plain stream).
+template <int W, bool FLT, int MODE, class Src>
+__device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const LaunchArgs& a, uint32_t page,
+                            uint8_t* xbuf = nullptr, uint32_t xpos = 0, uint32_t xcap = 0) {
   using T = typename VT<W>::T;
   const uint32_t tid = threadIdx.x;
   const uint32_t len = pd.byte_len, n = pd.num_values;
@@ -686,10 +839,45 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
       sh.top = st;
       sh.sub = inner;
       sh.chain = chain;
+      sh.defer = 0;
+      if (inner.codec == 1 || inner.codec == 2 || inner.codec == 3 || inner.codec == 16) {
+        if (MODE == 0) {
+          sh.defer = 1;
+          const uint32_t slot = atomicAdd(a.defer_count + a.parity, 1u);
+          a.defer_list[slot] = page;
+        }
+      }
     } while (0);
   }
   __syncthreads();
-  if (sh.err) return;
+  if (sh.err || sh.defer) return;
+
+  if constexpr (MODE == 1) {
+    Stream lf = sh.sub;
+    if (lf.codec == 1 || lf.codec == 2 || lf.codec == 3 || lf.codec == 16) {
+      const bool idx_stream = sh.chain == CH_DICT || sh.chain == CH_FREQ_DICT || sh.chain == CH_DICT_FREQ;
+      const uint32_t sw = idx_stream ? 4u : (uint32_t)W;
+      const uint64_t bytes = (uint64_t)lf.n * sw;
+      if (bytes > xcap) {
+        if (tid == 0) set_err(sh, ST_NYI);  // decompressed stream larger than the LDS budget
+      } else if (tid < 64) {
+        const lds_u8* in = (const lds_u8*)((const uint8_t*)s.w + s.base + lf.body);
+        lds_u8* xo = (lds_u8*)xbuf;
+        uint32_t st = ST_OK;
+        if (lf.codec == 1) st = lz4_expand(in, lf.csize, xo, (uint32_t)bytes);
+        else if (lf.codec == 3) st = snappy_expand(in, lf.csize, xo, (uint32_t)bytes);
+        else if (lf.codec == 16) {
+          if (!FLT || idx_stream) st = ST_OUT_OF_SPEC;  // Patas only in decompress_double
+          else st = patas_expand<W>(in, lf.csize, xo, lf.n);
+        } else st = ST_NYI;  // Zstd: host-only for now
+        if (st) set_err(sh, st);
+      }
+      __syncthreads();
+      if (sh.err) return;
+      if (tid == 0) sh.sub = Stream{0u, xpos - s.base, (uint32_t)bytes, lf.n};
+      __syncthreads();
+    }
+  }
 
   if (sh.has_valid) write_validity(s, sh.vb_pos, n, pd.row_off, a.out_validity);
 
@@ -759,18 +947,11 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
   }
 }
 
-template <int W, bool FLT>
-__global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
-  extern __shared__ u32x4 stage[];
-  __shared__ Shared sh;
-  const uint32_t page = a.list ? a.list[blockIdx.x] : blockIdx.x;
-  const PageDesc pd = a.pages[page];
-  if (threadIdx.x == 0) sh.err = 0;
-  // stage the page: aligned 16-byte loads covering [pg, pg + len)
-  const uint8_t* pg = a.chunk + pd.byte_off;
+// Stage [pg, pg + len) into LDS with aligned 16-byte pieces.
+__device__ __forceinline__ uint32_t stage_page(u32x4* stage, const uint8_t* pg, uint32_t len) {
   const uintptr_t a0 = (uintptr_t)pg & ~(uintptr_t)15;
   const uint32_t base = (uint32_t)((uintptr_t)pg & 15);
-  const uint32_t nchunks = (base + pd.byte_len + 15) >> 4;
+  const uint32_t nchunks = (base + len + 15) >> 4;
   const u32x4* gsrc = (const u32x4*)a0;
 #if SB_LDS_DMA
   {  // LDS-DMA: each wave instruction lands 64 x 16 B contiguously at the wave's LDS base
@@ -792,10 +973,24 @@ __global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
   }
 #endif
   __syncthreads();
+  return base;
+}
+
+template <int W, bool FLT>
+__global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
+  extern __shared__ u32x4 stage[];
+  __shared__ Shared sh;
+  const uint32_t page = a.list ? a.list[blockIdx.x] : blockIdx.x;
+  const PageDesc pd = a.pages[page];
+  if (threadIdx.x == 0) {
+    sh.err = 0;
+    if (blockIdx.x == 0) a.defer_count[a.parity ^ 1] = 0;  // the next decode's work list
+  }
+  const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
   LdsSrc s{(const uint32_t*)stage, base};
-  decode_page<W, FLT>(s, sh, pd, a);
+  decode_page<W, FLT, 0>(s, sh, pd, a, page);
   __syncthreads();
-  if (threadIdx.x == 0) a.status[page] = sh.err;
+  if (threadIdx.x == 0 && !sh.defer) a.status[page] = sh.err;
 }
 
 template <int W, bool FLT>
@@ -805,17 +1000,56 @@ __global__ __launch_bounds__(NT) void k_decode_global(LaunchArgs a) {
   const PageDesc pd = a.pages[page];
   if (threadIdx.x == 0) sh.err = 0;
   __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x == 0) a.defer_count[a.parity ^ 1] = 0;
   GlbSrc s{a.chunk + pd.byte_off};
-  decode_page<W, FLT>(s, sh, pd, a);
+  decode_page<W, FLT, 0>(s, sh, pd, a, page);
   __syncthreads();
-  if (threadIdx.x == 0) a.status[page] = sh.err;
+  if (threadIdx.x == 0 && !sh.defer) a.status[page] = sh.err;
+}
+
+// Deferred pages (general codecs, Patas): one workgroup per listed page, the
+// page and its expanded leaf stream both in LDS (a.stage_bytes in total).
+template <int W, bool FLT>
+__global__ __launch_bounds__(NT) void k_decode_deferred(LaunchArgs a) {
+  extern __shared__ u32x4 stage[];
+  __shared__ Shared sh;
+  const uint32_t count = a.defer_count[a.parity];
+  for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+    const uint32_t page = a.defer_list[i];
+    const PageDesc pd = a.pages[page];
+    if (threadIdx.x == 0) sh.err = 0;
+    const uint32_t need = ((pd.byte_len + 15 + kStagePad + 15) & ~15u);
+    if (need + 64 > a.stage_bytes) {  // page too large for the deferred LDS budget
+      __syncthreads();
+      if (threadIdx.x == 0) a.status[page] = ST_NYI;
+      continue;
+    }
+    const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
+    LdsSrc s{(const uint32_t*)stage, base};
+    uint8_t* xbuf = (uint8_t*)stage + need;
+    decode_page<W, FLT, 1>(s, sh, pd, a, page, xbuf, need, a.stage_bytes - need - kStagePad);
+    __syncthreads();
+    if (threadIdx.x == 0) a.status[page] = sh.err;
+    __syncthreads();
+  }
 }
 
 template <int W, bool FLT>
-static int launch(bool staged, const LaunchArgs& a, hipStream_t stream) {
+static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
+  dim3 block(NT);
+  if (kind == 2) {
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)k_decode_deferred<W, FLT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)a.stage_bytes);
+      attr = true;
+    }
+    hipLaunchKernelGGL((k_decode_deferred<W, FLT>), dim3(a.n_list), block, a.stage_bytes, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   if (a.n_list == 0) return 0;
-  dim3 grid(a.n_list), block(NT);
-  if (staged) {
+  dim3 grid(a.n_list);
+  if (kind == 0) {
     hipLaunchKernelGGL((k_decode_staged<W, FLT>), grid, block, a.stage_bytes, stream, a);
   } else {
     hipLaunchKernelGGL((k_decode_global<W, FLT>), grid, block, 0, stream, a);
@@ -826,18 +1060,18 @@ static int launch(bool staged, const LaunchArgs& a, hipStream_t stream) {
 }  // namespace sbk
 
 namespace sb {
-int launch_decode_fixed(int width, bool is_float, bool staged, const LaunchArgs& a, void* stream) {
+int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (is_float) {
-    if (width == 4) return sbk::launch<4, true>(staged, a, s);
-    if (width == 8) return sbk::launch<8, true>(staged, a, s);
+    if (width == 4) return sbk::launch<4, true>(kind, a, s);
+    if (width == 8) return sbk::launch<8, true>(kind, a, s);
     return -2;
   }
   switch (width) {
-    case 1: return sbk::launch<1, false>(staged, a, s);
-    case 2: return sbk::launch<2, false>(staged, a, s);
-    case 4: return sbk::launch<4, false>(staged, a, s);
-    case 8: return sbk::launch<8, false>(staged, a, s);
+    case 1: return sbk::launch<1, false>(kind, a, s);
+    case 2: return sbk::launch<2, false>(kind, a, s);
+    case 4: return sbk::launch<4, false>(kind, a, s);
+    case 8: return sbk::launch<8, false>(kind, a, s);
   }
   return -2;
 }

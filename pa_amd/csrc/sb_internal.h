@@ -42,9 +42,17 @@ struct LaunchArgs {
   uint32_t* out_validity;  // 32-bit words of the Arrow bitmap
   int nullable;
   uint32_t* status;
-  uint32_t stage_bytes;  // dynamic LDS (staged launch only)
+  uint32_t stage_bytes;  // dynamic LDS (staged / deferred launches)
+  uint32_t* defer_count;  // [2]: work-list lengths, double-buffered by decode parity
+  uint32_t* defer_list;   // page indices deferred to k_decode_deferred
+  uint32_t parity;
 };
 
-int launch_decode_fixed(int width, bool is_float, bool staged, const LaunchArgs& a, void* stream);
+// kind: 0 = LDS-staged pages, 1 = pages read from HBM, 2 = deferred work list
+int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a, void* stream);
+
+// dynamic LDS of the deferred pass: page + expanded stream
+constexpr uint32_t kDeferredLds = 150 * 1024;
+constexpr uint32_t kDeferredGrid = 1024;
 
 }  // namespace sb

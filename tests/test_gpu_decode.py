@@ -59,6 +59,10 @@ OPTS = {
     "force_dict": dict(ratio=2.0, forced=O.DICT),
     "force_rle": dict(ratio=2.0, forced=O.RLE),
     "force_bp": dict(ratio=2.0, forced=O.BITPACKING),
+    "lz4": dict(ratio=None, default_codec=O.LZ4),
+    "lz4_adaptive": dict(ratio=1.2, default_codec=O.LZ4),
+    "snappy": dict(ratio=None, default_codec=O.SNAPPY),
+    "snappy_dict": dict(ratio=2.0, default_codec=O.SNAPPY, forced=O.DICT),
 }
 
 INT_TYPES = [np.int32, np.uint32, np.int64, np.uint64, np.int8, np.uint8, np.int16, np.uint16]
@@ -82,7 +86,8 @@ def test_int_columns(ctx, dtype, opt, nullable):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64], ids=lambda d: np.dtype(d).name)
-@pytest.mark.parametrize("opt", ["plain", "adaptive12", "adaptive20", "force_freq", "force_dict", "force_rle"])
+@pytest.mark.parametrize("opt", ["plain", "adaptive12", "adaptive20", "force_freq", "force_dict", "force_rle",
+                                 "lz4", "lz4_adaptive", "snappy"])
 @pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
 def test_float_columns(ctx, dtype, opt, nullable):
     rng = np.random.default_rng(7)
@@ -182,3 +187,49 @@ def test_malformed_pages_report_errors(ctx):
     for bad in (bad_codec, truncated, wide):
         with pytest.raises(pa_amd.StrawboatError):
             gpu_decode(ctx, bytes(bad), [(len(bad), 8192)], np.uint32, False)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32], ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+def test_patas(ctx, dtype, nullable):
+    """Patas pages (double/patas.rs:107-132): slowly varying values, repeats
+    (f64 only: the reference's f32 repeat desync), nulls."""
+    rng = np.random.default_rng(21)
+    n = 20000
+    v = (np.cumsum(rng.standard_normal(n)) * 10).astype(dtype)
+    if dtype == np.float64:
+        v[::7] = v[::7][0]  # exact repeats -> reference back-references
+    else:
+        v = v + np.arange(n, dtype=dtype) * dtype(1e-3)  # no exact repeats
+    validity = (rng.random(n) > 0.2) if nullable else None
+    opts = O.WriteOptions.make(ratio=1.0, forced=O.PATAS)
+    codecs = check(ctx, v, validity, nullable, 2048, opts)
+    assert set(codecs) == {O.PATAS}
+    # Patas also under Freq exceptions of a double column
+    f = np.where(rng.random(n) < 0.93, dtype(2.5), v)
+    check(ctx, f, validity, nullable, 4096, O.WriteOptions.make(ratio=1.0, forced=O.FREQ))
+
+
+def test_lz4_compressible_and_long_matches(ctx):
+    """LZ4 pages with many short matches, overlapping matches (offset < length)
+    and long literal runs."""
+    rng = np.random.default_rng(8)
+    for v in [np.repeat(rng.integers(0, 1000, 3000), 7)[:20000].astype(np.int64),
+              np.tile(np.arange(3, dtype=np.int32), 7000),
+              rng.integers(-2**31, 2**31 - 1, 20000).astype(np.int32),
+              np.zeros(20000, np.int8)]:
+        for dc in (O.LZ4, O.SNAPPY):
+            check(ctx, v, None, False, 8192, O.WriteOptions.make(default_codec=dc))
+            check(ctx, v, rng.random(len(v)) > 0.5, True, 2048, O.WriteOptions.make(default_codec=dc))
+
+
+def test_zstd_pages_report_nyi(ctx):
+    """Zstd is not on the device yet: its pages report NotYetImplemented
+    (never a wrong answer)."""
+    import pa_amd
+
+    v = np.arange(5000, dtype=np.int32)
+    chunk, metas, _ = build_column(v, None, False, 2048, O.WriteOptions.make(default_codec=O.ZSTD))
+    with pytest.raises(pa_amd.StrawboatError) as e:
+        gpu_decode(ctx, chunk, metas, np.int32, False)
+    assert e.value.status == 2
