@@ -64,6 +64,10 @@ typedef enum {
   SB_T_UINT64 = 8,
   SB_T_FLOAT32 = 9,
   SB_T_FLOAT64 = 10,
+  SB_T_BINARY = 11,       /* i32 offsets */
+  SB_T_LARGE_BINARY = 12, /* i64 offsets */
+  SB_T_UTF8 = 13,         /* i32 offsets (bytes; UTF-8 validation is the caller's) */
+  SB_T_LARGE_UTF8 = 14,   /* i64 offsets */
 } sb_physical_type;
 
 /* PageMeta (src/lib.rs:75-80): compressed page length and num_values. */
@@ -89,6 +93,16 @@ typedef struct {
   void* d_values;
   uint8_t* d_validity;
 } sb_primitive_out;
+
+/* Output buffers of a Binary / Utf8 column (caller-allocated, device):
+ * offsets: (sum(num_values) + 1) offsets of 4 (Binary/Utf8) or 8 (Large*)
+ * bytes; values: sb_plan_values_bytes() bytes; validity as above. */
+typedef struct {
+  void* d_offsets;
+  uint8_t* d_values;
+  uint64_t values_capacity;
+  uint8_t* d_validity;
+} sb_binary_out;
 
 typedef struct sb_ctx sb_ctx;
 typedef struct sb_plan sb_plan;
@@ -125,6 +139,13 @@ uint64_t sb_plan_num_pages(const sb_plan* plan);
  * read/array/double.rs:210-238) as driven by batch_read_array
  * (read/batch_read.rs:190-209): validity + values of every page, appended. */
 sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* plan, const sb_primitive_out* out);
+
+/* Binary / Utf8 columns (read_binary, read/array/binary.rs:223-265; pages via
+ * decompress_binary, compression/binary/mod.rs:95-183).  For these types
+ * sb_plan_column also sizes every page's values on the device (synchronous)
+ * and fails with the first bad page's status. */
+uint64_t sb_plan_values_bytes(const sb_plan* plan);
+sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* plan, const sb_binary_out* out);
 
 /* Waits for the plan's last decode and returns the first failing page's
  * status (SB_OK if every page decoded); *h_bad_page = its index or -1. */
@@ -185,6 +206,15 @@ sb_status sb_encode_column(int32_t physical_type, const void* h_values, const ui
                            uint64_t n_rows, int32_t nullable, const sb_write_options* opts,
                            uint64_t max_page_rows, int32_t n_threads, uint8_t** h_out, uint64_t* out_len,
                            sb_page_meta** h_metas, uint64_t* n_pages);
+/* encode_chunk for one Binary / Utf8 leaf (serialize.rs:64-110 ->
+ * compress_binary, compression/binary/mod.rs:26-93): h_offsets holds
+ * n_rows + 1 absolute positions into h_values (values_len bytes, the
+ * array's whole buffer, which the reference's stats and Extend header use). */
+sb_status sb_encode_binary_column(int32_t physical_type, const uint8_t* h_values, uint64_t values_len,
+                                  const int64_t* h_offsets, const uint8_t* h_validity, uint64_t n_rows,
+                                  int32_t nullable, const sb_write_options* opts, uint64_t max_page_rows,
+                                  int32_t n_threads, uint8_t** h_out, uint64_t* out_len, sb_page_meta** h_metas,
+                                  uint64_t* n_pages);
 uint64_t sb_page_seed(uint64_t seed, uint64_t page);
 /* NativeWriter::finish (write/writer.rs:128-167) footer bytes. */
 sb_status sb_write_footer(const uint8_t* h_schema, uint64_t schema_len, const uint64_t* h_col_offsets,

@@ -287,3 +287,147 @@ def read_column(chunk: bytes, metas, dtype, nullable=False):
     rc = lib().orc_read_column(_ptr(src), len(chunk), _ptr(m), len(metas), kind, dtype.itemsize, int(nullable), _ptr(out), _ptr(bits))
     _check(rc, "read_column")
     return out[:n], (np.unpackbits(bits, bitorder="little")[:n].astype(bool) if nullable else None)
+
+
+# ---- binary / utf8 ------------------------------------------------------------
+class _BinVec(ctypes.Structure):
+    _fields_ = [("offsets", ctypes.POINTER(ctypes.c_int64)), ("n_off", ctypes.c_size_t), ("cap_off", ctypes.c_size_t),
+                ("values", ctypes.POINTER(ctypes.c_uint8)), ("n_val", ctypes.c_size_t), ("cap_val", ctypes.c_size_t)]
+
+
+def _bin_lib():
+    L = lib()
+    if not getattr(L, "_bin_ready", False):
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.orc_binvec_free.argtypes = [ctypes.POINTER(_BinVec)]
+        L.orc_read_binary_page.argtypes = [P, S, S, I, I, ctypes.POINTER(_BinVec), P]
+        L.orc_write_binary_page.argtypes = [P, P, P, S, I, I, ctypes.c_uint64, ctypes.POINTER(WriteOptions), ctypes.POINTER(_Buf)]
+        L._bin_ready = True
+    return L
+
+
+def strings_to_arrow(strings):
+    """list of bytes -> (values bytes, int64 offsets n+1)."""
+    offs = np.zeros(len(strings) + 1, np.int64)
+    offs[1:] = np.cumsum([len(s) for s in strings])
+    return b"".join(strings), offs
+
+
+def write_binary_page(values: bytes, offsets: np.ndarray, validity=None, nullable=False, opts=None,
+                      offset_width=4, parent_values_len=None) -> bytes:
+    """write_simple for Binary/Utf8 (serialize.rs:64-110) over rows
+    offsets[0..n]; parent_values_len = the array's whole values buffer."""
+    L = _bin_lib()
+    opts = opts or WriteOptions.make()
+    n = len(offsets) - 1
+    offs = np.ascontiguousarray(offsets, np.int64)
+    vals = np.frombuffer(values, np.uint8) if values else np.zeros(1, np.uint8)
+    vb = None if validity is None else np.packbits(np.asarray(validity, bool), bitorder="little")
+    buf = _Buf()
+    pl = len(values) if parent_values_len is None else parent_values_len
+    rc = L.orc_write_binary_page(_ptr(vals), _ptr(offs), _ptr(vb), n, offset_width, int(nullable), pl, ctypes.byref(opts), ctypes.byref(buf))
+    data = _take(buf)
+    _check(rc, "write_binary_page")
+    return data
+
+
+def read_binary_column(chunk: bytes, metas, nullable=False, offset_width=4):
+    """read_binary (read/array/binary.rs:223-265): pages appended -> (offsets
+    int64 array of n+1, values bytes, validity|None)."""
+    L = _bin_lib()
+    src = np.frombuffer(chunk, np.uint8) if chunk else np.zeros(1, np.uint8)
+    bv = _BinVec()
+    valid = []
+    pos = 0
+    try:
+        for length, nv in metas:
+            bits = np.zeros((nv + 7) // 8 + 1, np.uint8)
+            page = src[pos:pos + length]
+            rc = L.orc_read_binary_page(_ptr(np.ascontiguousarray(page)), length, nv, int(nullable), offset_width, ctypes.byref(bv), _ptr(bits))
+            _check(rc, "read_binary_page")
+            if nullable:
+                valid.append(np.unpackbits(bits, bitorder="little")[:nv].astype(bool))
+            pos += length
+        offs = np.ctypeslib.as_array(bv.offsets, shape=(bv.n_off,)).copy() if bv.n_off else np.zeros(0, np.int64)
+        vals = ctypes.string_at(bv.values, bv.n_val) if bv.n_val else b""
+    finally:
+        L.orc_binvec_free(ctypes.byref(bv))
+    return offs, vals, (np.concatenate(valid) if nullable and valid else None)
+
+
+# ---- nested List<primitive> ---------------------------------------------------
+def _list_lib():
+    L = lib()
+    if not getattr(L, "_list_ready", False):
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.orc_write_list_page.argtypes = [P, P, S, I, P, P, I, I, I, I, ctypes.POINTER(WriteOptions), ctypes.POINTER(_Buf),
+                                          ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_read_list_page.argtypes = [P, S, S, I, I, I, I, P, P, P, P, ctypes.POINTER(S), ctypes.POINTER(S)]
+        L._list_ready = True
+    return L
+
+
+def write_list_column(offsets, list_validity, child, child_validity, list_nullable, item_nullable, page_rows, opts=None):
+    """encode_chunk for one List<T> leaf: pages of page_rows top-level rows;
+    returns (chunk, [(length, num_levels)], [rows per page])."""
+    L = _list_lib()
+    opts = opts or WriteOptions.make()
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    child = np.ascontiguousarray(child)
+    rows = len(offsets) - 1
+    lvb = None if list_validity is None else np.packbits(np.asarray(list_validity, bool), bitorder="little")
+    cvb = None if child_validity is None else np.packbits(np.asarray(child_validity, bool), bitorder="little")
+    kind = 1 if child.dtype.kind == "f" else 0
+    pages, metas, prow = [], [], []
+    step = page_rows or max(rows, 1)
+    for r0 in range(0, rows, step):
+        m = min(step, rows - r0)
+        sub_lv = None
+        if lvb is not None:
+            sub_lv = np.packbits(np.asarray(list_validity, bool)[r0:r0 + m], bitorder="little")
+        buf = _Buf()
+        nlev = ctypes.c_uint64()
+        rc = L.orc_write_list_page(_ptr(offsets[r0:r0 + m + 1].copy()), _ptr(sub_lv), m, int(list_nullable),
+                                   _ptr(child), _ptr(cvb), int(item_nullable), kind, child.itemsize,
+                                   int(child.dtype.kind == "i"), ctypes.byref(opts), ctypes.byref(buf), ctypes.byref(nlev))
+        pg = _take(buf)
+        _check(rc, "write_list_page")
+        pages.append(pg)
+        metas.append((len(pg), nlev.value))
+        prow.append(m)
+    return b"".join(pages), metas, prow
+
+
+def read_list_column(chunk, metas, dtype, list_nullable, item_nullable):
+    """batch read of a List<T> leaf: per page create_list, then concatenate
+    -> (offsets int64 rows+1, list validity|None, values, leaf validity|None)."""
+    L = _list_lib()
+    dtype = np.dtype(dtype)
+    src = np.frombuffer(chunk, np.uint8)
+    offs_all, lv_all, vals_all, leafv_all = [np.zeros(1, np.int64)], [], [], []
+    base = 0
+    pos = 0
+    kind = 1 if dtype.kind == "f" else 0
+    for length, nlev in metas:
+        page = np.ascontiguousarray(src[pos:pos + length])
+        offs = np.zeros(nlev + 1, np.int64)
+        lbits = np.zeros(nlev // 8 + 2, np.uint8)
+        vals = np.zeros(nlev + 1, dtype)
+        fbits = np.zeros(nlev // 8 + 2, np.uint8)
+        nr, nleaf = ctypes.c_size_t(), ctypes.c_size_t()
+        rc = L.orc_read_list_page(_ptr(page), length, nlev, int(list_nullable), int(item_nullable), kind, dtype.itemsize,
+                                  _ptr(offs), _ptr(lbits), _ptr(vals), _ptr(fbits), ctypes.byref(nr), ctypes.byref(nleaf))
+        _check(rc, "read_list_page")
+        r, v = nr.value, nleaf.value
+        offs_all.append(offs[1:r].copy() + base)
+        offs_all.append(np.array([v + base], np.int64))
+        base += v
+        if list_nullable:
+            lv_all.append(np.unpackbits(lbits, bitorder="little")[:r].astype(bool))
+        vals_all.append(vals[:v])
+        if item_nullable:
+            leafv_all.append(np.unpackbits(fbits, bitorder="little")[:v].astype(bool))
+        pos += length
+    offsets = np.concatenate(offs_all)
+    return (offsets, np.concatenate(lv_all) if list_nullable else None, np.concatenate(vals_all),
+            np.concatenate(leafv_all) if item_nullable else None)

@@ -1295,3 +1295,524 @@ int orc_read_column(const uint8_t* chunk, size_t len, const uint64_t* metas, siz
   free(tmp);
   return ORC_OK;
 }
+
+/* ======================================================================= */
+/* binary / utf8 pages (compression/binary/{mod,dict,freq,one_value}.rs)     */
+/* ======================================================================= */
+
+static int bin_push_off(orc_binvec* o, int64_t v) {
+  if (o->n_off == o->cap_off) {
+    size_t nc = o->cap_off ? 2 * o->cap_off : 1024;
+    int64_t* p = (int64_t*)realloc(o->offsets, nc * sizeof(int64_t));
+    if (!p) return -1;
+    o->offsets = p;
+    o->cap_off = nc;
+  }
+  o->offsets[o->n_off++] = v;
+  return 0;
+}
+
+static int bin_push_vals(orc_binvec* o, const uint8_t* p, size_t n) {
+  if (o->n_val + n > o->cap_val) {
+    size_t nc = o->cap_val ? o->cap_val : 4096;
+    while (nc < o->n_val + n) nc *= 2;
+    uint8_t* q = (uint8_t*)realloc(o->values, nc);
+    if (!q) return -1;
+    o->values = q;
+    o->cap_val = nc;
+  }
+  if (n) memcpy(o->values + o->n_val, p, n);
+  o->n_val += n;
+  return 0;
+}
+
+void orc_binvec_free(orc_binvec* o) {
+  free(o->offsets);
+  free(o->values);
+  memset(o, 0, sizeof(*o));
+}
+
+static int64_t ld_off(const uint8_t* p, int ow) { return ow == 8 ? (int64_t)rd_u64(p) : (int64_t)(int32_t)rd_u32(p); }
+
+/* decompress_binary (binary/mod.rs:95-183): appends `length` rows to `o`
+ * exactly as the reference's Vec<O> / Vec<u8> pair grows. */
+int orc_decompress_binary(const uint8_t* buf, size_t len, size_t* pos, size_t length, int ow, orc_binvec* o) {
+  int codec;
+  size_t csize, usize;
+  int rc = read_header(buf, len, pos, &codec, &csize, &usize);
+  if (rc) return rc;
+  const uint8_t* body = buf + *pos;
+  if (codec <= ORC_SNAPPY) {
+    /* Basic: offsets stream ((length+1) offsets), then values stream decoded
+     * with the SAME codec (the second header's codec byte is not read) */
+    size_t ob = (length + 1) * (size_t)ow;
+    uint8_t* tmp = (uint8_t*)malloc(ob ? ob : 1);
+    rc = orc_common_decompress(codec, body, csize, tmp, ob);
+    if (rc) { free(tmp); return rc; }
+    *pos += csize;
+    int had = o->n_off > 0;
+    int64_t last = had ? o->offsets[o->n_off - 1] : 0;
+    for (size_t i = 0; i <= length; i++) bin_push_off(o, ld_off(tmp + i * ow, ow));
+    free(tmp);
+    if (had) { /* "fix offset" (mod.rs:136-144): o[i] = last + o[i+1], drop one */
+      size_t s = o->n_off - length - 1;
+      for (size_t i = s; i + 1 < o->n_off; i++) o->offsets[i] = last + o->offsets[i + 1];
+      o->n_off--;
+    }
+    size_t vcs, vus;
+    int vcodec;
+    rc = read_header(buf, len, pos, &vcodec, &vcs, &vus);
+    if (rc) return rc;
+    (void)vcodec;
+    uint8_t* vt = (uint8_t*)malloc(vus ? vus : 1);
+    rc = orc_common_decompress(codec, buf + *pos, vcs, vt, vus);
+    if (!rc) bin_push_vals(o, vt, vus);
+    free(vt);
+    if (rc) return rc;
+    *pos += vcs;
+    return ORC_OK;
+  }
+  size_t p = 0;
+  const uint8_t* in = body;
+  size_t n = csize;
+  if (codec == ORC_ONE_VALUE) { /* one_value.rs:71-99 */
+    if (n < 4) return ORC_E_IO;
+    uint32_t l = rd_u32(in);
+    if (n - 4 < l) return ORC_E_OUT_OF_SPEC;
+    if (o->n_off == 0) bin_push_off(o, 0);
+    for (size_t i = 0; i < length; i++) {
+      bin_push_vals(o, in + 4, l);
+      bin_push_off(o, (int64_t)o->n_val);
+    }
+  } else if (codec == ORC_DICT) { /* dict.rs:95-141 */
+    uint32_t* idx = (uint32_t*)malloc((length ? length : 1) * 4);
+    rc = decompress_stream(in, n, &p, 4, length, (uint8_t*)idx, 0);
+    if (rc) { free(idx); return rc; }
+    if (p + 4 > n) { free(idx); return ORC_E_IO; }
+    uint32_t k = rd_u32(in + p);
+    p += 4;
+    size_t* eoff = (size_t*)malloc(((size_t)k + 1) * sizeof(size_t));
+    uint64_t* elen = (uint64_t*)malloc(((size_t)k + 1) * sizeof(uint64_t));
+    for (uint32_t e = 0; e < k; e++) {
+      if (p + 8 > n) { free(idx); free(eoff); free(elen); return ORC_E_IO; }
+      uint64_t l = rd_u64(in + p);
+      p += 8;
+      if (n - p < l) { free(idx); free(eoff); free(elen); return ORC_E_OUT_OF_SPEC; }
+      eoff[e] = p;
+      elen[e] = l;
+      p += (size_t)l;
+    }
+    int64_t last;
+    if (o->n_off == 0) { bin_push_off(o, 0); last = 0; }
+    else last = o->offsets[o->n_off - 1];
+    for (size_t i = 0; i < length; i++) {
+      if (idx[i] >= k) { free(idx); free(eoff); free(elen); return ORC_E_OUT_OF_SPEC; }
+      bin_push_vals(o, in + eoff[idx[i]], (size_t)elen[idx[i]]);
+      last += (int64_t)elen[idx[i]];
+      bin_push_off(o, last);
+    }
+    free(idx); free(eoff); free(elen);
+  } else if (codec == ORC_FREQ) { /* freq.rs:102-145 */
+    if (n < 8) return ORC_E_IO;
+    uint64_t tl = rd_u64(in);
+    p = 8;
+    if (n - p < tl) return ORC_E_OUT_OF_SPEC;
+    const uint8_t* top = in + p;
+    p += (size_t)tl;
+    if (p + 4 > n) return ORC_E_IO;
+    uint32_t bm = rd_u32(in + p);
+    p += 4;
+    if (n - p < bm) return ORC_E_IO;
+    size_t cnt;
+    rc = orc_roaring_decode(in + p, bm, NULL, 0, &cnt);
+    if (rc) return rc;
+    uint32_t* pos_e = (uint32_t*)malloc((cnt ? cnt : 1) * 4);
+    orc_roaring_decode(in + p, bm, pos_e, cnt, &cnt);
+    p += bm;
+    if (o->n_off == 0) bin_push_off(o, 0);
+    size_t e = 0;
+    for (size_t i = 0; i < length; i++) {
+      while (e < cnt && pos_e[e] < i) e++; /* contains(i) on ascending positions */
+      if (e < cnt && pos_e[e] == i) {
+        if (p + 8 > n) { free(pos_e); return ORC_E_IO; }
+        uint64_t l = rd_u64(in + p);
+        p += 8;
+        if (n - p < l) { free(pos_e); return ORC_E_OUT_OF_SPEC; }
+        bin_push_vals(o, in + p, (size_t)l);
+        p += (size_t)l;
+      } else {
+        bin_push_vals(o, top, (size_t)tl);
+      }
+      bin_push_off(o, (int64_t)o->n_val);
+    }
+    free(pos_e);
+  } else {
+    return ORC_E_OUT_OF_SPEC;
+  }
+  *pos += csize;
+  return ORC_OK;
+}
+
+/* ---- binary encoder (compress_binary, binary/mod.rs:26-93) ---- */
+typedef struct {
+  const uint8_t* values;
+  const int64_t* offsets; /* n+1 absolute */
+  const uint8_t* validity;
+  size_t n;
+  int ow;
+  uint64_t parent_values_len;
+} barr_t;
+
+static uint64_t fnv1a(const uint8_t* p, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; }
+  return h;
+}
+
+/* string hash set: returns entry id (first occurrence order) */
+typedef struct {
+  uint64_t* h;
+  uint32_t* id;
+  uint32_t* cnt;
+  uint8_t* used;
+  size_t cap;
+  size_t* srow; /* representative row of id */
+  size_t n_ids;
+} smap;
+
+static void smap_init(smap* m, size_t n) {
+  size_t cap = 16;
+  while (cap < 2 * n + 16) cap <<= 1;
+  m->cap = cap;
+  m->h = (uint64_t*)malloc(cap * 8);
+  m->id = (uint32_t*)malloc(cap * 4);
+  m->cnt = (uint32_t*)malloc(cap * 4);
+  m->used = (uint8_t*)calloc(cap, 1);
+  m->srow = (size_t*)malloc((n + 1) * sizeof(size_t));
+  m->n_ids = 0;
+}
+static void smap_free(smap* m) { free(m->h); free(m->id); free(m->cnt); free(m->used); free(m->srow); }
+
+static const uint8_t* bstr(const barr_t* a, size_t i, size_t* l) {
+  *l = (size_t)(a->offsets[i + 1] - a->offsets[i]);
+  return a->values + a->offsets[i];
+}
+
+/* insert row i's string; returns id; *slot = table slot */
+static uint32_t smap_add(smap* m, const barr_t* a, size_t row, size_t* slot) {
+  size_t l;
+  const uint8_t* s = bstr(a, row, &l);
+  uint64_t h = fnv1a(s, l);
+  size_t i = (size_t)(h * 0x9E3779B97F4A7C15ull >> 17) & (m->cap - 1);
+  for (;;) {
+    if (!m->used[i]) {
+      m->used[i] = 1;
+      m->h[i] = h;
+      m->id[i] = (uint32_t)m->n_ids;
+      m->cnt[i] = 0;
+      m->srow[m->n_ids++] = row;
+      break;
+    }
+    if (m->h[i] == h) {
+      size_t l2;
+      const uint8_t* s2 = bstr(a, m->srow[m->id[i]], &l2);
+      if (l2 == l && !memcmp(s, s2, l)) break;
+    }
+    i = (i + 1) & (m->cap - 1);
+  }
+  m->cnt[i]++;
+  if (slot) *slot = i;
+  return m->id[i];
+}
+
+int orc_compress_binary(const uint8_t* values, const int64_t* offsets, const uint8_t* validity, size_t n, int ow,
+                        uint64_t parent_values_len, const orc_write_options* opt, orc_buf* out) {
+  barr_t a = {values, offsets, validity, n, ow, parent_values_len};
+  orc_rng rng = {opt->seed};
+  /* gen_stats (binary/mod.rs:265-300): distinct over every slot incl. nulls */
+  smap m;
+  smap_init(&m, n);
+  for (size_t i = 0; i < n; i++) smap_add(&m, &a, i, NULL);
+  size_t null_count = 0;
+  for (size_t i = 0; i < n; i++) null_count += !is_valid(validity, i);
+  size_t unique = m.n_ids, total_unique = 0;
+  for (size_t id = 0; id < m.n_ids; id++) { size_t l; bstr(&a, m.srow[id], &l); total_unique += l + 8; }
+  size_t total_bytes = (size_t)parent_values_len + (n + 1) * (size_t)ow;
+  size_t maxc = 0, top_id = 0;
+  { /* top value: highest count, first occurrence on ties */
+    for (size_t i = 0; i < m.cap; i++) {
+      if (!m.used[i]) continue;
+      if (m.cnt[i] > maxc || (m.cnt[i] == maxc && m.id[i] < top_id)) { maxc = m.cnt[i]; top_id = m.id[i]; }
+    }
+  }
+  (void)rng;
+  /* choose_compressor (binary/mod.rs:302-348) */
+  int codec = opt->default_codec;
+  uint32_t fm = opt->forbidden_mask;
+  int forced = -1;
+  if (opt->forced_codec == ORC_FREQ && !(fm & (1u << ORC_FREQ))) forced = ORC_FREQ;
+  else if (opt->forced_codec == ORC_DICT && !(fm & (1u << ORC_DICT))) forced = ORC_DICT;
+  if (forced >= 0) {
+    codec = forced;
+  } else if (opt->has_ratio) {
+    double maxr = opt->ratio;
+    int cands[3] = {ORC_ONE_VALUE, ORC_FREQ, ORC_DICT};
+    for (int k = 0; k < 3; k++) {
+      if (fm & (1u << cands[k])) continue;
+      double r = 0.0;
+      if (cands[k] == ORC_ONE_VALUE) r = unique <= 1 ? (double)n : 0.0;
+      else if (cands[k] == ORC_FREQ) {
+        if (unique <= 1) r = 0.0;
+        else if ((double)null_count / (double)n >= 0.9) r = (double)(n - 1);
+        else if ((double)maxc / (double)n >= 0.9) r = (double)(n - 1);
+      } else {
+        if (unique * 3 < n) {
+          size_t after = total_unique + n * (bits_needed(unique) / 8) + n * 2 / 128;
+          r = (double)total_bytes / (double)after;
+        }
+      }
+      if (r > maxr) {
+        maxr = r;
+        codec = cands[k];
+        if (r == (double)n) break;
+      }
+    }
+  }
+  int rc = ORC_OK;
+  buf_u8(out, (uint8_t)codec);
+  size_t hpos = out->len;
+  buf_u64(out, 0);
+  size_t before = out->len;
+  if (codec <= ORC_SNAPPY) {
+    /* offsets rebased to 0, then values [first, last) */
+    size_t ob = (n + 1) * (size_t)ow;
+    uint8_t* tmp = (uint8_t*)malloc(ob);
+    for (size_t i = 0; i <= n; i++) {
+      int64_t v = offsets[i] - offsets[0];
+      memcpy(tmp + i * ow, &v, (size_t)ow);
+    }
+    rc = orc_common_compress(codec, tmp, ob, out);
+    free(tmp);
+    if (rc) { smap_free(&m); return rc; }
+    uint32_t cs = (uint32_t)(out->len - before), us = (uint32_t)ob;
+    memcpy(out->data + hpos, &cs, 4);
+    memcpy(out->data + hpos + 4, &us, 4);
+    buf_u8(out, (uint8_t)codec);
+    size_t h2 = out->len;
+    buf_u64(out, 0);
+    size_t b2 = out->len;
+    size_t vl = (size_t)(offsets[n] - offsets[0]);
+    rc = orc_common_compress(codec, values + offsets[0], vl, out);
+    uint32_t cs2 = (uint32_t)(out->len - b2), us2 = (uint32_t)vl;
+    memcpy(out->data + h2, &cs2, 4);
+    memcpy(out->data + h2 + 4, &us2, 4);
+    smap_free(&m);
+    return rc;
+  }
+  if (codec == ORC_ONE_VALUE) { /* one_value.rs:50-68: first valid value */
+    size_t l = 0;
+    const uint8_t* s = (const uint8_t*)"";
+    for (size_t i = 0; i < n; i++)
+      if (is_valid(validity, i)) { s = bstr(&a, i, &l); break; }
+    buf_u32(out, (uint32_t)l);
+    buf_put(out, s, l);
+  } else if (codec == ORC_DICT) { /* dict.rs:55-93 */
+    smap d;
+    smap_init(&d, n);
+    uint32_t* idx = (uint32_t*)malloc((n ? n : 1) * 4);
+    for (size_t i = 0; i < n; i++) {
+      if (!is_valid(validity, i) && i > 0) idx[i] = idx[i - 1];
+      else idx[i] = smap_add(&d, &a, i, NULL);
+    }
+    arr_t ia = {(const uint8_t*)idx, NULL, n, 4, 0, 0};
+    orc_write_options o2 = *opt;
+    o2.forbidden_mask |= 1u << ORC_DICT;
+    rc = compress_stream(&ia, &o2, &rng, out);
+    if (!rc) {
+      buf_u32(out, (uint32_t)d.n_ids);
+      for (size_t id = 0; id < d.n_ids; id++) {
+        size_t l;
+        const uint8_t* s = bstr(&a, d.srow[id], &l);
+        buf_u64(out, (uint64_t)l);
+        buf_put(out, s, l);
+      }
+    }
+    free(idx);
+    smap_free(&d);
+  } else if (codec == ORC_FREQ) { /* freq.rs:44-100 */
+    int top_null = (double)null_count / (double)n >= 0.9;
+    size_t tl = 0;
+    const uint8_t* ts = (const uint8_t*)"";
+    if (!top_null) ts = bstr(&a, m.srow[top_id], &tl);
+    uint32_t* pos = (uint32_t*)malloc((n ? n : 1) * 4);
+    size_t ne = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (!is_valid(validity, i)) continue;
+      size_t l;
+      const uint8_t* s = bstr(&a, i, &l);
+      if (top_null || l != tl || memcmp(s, ts, l)) pos[ne++] = (uint32_t)i;
+    }
+    buf_u64(out, (uint64_t)tl);
+    buf_put(out, ts, tl);
+    orc_buf bmb = {0};
+    orc_roaring_encode(pos, ne, &bmb);
+    buf_u32(out, (uint32_t)bmb.len);
+    buf_put(out, bmb.data, bmb.len);
+    orc_buf_free(&bmb);
+    for (size_t e = 0; e < ne; e++) {
+      size_t l;
+      const uint8_t* s = bstr(&a, pos[e], &l);
+      buf_u64(out, (uint64_t)l);
+      buf_put(out, s, l);
+    }
+    free(pos);
+  }
+  smap_free(&m);
+  if (rc) return rc;
+  /* Extend header: csize, usize = parent values length (mod.rs:88) */
+  uint32_t cs = (uint32_t)(out->len - before), us = (uint32_t)parent_values_len;
+  memcpy(out->data + hpos, &cs, 4);
+  memcpy(out->data + hpos + 4, &us, 4);
+  return ORC_OK;
+}
+
+/* one binary page [validity?][binary streams] appended to o (read_binary loop body) */
+int orc_read_binary_page(const uint8_t* page, size_t page_len, size_t n, int nullable, int ow, orc_binvec* o,
+                         uint8_t* out_bits) {
+  size_t pos = 0;
+  int rc;
+  if (nullable) {
+    rc = orc_read_validity(page, page_len, &pos, n, out_bits);
+    if (rc) return rc;
+  }
+  return orc_decompress_binary(page, page_len, &pos, n, ow, o);
+}
+
+int orc_write_binary_page(const uint8_t* values, const int64_t* offsets, const uint8_t* validity, size_t n,
+                          int ow, int nullable, uint64_t parent_values_len, const orc_write_options* opt,
+                          orc_buf* out) {
+  if (nullable) orc_write_validity(validity, n, out);
+  return orc_compress_binary(values, offsets, validity, n, ow, parent_values_len, opt, out);
+}
+
+/* ======================================================================= */
+/* nested List<primitive> pages                                              */
+/* writer: write_nested_validity (write/serialize.rs:217-232) -> arrow2     */
+/*   write_rep_and_def V2 -> parquet2 encode_u32 (one bit-packed run);       */
+/* reader: read_validity_nested (read/read_basic.rs:65-173) + create_list    */
+/*   (read/array/list.rs:48).  One list level over a primitive leaf.         */
+/* ======================================================================= */
+static uint32_t bit_width_of(uint32_t max_level) { uint32_t b = 0; while (max_level) { b++; max_level >>= 1; } return b; }
+
+static void encode_levels(const uint32_t* lv, size_t n, uint32_t bw, orc_buf* out) {
+  size_t groups = (n + 7) / 8;
+  uint8_t hdr[10];
+  size_t hl = 0;
+  uint64_t h = ((uint64_t)groups << 1) | 1;
+  do { uint8_t c = h & 0x7F; h >>= 7; if (h) c |= 0x80; hdr[hl++] = c; } while (h);
+  buf_put(out, hdr, hl);
+  size_t nbytes = groups * bw, at = out->len;
+  buf_reserve(out, nbytes);
+  memset(out->data + at, 0, nbytes);
+  for (size_t i = 0; i < n; i++)
+    for (uint32_t k = 0; k < bw; k++)
+      if ((lv[i] >> k) & 1) { size_t q = i * bw + k; out->data[at + (q >> 3)] |= (uint8_t)(1u << (q & 7)); }
+  out->len += nbytes;
+}
+
+int orc_write_list_page(const int64_t* list_offsets, const uint8_t* list_validity, size_t rows, int list_nullable,
+                        const uint8_t* child_values, const uint8_t* child_validity, int item_nullable, int kind,
+                        int width, int is_signed, const orc_write_options* opt, orc_buf* out, uint64_t* num_levels) {
+  const uint32_t nl = list_nullable ? 1 : 0, ni = item_nullable ? 1 : 0;
+  const uint32_t max_def = nl + 1 + ni;
+  size_t cap = rows + (size_t)(list_offsets[rows] - list_offsets[0]) + 1;
+  uint32_t* rep = (uint32_t*)malloc(cap * 4);
+  uint32_t* def = (uint32_t*)malloc(cap * 4);
+  size_t L = 0;
+  for (size_t r = 0; r < rows; r++) {
+    int64_t b = list_offsets[r], e = list_offsets[r + 1];
+    if (nl && !is_valid(list_validity, r)) { rep[L] = 0; def[L] = 0; L++; continue; }
+    if (e == b) { rep[L] = 0; def[L] = nl; L++; continue; }
+    for (int64_t j = b; j < e; j++) {
+      rep[L] = j > b;
+      def[L] = ni ? (is_valid(child_validity, (size_t)j) ? max_def : max_def - 1) : max_def;
+      L++;
+    }
+  }
+  orc_buf lv = {0};
+  encode_levels(rep, L, bit_width_of(1), &lv);
+  size_t rep_len = lv.len;
+  encode_levels(def, L, bit_width_of(max_def), &lv);
+  size_t def_len = lv.len - rep_len;
+  buf_u32(out, (uint32_t)rows);
+  buf_u32(out, (uint32_t)rep_len);
+  buf_u32(out, (uint32_t)def_len);
+  buf_put(out, lv.data, lv.len);
+  orc_buf_free(&lv);
+  free(rep);
+  free(def);
+  /* leaf values of the page's rows (slice_parquet_array), their validity */
+  size_t v0 = (size_t)list_offsets[0], nv = (size_t)(list_offsets[rows] - list_offsets[0]);
+  uint8_t* vb = NULL;
+  if (child_validity) {
+    vb = (uint8_t*)calloc((nv + 7) / 8 + 1, 1);
+    for (size_t i = 0; i < nv; i++)
+      if (get_bit(child_validity, v0 + i)) vb[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  int rc = kind ? orc_compress_double(child_values + v0 * width, vb, nv, width, opt, out)
+                : orc_compress_integer(child_values + v0 * width, vb, nv, width, is_signed, opt, out);
+  free(vb);
+  *num_levels = L;
+  return rc;
+}
+
+/* One nested page -> this page's ListArray pieces (appended to the column):
+ * offsets (rows, page-relative leaf positions; the final offset is the
+ * returned leaf count), list validity bits, leaf values and leaf validity. */
+int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int list_nullable, int item_nullable,
+                       int kind, int width, int64_t* out_offsets, uint8_t* out_list_bits, uint8_t* out_values,
+                       uint8_t* out_leaf_bits, size_t* out_rows, size_t* out_leaves) {
+  if (len < 12) return ORC_E_IO;
+  uint32_t additional = rd_u32(page), rep_len = rd_u32(page + 4), def_len = rd_u32(page + 8);
+  size_t pos = 12;
+  if (pos + rep_len > len || pos + rep_len + def_len > len) return ORC_E_IO;
+  const uint32_t nl = list_nullable ? 1 : 0, ni = item_nullable ? 1 : 0;
+  const uint32_t max_def = nl + 1 + ni;
+  uint32_t* rep = (uint32_t*)malloc((num_levels + 1) * 4);
+  uint32_t* def = (uint32_t*)malloc((num_levels + 1) * 4);
+  int rc = orc_hybrid_decode(page + pos, rep_len, bit_width_of(1), num_levels, rep);
+  if (!rc) rc = orc_hybrid_decode(page + pos + rep_len, def_len, bit_width_of(max_def), num_levels, def);
+  if (rc) { free(rep); free(def); return rc; }
+  pos += rep_len + def_len;
+  /* read_basic.rs:107-164 with cum_sum = [0, nl + 1, nl + 1 + ni], cum_rep = [0, 1, 1] */
+  const uint32_t cs1 = nl + 1;
+  size_t rows = 0, leaves = 0;
+  for (size_t l = 0; l < num_levels; l++) {
+    uint32_t r = rep[l], d = def[l];
+    if (r == 0) rows++;
+    if (r == 0) { /* depth 0: list push(offset = leaf count, valid = nl && def > 0) */
+      out_offsets[rows - 1] = (int64_t)leaves;
+      if (nl) {
+        if (d > 0) out_list_bits[(rows - 1) >> 3] |= (uint8_t)(1u << ((rows - 1) & 7));
+        else out_list_bits[(rows - 1) >> 3] &= (uint8_t)~(1u << ((rows - 1) & 7));
+      }
+    }
+    if (r <= 1 && d >= cs1) { /* depth 1: leaf slot */
+      if (ni) {
+        if (d != cs1) out_leaf_bits[leaves >> 3] |= (uint8_t)(1u << (leaves & 7));
+        else out_leaf_bits[leaves >> 3] &= (uint8_t)~(1u << (leaves & 7));
+      }
+      leaves++;
+    }
+    uint32_t next_rep = l + 1 < num_levels ? rep[l + 1] : 0;
+    if (next_rep == 0 && rows == additional) break;
+  }
+  free(rep);
+  free(def);
+  if (rows != additional) return ORC_E_OUT_OF_SPEC; /* create_list would mis-size */
+  rc = kind ? orc_decompress_double(page, len, &pos, width, leaves, out_values)
+            : orc_decompress_integer(page, len, &pos, width, leaves, out_values);
+  *out_rows = rows;
+  *out_leaves = leaves;
+  return rc;
+}

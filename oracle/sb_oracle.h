@@ -105,6 +105,36 @@ int orc_write_flat_page(const uint8_t* values, const uint8_t* validity, size_t n
 int orc_read_column(const uint8_t* chunk, size_t len, const uint64_t* metas, size_t n_pages, int kind, int width,
                     int nullable, uint8_t* out_values, uint8_t* out_bits);
 
+/* ---- binary / utf8 (compression/binary/mod.rs) ---- */
+/* The reference's (Vec<O> offsets, Vec<u8> values) pair, grown by appends. */
+typedef struct {
+  int64_t* offsets;
+  size_t n_off, cap_off;
+  uint8_t* values;
+  size_t n_val, cap_val;
+} orc_binvec;
+void orc_binvec_free(orc_binvec* o);
+/* decompress_binary (binary/mod.rs:95-183); ow = sizeof(O) in {4, 8} */
+int orc_decompress_binary(const uint8_t* buf, size_t len, size_t* pos, size_t length, int ow, orc_binvec* o);
+/* compress_binary (binary/mod.rs:26-93); offsets are n+1 absolute positions
+ * into values; parent_values_len = the array's whole values buffer length
+ * (stats total_bytes and the Extend header's usize use it) */
+int orc_compress_binary(const uint8_t* values, const int64_t* offsets, const uint8_t* validity, size_t n, int ow,
+                        uint64_t parent_values_len, const orc_write_options* opt, orc_buf* out);
+int orc_read_binary_page(const uint8_t* page, size_t page_len, size_t n, int nullable, int ow, orc_binvec* o,
+                         uint8_t* out_bits);
+int orc_write_binary_page(const uint8_t* values, const int64_t* offsets, const uint8_t* validity, size_t n,
+                          int ow, int nullable, uint64_t parent_values_len, const orc_write_options* opt,
+                          orc_buf* out);
+
+/* ---- nested List<primitive> (read_basic.rs:65-173, serialize.rs:217-232) ---- */
+int orc_write_list_page(const int64_t* list_offsets, const uint8_t* list_validity, size_t rows, int list_nullable,
+                        const uint8_t* child_values, const uint8_t* child_validity, int item_nullable, int kind,
+                        int width, int is_signed, const orc_write_options* opt, orc_buf* out, uint64_t* num_levels);
+int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int list_nullable, int item_nullable,
+                       int kind, int width, int64_t* out_offsets, uint8_t* out_list_bits, uint8_t* out_values,
+                       uint8_t* out_leaf_bits, size_t* out_rows, size_t* out_leaves);
+
 /* ---- roaring portable format (roaring 0.10.1) ---- */
 /* Deserializes into ascending positions.  *count set; positions may be NULL to
  * size.  cap = capacity of positions. */

@@ -36,6 +36,10 @@ struct sb_plan {
   uint32_t* d_defer = nullptr;  // [count parity 0, count parity 1, work list...]
   uint64_t decodes = 0;
   int deferred_state = -1;  // -1 unknown, 0 no deferred pages, 1 some
+  bool binary = false;
+  int offset_width = 0;
+  uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1]
+  uint64_t values_bytes = 0;
   uint32_t n_staged = 0, n_global = 0;
   bool staged_identity = false;  // every page staged: no index list
   uint32_t stage_bytes = 0;
@@ -136,6 +140,7 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_status) (void)hipFree(p->d_status);
   if (p->d_lists) (void)hipFree(p->d_lists);
   if (p->d_defer) (void)hipFree(p->d_defer);
+  if (p->d_bin) (void)hipFree(p->d_bin);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   delete p;
@@ -149,7 +154,10 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   if (!ctx || !desc || !out || (!h_metas && n_pages)) return fail(ctx, SB_E_ARG, "null argument");
   bool is_float;
   int width = type_width(desc->physical_type, &is_float);
-  if (!width) return fail(ctx, SB_E_NYI, "physical type %d not supported", desc->physical_type);
+  const int ptype = desc->physical_type;
+  const int owidth = (ptype == SB_T_BINARY || ptype == SB_T_UTF8) ? 4
+                     : (ptype == SB_T_LARGE_BINARY || ptype == SB_T_LARGE_UTF8) ? 8 : 0;
+  if (!width && !owidth) return fail(ctx, SB_E_NYI, "physical type %d not supported", desc->physical_type);
   if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
 
@@ -190,6 +198,8 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   p->staged_identity = global.empty();
   p->stage_bytes = ((max_stage + 16 + 15) & ~15u) + sb::kStagePad;
   p->validity_needs_zero = needs_zero;
+  p->binary = owidth != 0;
+  p->offset_width = owidth;
   size_t np = n_pages ? n_pages : 1;
   hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
   if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
@@ -211,12 +221,61 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     sb_plan_destroy(p);
     return fail(ctx, SB_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
   }
+  if (p->binary && n_pages) {  // size every page's values once: they are fixed for the plan
+    e = hipMalloc(&p->d_bin, (2 * np + 1) * sizeof(uint64_t));
+    if (e != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "plan alloc: %s", hipGetErrorString(e));
+    }
+    sb::BinLaunch L{d_chunk, p->d_pages, (uint32_t)n_pages, desc->nullable, p->d_bin, p->d_bin + np,
+                    p->d_bin + 2 * np, nullptr, nullptr, 0, nullptr, p->d_status};
+    if (sb::launch_binary(0, owidth, L, ctx->stream) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "binary sizing failed: %s", hipGetErrorString(hipGetLastError()));
+    }
+    std::vector<uint32_t> st(n_pages);
+    (void)hipMemcpy(st.data(), p->d_status, n_pages * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&p->values_bytes, p->d_bin + 2 * np, 8, hipMemcpyDeviceToHost);
+    for (uint64_t i = 0; i < n_pages; i++) {
+      if (st[i]) {
+        sb_plan_destroy(p);
+        return fail(ctx, (sb_status)st[i], "page %llu: %s", (unsigned long long)i, sb_status_str((int)st[i]));
+      }
+    }
+  }
   *out = p;
+  return SB_OK;
+}
+
+uint64_t sb_plan_values_bytes(const sb_plan* p) { return p ? p->values_bytes : 0; }
+
+sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out* out) {
+  if (!ctx || !p || !out) return fail(ctx, SB_E_ARG, "null argument");
+  if (!p->binary) return fail(ctx, SB_E_ARG, "not a binary plan");
+  if (!out->d_offsets || (p->values_bytes && (!out->d_values || out->values_capacity < p->values_bytes)))
+    return fail(ctx, SB_E_ARG, "binary output buffers too small");
+  if (p->desc.nullable && p->n_rows && !out->d_validity) return fail(ctx, SB_E_ARG, "validity buffer is null");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (p->desc.nullable && p->validity_needs_zero)
+    HIP_TRY(ctx, hipMemsetAsync(out->d_validity, 0, (p->n_rows + 31) / 32 * 4, ctx->stream));
+  if (!p->n_pages) return SB_OK;
+  if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
+  const size_t np = p->n_pages;
+  sb::BinLaunch L{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
+                  (uint8_t*)out->d_offsets, out->d_values, out->values_capacity, (uint32_t*)out->d_validity,
+                  p->d_status};
+  if (sb::launch_binary(1, p->offset_width, L, ctx->stream))
+    return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (p->timing) {
+    HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
+    p->timed = true;
+  }
   return SB_OK;
 }
 
 sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out) {
   if (!ctx || !p || !out) return fail(ctx, SB_E_ARG, "null argument");
+  if (p->binary) return fail(ctx, SB_E_ARG, "binary plan: use sb_decode_binary_planned");
   if (p->n_rows && !out->d_values) return fail(ctx, SB_E_ARG, "values buffer is null");
   if (p->desc.nullable && p->n_rows && !out->d_validity) return fail(ctx, SB_E_ARG, "validity buffer is null");
   HIP_TRY(ctx, hipSetDevice(ctx->device));

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "sb_internal.h"
 
 namespace sbk {
@@ -559,16 +561,13 @@ __device__ void write_validity(const Src& s, uint32_t vb, uint32_t n, uint64_t r
 // ---------------------------------------------------------------------------
 // the page kernel
 // ---------------------------------------------------------------------------
-// Parses a Freq body [T top][u32 bm][roaring][exceptions stream] whose value
-// width is `vw` (integer/freq.rs:88-123).  Thread 0 only.
+// Parses a roaring portable bitmap of bm bytes at r into the container table
+// (array and bitmap containers; cookie 12347 run containers are not written
+// by roaring 0.10.1 and report NYI).  Thread 0 only; total = cardinality.
 template <class Src>
-__device__ bool parse_freq(const Src& s, Shared& sh, const Stream& st, uint32_t vw, Stream* ex) {
-  const uint32_t e = st.body + st.csize;
-  if (st.body + vw + 4 > e) { set_err(sh, ST_IO); return false; }
-  sh.freq_top = vw == 8 ? s.u64(st.body) : vw == 4 ? s.u32(st.body) : vw == 2 ? (s.u32(st.body) & 0xFFFFu) : s.u8(st.body);
-  const uint32_t bm = s.u32(st.body + vw), r = st.body + vw + 4;
-  if (bm > e - r || bm < 8) { set_err(sh, ST_IO); return false; }
-  if (s.u32(r) != 12346) { set_err(sh, ST_NYI); return false; }  // run containers (cookie 12347)
+__device__ bool parse_roaring(const Src& s, Shared& sh, uint32_t r, uint32_t bm, uint32_t* total) {
+  if (bm < 8) { set_err(sh, ST_IO); return false; }
+  if (s.u32(r) != 12346) { set_err(sh, ST_NYI); return false; }
   const uint32_t nc = s.u32(r + 4);
   if (nc > kMaxConts || 8 + 8 * (uint64_t)nc > bm) { set_err(sh, ST_NYI); return false; }
   uint32_t tot = 0, nbm = 0;
@@ -596,6 +595,21 @@ __device__ bool parse_freq(const Src& s, Shared& sh, const Stream& st, uint32_t 
     tot += card;
   }
   sh.cont_prefix[nc] = tot;
+  *total = tot;
+  return true;
+}
+
+// Parses a Freq body [T top][u32 bm][roaring][exceptions stream] whose value
+// width is `vw` (integer/freq.rs:88-123).  Thread 0 only.
+template <class Src>
+__device__ bool parse_freq(const Src& s, Shared& sh, const Stream& st, uint32_t vw, Stream* ex) {
+  const uint32_t e = st.body + st.csize;
+  if (st.body + vw + 4 > e) { set_err(sh, ST_IO); return false; }
+  sh.freq_top = vw == 8 ? s.u64(st.body) : vw == 4 ? s.u32(st.body) : vw == 2 ? (s.u32(st.body) & 0xFFFFu) : s.u8(st.body);
+  const uint32_t bm = s.u32(st.body + vw), r = st.body + vw + 4;
+  if (bm > e - r) { set_err(sh, ST_IO); return false; }
+  uint32_t tot;
+  if (!parse_roaring(s, sh, r, bm, &tot)) return false;
   if (!parse_stream(s, r + bm, e, tot, ex)) { set_err(sh, ST_IO); return false; }
   return true;
 }
@@ -762,6 +776,39 @@ __device__ uint32_t patas_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, u
   return ST_OK;
 }
 
+// read_validity (read/read_basic.rs:36-63): [def_len u32][ULEB128 h, h&1 =
+// bit-packed, h>>1 groups][bitmap].  An RLE run (unreachable!() at :59) or
+// fewer than n bits is OutOfSpec; def_len 0 pushes nothing, which only an
+// empty page survives.  Thread 0; advances *p past the prefix.
+template <class Src>
+__device__ bool parse_validity(const Src& s, Shared& sh, uint32_t len, uint32_t n, uint32_t* pp) {
+  uint32_t p = *pp;
+  if (p + 4 > len) { set_err(sh, ST_IO); return false; }
+  const uint32_t def_len = s.u32(p);
+  p += 4;
+  if (def_len == 0) {
+    if (n) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+    *pp = p;
+    return true;
+  }
+  if (def_len > len - p) { set_err(sh, ST_IO); return false; }
+  uint32_t q = p, h = 0, sft = 0;
+  for (;;) {
+    if (q >= p + def_len || sft > 28) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+    const uint32_t c = s.u8(q++);
+    h |= (c & 0x7Fu) << sft;
+    if (!(c & 0x80)) break;
+    sft += 7;
+  }
+  if (!(h & 1)) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+  const uint32_t groups = min(h >> 1, p + def_len - q);
+  if ((uint64_t)groups * 8 < n) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+  sh.has_valid = 1;
+  sh.vb_pos = q;
+  *pp = p + def_len;
+  return true;
+}
+
 // Cascade shapes the writer produces (Dict forbids Dict below it, Freq forbids
 // Freq: dict.rs:60-62, freq.rs:79-83).
 enum : uint32_t { CH_LEAF = 0, CH_DICT = 1, CH_FREQ = 2, CH_DICT_FREQ = 3, CH_FREQ_DICT = 4 };
@@ -780,32 +827,7 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
     uint32_t p = 0;
     sh.has_valid = 0;
     do {
-      if (a.nullable) {
-        // read_validity: [def_len u32][ULEB128 h: h&1 = bit-packed, h>>1 groups][bitmap]
-        if (p + 4 > len) { set_err(sh, ST_IO); break; }
-        uint32_t def_len = s.u32(p);
-        p += 4;
-        if (def_len == 0) {  // nothing pushed: validity length mismatch
-          if (n) set_err(sh, ST_OUT_OF_SPEC);
-        } else {
-          if (def_len > len - p) { set_err(sh, ST_IO); break; }
-          uint32_t q = p, h = 0, sft = 0;
-          for (;;) {
-            if (q >= p + def_len || sft > 28) { set_err(sh, ST_OUT_OF_SPEC); break; }
-            uint32_t c = s.u8(q++);
-            h |= (c & 0x7Fu) << sft;
-            if (!(c & 0x80)) break;
-            sft += 7;
-          }
-          if (sh.err) break;
-          if (!(h & 1)) { set_err(sh, ST_OUT_OF_SPEC); break; }  // Rle run: unreachable!()
-          uint32_t groups = min(h >> 1, p + def_len - q);
-          if ((uint64_t)groups * 8 < n) { set_err(sh, ST_OUT_OF_SPEC); break; }
-          sh.has_valid = 1;
-          sh.vb_pos = q;
-          p += def_len;
-        }
-      }
+      if (a.nullable && !parse_validity(s, sh, len, n, &p)) break;
       Stream st;
       if (!parse_stream(s, p, len, n, &st)) { set_err(sh, ST_IO); break; }
       uint32_t chain = CH_LEAF;
@@ -1057,6 +1079,423 @@ static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ===========================================================================
+// Binary / Utf8 pages (compression/binary/mod.rs:95-183, dict.rs:95-141,
+// freq.rs:102-145, one_value.rs:71-99), assembled as read_binary does
+// (read/array/binary.rs:223-265): per-page offsets rebased onto the running
+// values length, values appended.  Pass 1 (k_bin_size) sizes each page's
+// values; k_bin_scan turns sizes into bases; pass 2 (k_bin_decode) writes
+// offsets, values and validity.  A workgroup holds its page, the expanded
+// offsets / index stream, the expanded values and the entry table in LDS.
+// ===========================================================================
+struct BinArgs {
+  const uint8_t* chunk;
+  const PageDesc* pages;
+  uint32_t n_pages;
+  int nullable;
+  uint64_t* sizes;   // pass 1 out: values bytes per page
+  uint64_t* bases;   // scan out: first values byte of each page
+  uint64_t* total;   // scan out
+  uint8_t* out_offsets;
+  uint8_t* out_values;
+  uint64_t values_cap;
+  uint32_t* out_validity;
+  uint32_t* status;
+  uint32_t lds_bytes;
+};
+
+enum : uint32_t { BIN_BASIC = 0, BIN_ONE = 12, BIN_DICT = 11, BIN_FREQ = 13 };
+
+struct BinInfo {
+  uint32_t codec;      // leading codec byte
+  uint32_t ob, ocs;    // Basic: offsets stream body / csize
+  uint32_t vb, vcs;    // Basic: values stream body / csize
+  uint64_t S;          // values bytes of the page
+  uint32_t L, top;     // OneValue / Freq top: length and position
+  uint32_t k;          // Dict entries / Freq exceptions consumed (positions < n)
+  uint32_t tab;        // LDS byte offset of the (pos, len) entry table
+  uint32_t xoff, yoff; // LDS byte offsets of the X (offsets / indices) and Y (values) regions
+};
+
+// Thread 0: parse validity prefix + binary header; walk Dict entries / Freq
+// exception records into the LDS table (pos, len).  Returns false on error.
+template <int OW, class Src>
+__device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc& pd, int nullable, uint8_t* lds,
+                          uint32_t stage_end, uint32_t lds_bytes, Stream* idx) {
+  const uint32_t len = pd.byte_len, n = pd.num_values;
+  uint32_t p = 0;
+  sh.has_valid = 0;
+  if (nullable && !parse_validity(s, sh, len, n, &p)) return false;
+  if (p + 9 > len) { set_err(sh, ST_IO); return false; }
+  bi.codec = s.u8(p);
+  const uint32_t cs = s.u32(p + 1), body = p + 9;
+  if (cs > len - body) { set_err(sh, ST_IO); return false; }
+  const uint32_t end = body + cs;
+  bi.xoff = stage_end;
+  bi.S = 0;
+  bi.k = 0;
+  if (bi.codec <= 3) {  // Basic: offsets stream then values stream (same codec)
+    bi.ob = body;
+    bi.ocs = cs;
+    const uint32_t vh = end;
+    if (vh + 9 > len) { set_err(sh, ST_IO); return false; }
+    bi.vcs = s.u32(vh + 1);
+    bi.S = s.u32(vh + 5);
+    bi.vb = vh + 9;
+    if (bi.vcs > len - bi.vb) { set_err(sh, ST_IO); return false; }
+    const uint32_t xb = ((n + 1) * OW + 15) & ~15u;
+    bi.yoff = bi.xoff + xb;
+    bi.tab = bi.yoff;
+    if (bi.codec != 0 && bi.yoff + bi.S + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
+    return true;
+  }
+  if (bi.codec == BIN_ONE) {
+    if (cs < 4) { set_err(sh, ST_IO); return false; }
+    bi.L = s.u32(body);
+    if (bi.L > cs - 4) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+    bi.top = body + 4;
+    bi.S = (uint64_t)n * bi.L;
+    return true;
+  }
+  uint2* tab = nullptr;
+  if (bi.codec == BIN_DICT) {
+    Stream ix;
+    if (!parse_stream(s, body, end, n, &ix)) { set_err(sh, ST_IO); return false; }
+    if (ix.codec == 11) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+    if (ix.codec == 2) { set_err(sh, ST_NYI); return false; }  // Zstd index stream: host-only for now
+    *idx = ix;
+    uint32_t q = ix.body + ix.csize;
+    if (q + 4 > end) { set_err(sh, ST_IO); return false; }
+    const uint32_t k = s.u32(q);
+    q += 4;
+    bi.tab = bi.xoff + ((n * 4 + 15) & ~15u);  // X = indices
+    if (bi.tab + 8 * (uint64_t)k + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
+    tab = (uint2*)(lds + bi.tab);
+    for (uint32_t e = 0; e < k; e++) {  // u64 len + bytes per entry
+      if (q + 8 > end) { set_err(sh, ST_IO); return false; }
+      const uint64_t l = s.u64(q);
+      q += 8;
+      if (l > end - q) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      tab[e] = make_uint2(q, (uint32_t)l);
+      q += (uint32_t)l;
+    }
+    bi.k = k;
+    return true;
+  }
+  if (bi.codec == BIN_FREQ) {
+    if (cs < 8) { set_err(sh, ST_IO); return false; }
+    const uint64_t tl = s.u64(body);
+    uint32_t q = body + 8;
+    if (tl > end - q) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+    bi.L = (uint32_t)tl;
+    bi.top = q;
+    q += bi.L;
+    if (q + 4 > end) { set_err(sh, ST_IO); return false; }
+    const uint32_t bm = s.u32(q);
+    q += 4;
+    if (bm > end - q) { set_err(sh, ST_IO); return false; }
+    uint32_t tot;
+    if (!parse_roaring(s, sh, q, bm, &tot)) return false;
+    q += bm;
+    // exceptions at rows < n are consumed in row order (freq.rs:127-141)
+    uint32_t ep = 0;
+    while (ep < tot && roaring_select(s, sh, ep) < n) ep++;
+    bi.tab = bi.xoff + ((((n + 31) / 32) * 8 + 15) & ~15u);  // X = row bitmap + prefix
+    if (bi.tab + 8 * (uint64_t)ep + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
+    tab = (uint2*)(lds + bi.tab);
+    uint64_t sum = 0;
+    for (uint32_t e = 0; e < ep; e++) {
+      if (q + 8 > end) { set_err(sh, ST_IO); return false; }
+      const uint64_t l = s.u64(q);
+      q += 8;
+      if (l > end - q) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      tab[e] = make_uint2(q, (uint32_t)l);
+      sum += l;
+      q += (uint32_t)l;
+    }
+    bi.k = ep;
+    bi.S = (uint64_t)(n - ep) * bi.L + sum;
+    return true;
+  }
+  set_err(sh, ST_OUT_OF_SPEC);
+  return false;
+}
+
+template <int OW, class Src>
+__device__ __forceinline__ uint64_t ldo(const Src& s, uint32_t p) {
+  if constexpr (OW == 8) return s.u64(p);
+  else return (uint64_t)(int64_t)(int32_t)s.u32(p);
+}
+
+__device__ __forceinline__ void bin_put_off(uint8_t* out, uint64_t row, uint64_t v, int ow) {
+  if (ow == 8) ((uint64_t*)out)[row] = v;
+  else ((uint32_t*)out)[row] = (uint32_t)v;
+}
+
+// Copy `len` bytes from LDS byte position `src` to global `dst`, all threads.
+__device__ void copy_lds_to_global(const uint8_t* lds, uint32_t src, uint8_t* dst, uint64_t len) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t head = (uint32_t)min<uint64_t>(len, (4 - ((uintptr_t)dst & 3)) & 3);
+  if (tid < head) dst[tid] = lds[src + tid];
+  const uint64_t body = (len - head) >> 2;
+  const uint32_t* lw = (const uint32_t*)lds;
+  uint32_t* dw = (uint32_t*)(dst + head);
+  for (uint64_t w = tid; w < body; w += NT) {
+    const uint32_t p = src + head + (uint32_t)w * 4, i = p >> 2;
+    dw[w] = __builtin_amdgcn_alignbyte(lw[i + 1], lw[i], p & 3);
+  }
+  const uint64_t done = head + body * 4;
+  if (tid < len - done) dst[done + tid] = lds[src + done + tid];
+}
+
+// Materializes a binary Dict's u32 index stream (n values) into LDS xi: leaf
+// codecs via run_leaf, LZ4 / Snappy expanded straight into xi, Freq (top +
+// roaring-placed exceptions of a leaf stream) filled then scattered.
+__device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, uint32_t* xi) {
+  const uint32_t tid = threadIdx.x, n = ix.n;
+  if (ix.codec == 1 || ix.codec == 3) {
+    if (tid < 64) {
+      const lds_u8* in = (const lds_u8*)((const uint8_t*)s.w + s.base + ix.body);
+      const uint32_t st = ix.codec == 1 ? lz4_expand(in, ix.csize, (lds_u8*)xi, 4 * n)
+                                        : snappy_expand(in, ix.csize, (lds_u8*)xi, 4 * n);
+      if (st) set_err(sh, st);
+    }
+    __syncthreads();
+    return;
+  }
+  if (ix.codec == 13) {
+    __shared__ Stream ex;
+    if (tid == 0 && parse_freq(s, sh, ix, 4, &ex)) {
+      if (ex.codec == 11 || ex.codec == 13 || ex.codec == 1 || ex.codec == 2 || ex.codec == 3) set_err(sh, ST_NYI);
+    }
+    __syncthreads();
+    if (sh.err) return;
+    const uint32_t top = (uint32_t)sh.freq_top;
+    for (uint32_t i = tid; i < n; i += NT) xi[i] = top;
+    __syncthreads();
+    run_leaf<4>(s, sh, ex, [&](uint32_t i0, const uint32_t* v, uint32_t nv) {
+      for (uint32_t l = 0; l < nv; l++) {
+        const uint32_t row = roaring_select(s, sh, i0 + l);
+        if (row < n) xi[row] = v[l];
+        else set_err(sh, ST_OUT_OF_SPEC);
+      }
+    });
+    __syncthreads();
+    return;
+  }
+  run_leaf<4>(s, sh, ix, [&](uint32_t row, const uint32_t* v, uint32_t nv) {
+    for (uint32_t l = 0; l < nv; l++) xi[row + l] = v[l];
+  });
+  __syncthreads();
+}
+
+template <int OW>
+__global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
+  extern __shared__ u32x4 stage[];
+  __shared__ Shared sh;
+  __shared__ BinInfo bi;
+  __shared__ Stream idx;
+  uint8_t* lds = (uint8_t*)stage;
+  for (uint32_t page = blockIdx.x; page < a.n_pages; page += gridDim.x) {
+    const PageDesc pd = a.pages[page];
+    if (threadIdx.x == 0) sh.err = 0;
+    const uint32_t stage_end = ((pd.byte_len + 15 + kStagePad) + 15) & ~15u;
+    if (stage_end + 64 > a.lds_bytes) {  // page larger than the LDS budget
+      __syncthreads();
+      if (threadIdx.x == 0) { a.status[page] = ST_NYI; a.sizes[page] = 0; }
+      __syncthreads();
+      continue;
+    }
+    const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
+    LdsSrc s{(const uint32_t*)stage, base};
+    if (threadIdx.x == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, &idx);
+    __syncthreads();
+    if (!sh.err && bi.codec == BIN_DICT) {
+      const uint2* tab = (const uint2*)(lds + bi.tab);
+      const uint32_t k = bi.k;
+      uint32_t* xi = (uint32_t*)(lds + bi.xoff);
+      materialize_idx(s, sh, idx, xi);
+      uint64_t part = 0;
+      for (uint32_t i = threadIdx.x; i < pd.num_values; i += NT) {
+        if (xi[i] < k) part += tab[xi[i]].y;
+        else set_err(sh, ST_OUT_OF_SPEC);  // data_offsets[i] out of range panics
+      }
+      uint64_t tot;
+      block_excl_scan<uint64_t>(part, sh, &tot);
+      if (threadIdx.x == 0) bi.S = tot;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      a.status[page] = sh.err;
+      a.sizes[page] = sh.err ? 0 : bi.S;
+    }
+    __syncthreads();
+  }
+}
+
+// Exclusive scan of the page sizes (one workgroup).
+__global__ __launch_bounds__(NT) void k_bin_scan(BinArgs a) {
+  __shared__ Shared sh;
+  uint64_t carry = 0;
+  for (uint32_t p0 = 0; p0 < a.n_pages; p0 += NT) {
+    const uint32_t p = p0 + threadIdx.x;
+    const uint64_t v = p < a.n_pages ? a.sizes[p] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan<uint64_t>(v, sh, &tot);
+    if (p < a.n_pages) a.bases[p] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *a.total = carry;
+}
+
+// Offsets and values for rows whose byte lengths come from len_of(i) and
+// bytes from src_of(i) (LDS position): Dict, Freq and OneValue pages.
+template <int OW, class LenF, class SrcF>
+__device__ void bin_emit_rows(Shared& sh, const uint8_t* lds, uint32_t n, uint64_t R, uint64_t V, const BinArgs& a,
+                              LenF len_of, SrcF src_of) {
+  const uint32_t tid = threadIdx.x;
+  uint64_t carry = 0;
+  for (uint32_t r0 = 0; r0 < n; r0 += NT * 4) {
+    uint32_t l[4];
+    uint64_t tsum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t i = r0 + tid * 4 + j;
+      l[j] = i < n ? len_of(i) : 0u;
+      tsum += l[j];
+    }
+    uint64_t tot;
+    uint64_t pre = block_excl_scan<uint64_t>(tsum, sh, &tot) + carry;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t i = r0 + tid * 4 + j;
+      if (i < n) {
+        uint8_t* dst = a.out_values + V + pre;
+        const uint32_t sp = src_of(i);
+        for (uint32_t b = 0; b < l[j]; b++) dst[b] = lds[sp + b];
+        pre += l[j];
+        bin_put_off(a.out_offsets, R + i + 1, V + pre, OW);
+      }
+    }
+    carry += tot;
+  }
+}
+
+template <int OW>
+__global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
+  extern __shared__ u32x4 stage[];
+  __shared__ Shared sh;
+  __shared__ BinInfo bi;
+  __shared__ Stream idx;
+  uint8_t* lds = (uint8_t*)stage;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t page = blockIdx.x; page < a.n_pages; page += gridDim.x) {
+    const PageDesc pd = a.pages[page];
+    const uint32_t n = pd.num_values;
+    const uint64_t R = pd.row_off, V = a.bases[page];
+    if (tid == 0) sh.err = a.status[page];  // sizing errors stand
+    const uint32_t stage_end = ((pd.byte_len + 15 + kStagePad) + 15) & ~15u;
+    __syncthreads();
+    if (sh.err || stage_end + 64 > a.lds_bytes) {
+      __syncthreads();
+      continue;
+    }
+    const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
+    LdsSrc s{(const uint32_t*)stage, base};
+    if (tid == 0) {
+      bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, &idx);
+      if (!sh.err && V + bi.S > a.values_cap) set_err(sh, ST_OUT_OF_SPEC);
+    }
+    __syncthreads();
+    if (!sh.err) {
+      if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
+      if (R == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);
+      if (bi.codec <= 3) {
+        // offsets: rows 1..n at V + p[i] (mod.rs:136-144 rebase); p[0] must be
+        // 0 and p[n] the values length (the writer rebases, mod.rs:45-55)
+        uint32_t opos = bi.ob;  // stream position of p[0]
+        if (bi.codec != 0) {
+          const uint32_t ob = (n + 1) * OW;
+          if (tid < 64) {
+            const lds_u8* in = (const lds_u8*)(lds + base + bi.ob);
+            lds_u8* xo = (lds_u8*)(lds + bi.xoff);
+            uint32_t st = ST_NYI;
+            if (bi.codec == 1) st = lz4_expand(in, bi.ocs, xo, ob);
+            else if (bi.codec == 3) st = snappy_expand(in, bi.ocs, xo, ob);
+            if (st) set_err(sh, st);
+            if (!st) {
+              const lds_u8* vin = (const lds_u8*)(lds + base + bi.vb);
+              lds_u8* yo = (lds_u8*)(lds + bi.yoff);
+              uint32_t st2 = bi.codec == 1 ? lz4_expand(vin, bi.vcs, yo, (uint32_t)bi.S)
+                                            : snappy_expand(vin, bi.vcs, yo, (uint32_t)bi.S);
+              if (st2) set_err(sh, st2);
+            }
+          }
+          opos = bi.xoff - base;
+          __syncthreads();
+        } else if (tid == 0 && (bi.ocs != (n + 1) * OW || bi.vcs != bi.S)) {
+          set_err(sh, ST_OUT_OF_SPEC);  // copy_from_slice length mismatch
+        }
+        __syncthreads();
+        if (!sh.err && tid == 0) {
+          if (ldo<OW>(s, opos) != 0 || ldo<OW>(s, opos + n * OW) != bi.S) set_err(sh, ST_OUT_OF_SPEC);
+        }
+        __syncthreads();
+        if (!sh.err) {
+          for (uint32_t i = tid + 1; i <= n; i += NT) bin_put_off(a.out_offsets, R + i, V + ldo<OW>(s, opos + i * OW), OW);
+          const uint32_t vsrc = bi.codec != 0 ? bi.yoff : base + bi.vb;
+          copy_lds_to_global(lds, vsrc, a.out_values + V, bi.S);
+        }
+      } else if (bi.codec == BIN_ONE) {
+        const uint32_t L = bi.L, top = base + bi.top;
+        for (uint32_t i = tid + 1; i <= n; i += NT) bin_put_off(a.out_offsets, R + i, V + (uint64_t)i * L, OW);
+        for (uint64_t j = tid; j < (uint64_t)n * L; j += NT) a.out_values[V + j] = lds[top + (uint32_t)(j % L)];
+      } else if (bi.codec == BIN_DICT) {
+        uint32_t* xi = (uint32_t*)(lds + bi.xoff);
+        materialize_idx(s, sh, idx, xi);
+        const uint2* tab = (const uint2*)(lds + bi.tab);
+        const uint32_t k = bi.k;
+        if (!sh.err)
+          bin_emit_rows<OW>(sh, lds, n, R, V, a, [&](uint32_t i) { return xi[i] < k ? tab[xi[i]].y : 0u; },
+                            [&](uint32_t i) { return xi[i] < k ? base + tab[xi[i]].x : 0u; });
+      } else {  // Freq: row bitmap of exceptions + prefix popcount -> exception rank
+        uint32_t* bits = (uint32_t*)(lds + bi.xoff);
+        const uint32_t nw = (n + 31) / 32;
+        uint32_t* pref = bits + nw;
+        for (uint32_t w = tid; w < nw; w += NT) bits[w] = 0;
+        __syncthreads();
+        for (uint32_t e = tid; e < bi.k; e += NT) {
+          const uint32_t row = roaring_select(s, sh, e);
+          atomicOr(&bits[row >> 5], 1u << (row & 31));
+        }
+        __syncthreads();
+        uint64_t carry = 0;
+        for (uint32_t w0 = 0; w0 < nw; w0 += NT) {
+          const uint32_t w = w0 + tid;
+          const uint32_t pc = w < nw ? __popc(bits[w]) : 0u;
+          uint32_t tot;
+          const uint32_t pre = block_excl_scan<uint32_t>(pc, sh, &tot);
+          if (w < nw) pref[w] = (uint32_t)carry + pre;
+          carry += tot;
+        }
+        __syncthreads();
+        const uint2* tab = (const uint2*)(lds + bi.tab);
+        const uint32_t L = bi.L, top = base + bi.top;
+        auto rank = [&](uint32_t i) {
+          const uint32_t word = bits[i >> 5], b = i & 31;
+          return pref[i >> 5] + __popc(word & ((1u << b) - 1));
+        };
+        auto exc = [&](uint32_t i) { return (bits[i >> 5] >> (i & 31)) & 1u; };
+        bin_emit_rows<OW>(sh, lds, n, R, V, a, [&](uint32_t i) { return exc(i) ? tab[rank(i)].y : L; },
+                          [&](uint32_t i) { return exc(i) ? base + tab[rank(i)].x : top; });
+      }
+    }
+    __syncthreads();
+    if (tid == 0) a.status[page] = sh.err;
+    __syncthreads();
+  }
+}
+
 }  // namespace sbk
 
 namespace sb {
@@ -1074,5 +1513,32 @@ int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a,
     case 8: return sbk::launch<8, false>(kind, a, s);
   }
   return -2;
+}
+}  // namespace sb
+
+namespace sb {
+int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream) {
+  sbk::BinArgs a{L.chunk, L.pages, L.n_pages, L.nullable, L.sizes, L.bases, L.total, L.out_offsets, L.out_values,
+                 L.values_cap, L.out_validity, L.status, kDeferredLds};
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 block(sbk::NT);
+  const dim3 grid(std::min<uint32_t>(L.n_pages ? L.n_pages : 1, kDeferredGrid));
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)sbk::k_bin_size<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
+    hipFuncSetAttribute((const void*)sbk::k_bin_size<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
+    hipFuncSetAttribute((const void*)sbk::k_bin_decode<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
+    hipFuncSetAttribute((const void*)sbk::k_bin_decode<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
+    attr = true;
+  }
+  if (stage == 0) {
+    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_size<8>, grid, block, kDeferredLds, st, a);
+    else hipLaunchKernelGGL(sbk::k_bin_size<4>, grid, block, kDeferredLds, st, a);
+    hipLaunchKernelGGL(sbk::k_bin_scan, dim3(1), block, 0, st, a);
+  } else {
+    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, kDeferredLds, st, a);
+    else hipLaunchKernelGGL(sbk::k_bin_decode<4>, grid, block, kDeferredLds, st, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb

@@ -633,3 +633,187 @@ int type_size(int phys) {
 
 }  // namespace enc
 }  // namespace sb
+
+// ===========================================================================
+// Binary / Utf8 pages: compress_binary (compression/binary/mod.rs:26-93),
+// gen_stats (:265-300), choose_compressor (:302-348), Dict (dict.rs:55-93),
+// Freq (freq.rs:44-100), OneValue (one_value.rs:50-68).
+// ===========================================================================
+namespace sb {
+namespace enc {
+
+namespace {
+
+struct BArr {
+  const uint8_t* values;
+  const int64_t* offsets;  // n + 1 absolute
+  const uint8_t* valid;
+  size_t n;
+  int ow;
+  uint64_t parent_len;
+  size_t len(size_t i) const { return (size_t)(offsets[i + 1] - offsets[i]); }
+  const uint8_t* str(size_t i) const { return values + offsets[i]; }
+};
+
+uint64_t fnv1a(const uint8_t* p, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; }
+  return h;
+}
+
+// distinct strings in first-occurrence order
+struct StrSet {
+  std::vector<uint64_t> h;
+  std::vector<uint32_t> id, cnt;
+  std::vector<uint8_t> used;
+  std::vector<size_t> row;  // representative row per id
+  size_t mask;
+  explicit StrSet(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 16) cap <<= 1;
+    h.resize(cap); id.resize(cap); cnt.resize(cap); used.assign(cap, 0);
+    mask = cap - 1;
+  }
+  uint32_t add(const BArr& a, size_t r, size_t* slot = nullptr) {
+    const size_t l = a.len(r);
+    const uint8_t* s = a.str(r);
+    const uint64_t hh = fnv1a(s, l);
+    size_t i = (size_t)((hh * 0x9E3779B97F4A7C15ull) >> 17) & mask;
+    for (;;) {
+      if (!used[i]) { used[i] = 1; h[i] = hh; id[i] = (uint32_t)row.size(); cnt[i] = 0; row.push_back(r); break; }
+      if (h[i] == hh) {
+        const size_t r2 = row[id[i]];
+        if (a.len(r2) == l && std::memcmp(a.str(r2), s, l) == 0) break;
+      }
+      i = (i + 1) & mask;
+    }
+    cnt[i]++;
+    if (slot) *slot = i;
+    return id[i];
+  }
+};
+
+}  // namespace
+
+int encode_binary_page(const uint8_t* values, const int64_t* offsets, const uint8_t* valid, size_t n, bool nullable,
+                       int ow, uint64_t parent_len, const Opts& opt, uint64_t seed, Bytes& out) {
+  Rng rng{seed};
+  if (nullable) write_validity(valid, n, out);
+  BArr a{values, offsets, valid, n, ow, parent_len};
+  StrSet m(n);
+  for (size_t i = 0; i < n; i++) m.add(a, i);
+  size_t nulls = 0;
+  for (size_t i = 0; i < n; i++) nulls += !bit(valid, i);
+  const size_t unique = m.row.size();
+  size_t total_unique = 0;
+  for (size_t r : m.row) total_unique += a.len(r) + 8;
+  const size_t total_bytes = (size_t)parent_len + (n + 1) * (size_t)ow;
+  size_t maxc = 0;
+  uint32_t top_id = 0;
+  for (size_t i = 0; i <= m.mask; i++) {
+    if (!m.used[i]) continue;
+    if (m.cnt[i] > maxc || (m.cnt[i] == maxc && m.id[i] < top_id)) { maxc = m.cnt[i]; top_id = m.id[i]; }
+  }
+  int codec = opt.default_codec;
+  const uint32_t fm = opt.forbidden;
+  if (opt.forced == kFreq && !(fm & (1u << kFreq))) codec = kFreq;
+  else if (opt.forced == kDict && !(fm & (1u << kDict))) codec = kDict;
+  else if (opt.has_ratio) {
+    double maxr = opt.ratio;
+    for (int c : {kOneValue, kFreq, kDict}) {
+      if (fm & (1u << c)) continue;
+      double r = 0.0;
+      if (c == kOneValue) r = unique <= 1 ? (double)n : 0.0;
+      else if (c == kFreq) {
+        if (unique > 1) {
+          if ((double)nulls / (double)n >= 0.9) r = (double)(n - 1);
+          else if ((double)maxc / (double)n >= 0.9) r = (double)(n - 1);
+        }
+      } else if (unique * 3 < n) {
+        const size_t after = total_unique + n * (bits_needed(unique) / 8) + n * 2 / 128;
+        r = (double)total_bytes / (double)after;
+      }
+      if (r > maxr) {
+        maxr = r;
+        codec = c;
+        if (r == (double)n) break;
+      }
+    }
+  }
+  const size_t hpos = out.size();
+  put<uint8_t>(out, (uint8_t)codec);
+  put<uint64_t>(out, 0);
+  const size_t before = out.size();
+  if (codec <= kSnappy) {
+    std::vector<uint8_t> ob((n + 1) * (size_t)ow);
+    for (size_t i = 0; i <= n; i++) {
+      const int64_t v = offsets[i] - offsets[0];
+      std::memcpy(ob.data() + i * ow, &v, (size_t)ow);
+    }
+    int rc = common_compress(codec, ob.data(), ob.size(), out);
+    if (rc) return rc;
+    const uint32_t cs = (uint32_t)(out.size() - before), us = (uint32_t)ob.size();
+    std::memcpy(out.data() + hpos + 1, &cs, 4);
+    std::memcpy(out.data() + hpos + 5, &us, 4);
+    const size_t h2 = out.size();
+    put<uint8_t>(out, (uint8_t)codec);
+    put<uint64_t>(out, 0);
+    const size_t b2 = out.size();
+    const size_t vl = (size_t)(offsets[n] - offsets[0]);
+    rc = common_compress(codec, values + offsets[0], vl, out);
+    if (rc) return rc;
+    const uint32_t cs2 = (uint32_t)(out.size() - b2), us2 = (uint32_t)vl;
+    std::memcpy(out.data() + h2 + 1, &cs2, 4);
+    std::memcpy(out.data() + h2 + 5, &us2, 4);
+    return 0;
+  }
+  if (codec == kOneValue) {
+    size_t l = 0;
+    const uint8_t* s = nullptr;
+    for (size_t i = 0; i < n; i++)
+      if (bit(valid, i)) { s = a.str(i); l = a.len(i); break; }
+    put<uint32_t>(out, (uint32_t)l);
+    if (l) out.insert(out.end(), s, s + l);
+  } else if (codec == kDict) {
+    StrSet d(n);
+    std::vector<uint32_t> idx(n);
+    for (size_t i = 0; i < n; i++) idx[i] = (!bit(valid, i) && i > 0) ? idx[i - 1] : d.add(a, i);
+    Opts o2 = opt;
+    o2.forbidden |= 1u << kDict;
+    Arr<uint32_t> ia{idx.data(), nullptr, n, false};
+    const int rc = compress_stream(ia, o2, rng, out);
+    if (rc) return rc;
+    put<uint32_t>(out, (uint32_t)d.row.size());
+    for (size_t r : d.row) {
+      put<uint64_t>(out, (uint64_t)a.len(r));
+      out.insert(out.end(), a.str(r), a.str(r) + a.len(r));
+    }
+  } else {  // Freq
+    const bool top_null = (double)nulls / (double)n >= 0.9;
+    size_t tl = 0;
+    const uint8_t* ts = nullptr;
+    if (!top_null) { ts = a.str(m.row[top_id]); tl = a.len(m.row[top_id]); }
+    std::vector<uint32_t> pos;
+    for (size_t i = 0; i < n; i++) {
+      if (!bit(valid, i)) continue;
+      if (top_null || a.len(i) != tl || std::memcmp(a.str(i), ts, tl) != 0) pos.push_back((uint32_t)i);
+    }
+    put<uint64_t>(out, (uint64_t)tl);
+    if (tl) out.insert(out.end(), ts, ts + tl);
+    Bytes bm;
+    roaring_serialize(pos, bm);
+    put<uint32_t>(out, (uint32_t)bm.size());
+    out.insert(out.end(), bm.begin(), bm.end());
+    for (uint32_t r : pos) {
+      put<uint64_t>(out, (uint64_t)a.len(r));
+      out.insert(out.end(), a.str(r), a.str(r) + a.len(r));
+    }
+  }
+  const uint32_t cs = (uint32_t)(out.size() - before), us = (uint32_t)parent_len;
+  std::memcpy(out.data() + hpos + 1, &cs, 4);
+  std::memcpy(out.data() + hpos + 5, &us, 4);
+  return 0;
+}
+
+}  // namespace enc
+}  // namespace sb

@@ -19,6 +19,11 @@ struct Opts {
 // One flat page of n rows (serialize.rs:52-132) appended to out.
 int encode_page(int phys, const void* values, const uint8_t* validity, size_t n, bool nullable, const Opts& opt,
                 uint64_t seed, std::vector<uint8_t>& out);
+// One Binary / Utf8 page: offsets are n+1 absolute positions into values;
+// ow = offset width (4 or 8); parent_len = the array's whole values length.
+int encode_binary_page(const uint8_t* values, const int64_t* offsets, const uint8_t* validity, size_t n,
+                       bool nullable, int ow, uint64_t parent_len, const Opts& opt, uint64_t seed,
+                       std::vector<uint8_t>& out);
 // Sampler seed of page `page` of a column written with `seed`.
 uint64_t page_seed(uint64_t seed, uint64_t page);
 int type_size(int phys);

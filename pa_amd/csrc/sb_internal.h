@@ -55,4 +55,21 @@ int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a,
 constexpr uint32_t kDeferredLds = 150 * 1024;
 constexpr uint32_t kDeferredGrid = 1024;
 
+// Binary / Utf8 columns: stage 0 = size pages + scan bases, stage 1 = decode.
+struct BinLaunch {
+  const uint8_t* chunk;
+  const PageDesc* pages;
+  uint32_t n_pages;
+  int nullable;
+  uint64_t* sizes;
+  uint64_t* bases;
+  uint64_t* total;
+  uint8_t* out_offsets;
+  uint8_t* out_values;
+  uint64_t values_cap;
+  uint32_t* out_validity;
+  uint32_t* status;
+};
+int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
+
 }  // namespace sb
