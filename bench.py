@@ -152,6 +152,85 @@ def cpu_baseline(wl: Workload, budget_s: float = 10.0) -> dict:
     }
 
 
+def decimal_strings(vals: np.ndarray):
+    """Decimal strings of non-negative ints (tests/it/io.rs:385-397 shape),
+    vectorized: -> (values bytes, int64 offsets)."""
+    v = vals.astype(np.int64)
+    nd = np.ones(len(v), np.int64)
+    for k in range(1, 19):
+        nd += v >= 10**k
+    offs = np.zeros(len(v) + 1, np.int64)
+    np.cumsum(nd, out=offs[1:])
+    out = np.empty(int(offs[-1]), np.uint8)
+    pos = offs[1:] - 1  # last digit of each row
+    x = v.copy()
+    left = nd.copy()
+    while True:
+        m = left > 0
+        if not m.any():
+            break
+        out[pos[m]] = (48 + x[m] % 10).astype(np.uint8)
+        x[m] //= 10
+        pos[m] -= 1
+        left[m] -= 1
+    return out.tobytes(), offs
+
+
+class WorkloadC3:
+    """BASELINE.json configs[2]: nullable Float64 + nullable Utf8, LZ4 pages,
+    ratio None (always the general codec), 10 % nulls, 8192-row pages.
+    A step decodes both columns; two input/output copies rotate."""
+
+    def __init__(self, torch, pa, rows, seed, device, threads):
+        rng = np.random.default_rng(seed)
+        self.rows = rows
+        f = np.round(rng.standard_normal(rows) * 1e4, 2)
+        fvalid = rng.random(rows) >= 0.1
+        svals, soffs = decimal_strings(rng.integers(0, 10**6, rows))
+        svalid = rng.random(rows) >= 0.1
+        opts = pa.WriteOptions(default_compression=1, default_compress_ratio=None, max_page_size=PAGE_ROWS, seed=seed)
+        self.fchunk, self.fmetas = pa.encode_column(f, fvalid, True, opts, n_threads=threads)
+        self.schunk, self.smetas = pa.encode_binary_column(svals, soffs, svalid, True, opts, physical_type=pa.UTF8,
+                                                           n_threads=threads)
+        dev = f"cuda:{device}"
+        fh = torch.from_numpy(np.frombuffer(self.fchunk, np.uint8).copy())
+        sh = torch.from_numpy(np.frombuffer(self.schunk, np.uint8).copy())
+        self.fdec = [pa.ColumnDecoder(fh.to(dev), self.fmetas, np.float64, True) for _ in range(2)]
+        self.sdec = [pa.BinaryColumnDecoder(sh.to(dev), self.smetas, pa.UTF8, True) for _ in range(2)]
+        self.fout = [d.alloc_outputs() for d in self.fdec]
+        self.sout = [d.alloc_outputs() for d in self.sdec]
+        self.in_bytes = len(self.fchunk) + len(self.schunk)
+        nb = (rows + 7) // 8
+        self.out_bytes = rows * 8 + nb + 4 * (rows + 1) + len(svals) + nb
+        self.exp = (torch.from_numpy(f.view(np.int64)).to(dev), torch.from_numpy(np.packbits(fvalid, bitorder="little")).to(dev),
+                    torch.from_numpy(soffs.astype(np.int32)).to(dev), torch.from_numpy(np.frombuffer(svals, np.uint8).copy()).to(dev),
+                    torch.from_numpy(np.packbits(svalid, bitorder="little")).to(dev))
+        torch.cuda.synchronize()
+
+    def step(self, k):
+        self.fdec[k & 1].decode_async(*self.fout[k & 1])
+        self.sdec[k & 1].decode_async(*self.sout[k & 1])
+
+    def verify(self, torch) -> bool:
+        ok = True
+        nb = (self.rows + 7) // 8
+        for i in range(2):
+            self.fdec[i].check()
+            self.sdec[i].check()
+            fv, fm = self.fout[i]
+            so, sv, sm = self.sout[i]
+            ok &= bool(torch.equal(fv[: self.rows], self.exp[0]))
+            ok &= bool(torch.equal(fm[:nb], self.exp[1]))
+            ok &= bool(torch.equal(so, self.exp[2]))
+            ok &= bool(torch.equal(sv[: self.exp[3].numel()], self.exp[3]))
+            ok &= bool(torch.equal(sm[:nb], self.exp[4]))
+        return ok
+
+    @property
+    def decs(self):
+        return self.fdec + self.sdec
+
+
 def load_traffic(workload: str):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -171,6 +250,8 @@ def main():
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-b12", action="store_true", help="skip the all-bitpack b=12 variant")
+    ap.add_argument("--no-c3", action="store_true", help="skip the config-3 (Float64 + Utf8, LZ4) workload")
+    ap.add_argument("--c3-rows", type=int, default=100_000_000)
     args = ap.parse_args()
 
     import torch
@@ -215,6 +296,23 @@ def main():
             "bit_exact": bool(ok12),
         }
         del wl12
+
+    if not args.no_c3:
+        wl3 = WorkloadC3(torch, pa_amd, args.c3_rows, 77 + rank, local, threads)
+        w3, k3, ok3 = timed(torch, dist, wl3, max(3, args.steps // 4), args.warmup)
+        steps3 = max(3, args.steps // 4)
+        extra["c3_f64_utf8_lz4_nullable"] = {
+            "rows": args.c3_rows,
+            "decoded_GBps": round(wl3.out_bytes * steps3 / w3 / 1e9, 1),
+            "ms_per_step": round(w3 / steps3 * 1e3, 3),
+            "step_traffic_GBps": round((wl3.in_bytes + wl3.out_bytes) / (float(np.mean(k3)) / 1e3) / 1e9, 1),
+            "roofline_frac": round((wl3.in_bytes + wl3.out_bytes) / (float(np.mean(k3)) / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "compressed_bytes": wl3.in_bytes,
+            "decoded_bytes": wl3.out_bytes,
+            "bit_exact": bool(ok3),
+            "kernels": "k_decode_staged<8,true> + k_decode_deferred<8,true> (LZ4) + k_bin_decode<4>",
+        }
+        del wl3
 
     if rank == 0:
         line = {
