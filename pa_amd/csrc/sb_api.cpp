@@ -33,9 +33,13 @@ struct sb_plan {
   sb::PageDesc* d_pages = nullptr;
   uint32_t* d_status = nullptr;
   uint32_t* d_lists = nullptr;  // [staged list | global list]
-  uint32_t* d_defer = nullptr;  // [count parity 0, count parity 1, work list...]
+  uint32_t* d_defer = nullptr;  // [defer count x2 | inflate job count x2 | work list...]
+  sb::InflateJob* d_jobs = nullptr;  // fixed: one per page; binary: two per page
+  uint8_t* d_scratch = nullptr;      // binary: expanded offsets streams
+  uint32_t n_bin_jobs = 0;
   uint64_t decodes = 0;
   int deferred_state = -1;  // -1 unknown, 0 no deferred pages, 1 some
+  int inflate_state = -1;   // same, for k_inflate jobs
   bool binary = false;
   int offset_width = 0;
   uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1]
@@ -140,6 +144,8 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_status) (void)hipFree(p->d_status);
   if (p->d_lists) (void)hipFree(p->d_lists);
   if (p->d_defer) (void)hipFree(p->d_defer);
+  if (p->d_jobs) (void)hipFree(p->d_jobs);
+  if (p->d_scratch) (void)hipFree(p->d_scratch);
   if (p->d_bin) (void)hipFree(p->d_bin);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
@@ -204,8 +210,9 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
   if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&p->d_lists, np * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMalloc(&p->d_defer, (np + 2) * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemsetAsync(p->d_defer, 0, 2 * sizeof(uint32_t), ctx->stream);
+  if (e == hipSuccess) e = hipMalloc(&p->d_defer, (np + 4) * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(p->d_defer, 0, 4 * sizeof(uint32_t), ctx->stream);
+  if (e == hipSuccess) e = hipMalloc(&p->d_jobs, (owidth ? 2 : 1) * np * sizeof(sb::InflateJob));
   if (e == hipSuccess) e = hipEventCreate(&p->ev0);
   if (e == hipSuccess) e = hipEventCreate(&p->ev1);
   if (e == hipSuccess && n_pages) {
@@ -228,7 +235,7 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
       return fail(ctx, SB_E_DEVICE, "plan alloc: %s", hipGetErrorString(e));
     }
     sb::BinLaunch L{d_chunk, p->d_pages, (uint32_t)n_pages, desc->nullable, p->d_bin, p->d_bin + np,
-                    p->d_bin + 2 * np, nullptr, nullptr, 0, nullptr, p->d_status};
+                    p->d_bin + 2 * np, nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr};
     if (sb::launch_binary(0, owidth, L, ctx->stream) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "binary sizing failed: %s", hipGetErrorString(hipGetLastError()));
@@ -236,11 +243,16 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     std::vector<uint32_t> st(n_pages);
     (void)hipMemcpy(st.data(), p->d_status, n_pages * 4, hipMemcpyDeviceToHost);
     (void)hipMemcpy(&p->values_bytes, p->d_bin + 2 * np, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&p->n_bin_jobs, p->d_defer + 2, 4, hipMemcpyDeviceToHost);
     for (uint64_t i = 0; i < n_pages; i++) {
       if (st[i]) {
         sb_plan_destroy(p);
         return fail(ctx, (sb_status)st[i], "page %llu: %s", (unsigned long long)i, sb_status_str((int)st[i]));
       }
+    }
+    if (p->n_bin_jobs && hipMalloc(&p->d_scratch, (rows + n_pages) * (uint64_t)owidth) != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "plan alloc: scratch");
     }
   }
   *out = p;
@@ -263,7 +275,13 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   const size_t np = p->n_pages;
   sb::BinLaunch L{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
                   (uint8_t*)out->d_offsets, out->d_values, out->values_capacity, (uint32_t*)out->d_validity,
-                  p->d_status};
+                  p->d_status, p->d_jobs, nullptr, p->d_scratch};
+  if (p->n_bin_jobs) {  // Basic LZ4 / Snappy pages: streams expanded first, one wave each
+    sb::InflateLaunch I{p->d_chunk, p->d_jobs, nullptr, p->n_bin_jobs, out->d_values, p->d_scratch, p->d_bin + np,
+                        p->d_status};
+    if (sb::launch_inflate(I, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
   if (sb::launch_binary(1, p->offset_width, L, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (p->timing) {
@@ -291,7 +309,9 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   a.status = p->d_status;
   a.stage_bytes = p->stage_bytes;
   a.defer_count = p->d_defer;
-  a.defer_list = p->d_defer + 2;
+  a.job_count = p->d_defer + 2;
+  a.defer_list = p->d_defer + 4;
+  a.jobs = p->d_jobs;
   a.parity = (uint32_t)(p->decodes & 1);
   p->decodes++;
   a.list = p->staged_identity ? nullptr : p->d_lists;
@@ -302,6 +322,13 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   a.n_list = p->n_global;
   if (sb::launch_decode_fixed(p->width, p->is_float, 1, a, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "global decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (p->inflate_state != 0 && p->n_pages) {
+    // CH_LEAF LZ4 / Snappy pages listed by the pass above: values straight into the column
+    sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2 + a.parity, (uint32_t)p->n_pages,
+                        (uint8_t*)out->d_values, nullptr, nullptr, p->d_status};
+    if (sb::launch_inflate(I, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
   if (p->deferred_state != 0 && p->n_pages) {
     // pages whose leaf stream is LZ4 / Zstd / Snappy / Patas, listed by the pass above
     a.list = nullptr;
@@ -325,10 +352,13 @@ sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
   if (!p->n_pages) return SB_OK;
   std::vector<uint32_t> st(p->n_pages);
   HIP_TRY(ctx, hipMemcpy(st.data(), p->d_status, p->n_pages * 4, hipMemcpyDeviceToHost));
-  if (p->decodes && p->deferred_state == -1) {  // the plan's pages are fixed: learn once
-    uint32_t cnt = 0;
-    HIP_TRY(ctx, hipMemcpy(&cnt, p->d_defer + ((p->decodes - 1) & 1), 4, hipMemcpyDeviceToHost));
-    p->deferred_state = cnt ? 1 : 0;
+  if (!p->binary && p->decodes && (p->deferred_state == -1 || p->inflate_state == -1)) {
+    // the plan's pages are fixed: learn once which passes they need
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    HIP_TRY(ctx, hipMemcpy(cnt, p->d_defer, sizeof cnt, hipMemcpyDeviceToHost));
+    const uint32_t par = (uint32_t)((p->decodes - 1) & 1);
+    p->deferred_state = cnt[par] ? 1 : 0;
+    p->inflate_state = cnt[2 + par] ? 1 : 0;
   }
   for (uint64_t i = 0; i < p->n_pages; i++) {
     if (st[i]) {

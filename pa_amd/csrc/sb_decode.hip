@@ -630,117 +630,534 @@ __device__ bool parse_dict(const Src& s, Shared& sh, const Stream& st, uint32_t 
 
 
 // ---------------------------------------------------------------------------
-// general codecs and Patas, expanded into LDS by wave 0 (deferred pages)
+// general codecs: wave-level LZ4 / Snappy block decoder
 // ---------------------------------------------------------------------------
 // LZ4 raw block (basic.rs:87-91 -> liblz4 LZ4_decompress_safe with the exact
-// output size).  Tokens are parsed by every lane of the wave (uniform LDS
-// reads); literal and match bytes are copied lane-parallel.  A match copy
-// reads only bytes before `op`: byte i of a match is out[op - off + i % off].
+// output size) and Snappy raw (basic.rs:99-106, snap 1.1 raw::Decoder).  The
+// format is a serial token stream, so one wave decodes one stream and pages
+// run side by side, many waves per CU:
+//  * input: a window of four 256-byte register blocks (one dword per lane
+//    each) slides over the compressed bytes in HBM, prefetching 768 bytes
+//    ahead; tokens are parsed in scalar registers (v_readlane at the uniform
+//    position) and literal bytes fetched lane-parallel with ds_bpermute;
+//  * output: RING mode keeps the last kRing bytes in a per-wave LDS ring and
+//    writes each completed kChunk to HBM; match bytes older than the ring
+//    are re-read from HBM at device scope (those chunks were written and
+//    waited for at least two chunks earlier).  FULL mode keeps the whole
+//    output in LDS (the deferred pass decodes from it).
+// A match byte i is out[op - off + i] (off >= 64) or out[op - off + i % off],
+// which always lies before op: overlapping copies replicate the period.
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
-__device__ uint32_t lz4_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, uint32_t olen) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t ip = 0, op = 0;
-  if (ilen == 0) return olen == 0 ? ST_OK : ST_CODEC;
+#ifndef SB_INF_WPB
+#define SB_INF_WPB 4
+#endif
+constexpr uint32_t kRing = 4096, kChunk = 1024;
+constexpr uint32_t kInfWaves = SB_INF_WPB;  // waves (jobs in flight) per k_inflate workgroup
+
+typedef const __attribute__((address_space(1))) uint32_t gmem_u32;
+typedef const __attribute__((address_space(1))) uint8_t gmem_u8;
+
+// (Stream pointers are global-address-space: a flat load is divergent to the
+// compiler even at a uniform address, which would push the parse into VGPRs.)
+struct WaveWin {
+  gmem_u32* g;        // dword-aligned base of the stream
+  uint32_t nd;        // dwords of g holding stream bytes
+  uint32_t lo;        // byte position (from g) of w0 lane 0, a multiple of 4
+  uint32_t w0, w1, w2, w3;  // blocks [lo, lo + 256), ... [lo + 768, lo + 1024)
+
+  // clamped, not predicated: a select on the loaded value would wait for it
+  __device__ __forceinline__ uint32_t ld(uint32_t dw) const { return __builtin_nontemporal_load(g + min(dw, nd - 1)); }
+  __device__ void init(const uint8_t* start, uint32_t len) {
+    g = (gmem_u32*)((uintptr_t)start & ~(uintptr_t)3);
+    nd = (((uint32_t)((uintptr_t)start & 3)) + len + 3) >> 2;
+    seek((uint32_t)((uintptr_t)start & 3));
+  }
+  __device__ void seek(uint32_t pos) {
+    const uint32_t lane = threadIdx.x & 63;
+    lo = pos & ~3u;
+    const uint32_t d = (lo >> 2) + lane;
+    w0 = ld(d);
+    w1 = ld(d + 64);
+    w2 = ld(d + 128);
+    w3 = ld(d + 192);
+  }
+  // after slide(pos): pos - lo < 256.  The shift only waits for the load
+  // issued one slide earlier; parsing reads w0 / w1 alone.
+  __device__ __forceinline__ void slide(uint32_t pos) {
+    if (pos - lo < 256) return;
+    if (pos - lo >= 512) { seek(pos); return; }
+    w0 = w1;
+    w1 = w2;
+    w2 = w3;
+    lo += 256;
+    w3 = ld((lo >> 2) + 192 + (threadIdx.x & 63));
+  }
+  // uniform byte at pos (the caller bounds pos by the stream end)
+  __device__ __forceinline__ uint32_t byte(uint32_t pos) const {
+    const uint32_t r = pos - lo;
+    uint32_t d;
+    if (r < 256) d = __builtin_amdgcn_readlane(w0, r >> 2);
+    else if (r < 512) d = __builtin_amdgcn_readlane(w1, (r >> 2) - 64);
+    else return ((gmem_u8*)g)[pos];  // past the window (long length runs)
+    return (d >> ((r & 3) * 8)) & 0xFFu;
+  }
+  // byte at pos + lane, for pos - lo < 256
+  __device__ __forceinline__ uint32_t lane_byte(uint32_t pos) const {
+    const uint32_t r = pos - lo + (threadIdx.x & 63);
+    const int addr = (int)(((r >> 2) & 63) << 2);
+    const uint32_t a = __builtin_amdgcn_ds_bpermute(addr, (int)w0), b = __builtin_amdgcn_ds_bpermute(addr, (int)w1);
+    return ((r < 256 ? a : b) >> ((r & 3) * 8)) & 0xFFu;
+  }
+};
+
+template <bool RING>
+struct WaveOut {
+  lds_u8* ring;   // RING: kRing bytes (16-byte aligned); FULL: olen bytes
+  uint8_t* dst;   // RING: HBM destination of the whole stream
+  __amdgpu_buffer_rsrc_t rs;  // RING: dst, olen bytes (far history reads)
+  uint32_t olen;
+  uint32_t op;
+
+  __device__ __forceinline__ uint32_t slot(uint32_t q) const { return RING ? (q & (kRing - 1)) : q; }
+  // History below this position is read from HBM: writes of up to one chunk
+  // past op overwrite the ring slots of chunks k-4 and k-3, and the flushes of
+  // chunks <= k-2 have completed (each flush first waits for the previous).
+  __device__ __forceinline__ uint32_t far_limit() const {
+    const uint32_t k = op / kChunk;
+    return k >= 2 ? (k - 2) * kChunk : 0u;
+  }
+  __device__ __forceinline__ uint32_t room() const {
+    return RING ? min(64u, kChunk - (op & (kChunk - 1))) : 64u;
+  }
+  __device__ void flush(uint32_t c0, uint32_t len) {
+    const uint32_t lane = threadIdx.x & 63;
+    // the previous chunk's stores must complete before far reads may use them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint8_t* d = dst + c0;
+    if (len == kChunk) {
+      const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(ring + slot(c0 + 16 * lane));
+      const uintptr_t al = (uintptr_t)d;
+      if ((al & 15) == 0) {
+        ((u32x4*)d)[lane] = v;
+      } else if ((al & 3) == 0) {
+        uint32_t* q = (uint32_t*)(d + 16 * lane);
+        q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 16; j++) d[j * 64 + lane] = ring[slot(c0 + j * 64 + lane)];
+      }
+      return;
+    }
+    for (uint32_t j = lane; j < len; j += 64) d[j] = ring[slot(c0 + j)];
+  }
+  __device__ __forceinline__ void advance(uint32_t m) {
+    op += m;
+    if (RING && (op & (kChunk - 1)) == 0) flush(op - kChunk, kChunk);
+  }
+  __device__ __forceinline__ void lit(const WaveWin& w, uint32_t pos, uint32_t m) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t v = w.lane_byte(pos);
+    if (lane < m) ring[slot(op + lane)] = (uint8_t)v;
+    advance(m);
+  }
+  __device__ __forceinline__ void match(uint32_t off, uint32_t m) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (lane < m) {
+      const uint32_t q = op - off + (off >= 64 ? lane : lane % off);
+      uint32_t v;
+      if (RING && q < far_limit())
+        v = __builtin_amdgcn_raw_buffer_load_b8(rs, q, 0, 16);  // sc1: device scope, misses L1
+      else
+        v = ring[slot(q)];
+      ring[slot(op + lane)] = (uint8_t)v;
+    }
+    advance(m);
+  }
+  __device__ __forceinline__ void finish() {
+    if (RING && (op & (kChunk - 1))) flush(op & ~(kChunk - 1), op & (kChunk - 1));
+  }
+  __device__ __forceinline__ uint32_t hist(uint32_t q) const {
+    if (RING && q < far_limit()) return __builtin_amdgcn_raw_buffer_load_b8(rs, q, 0, 16);
+    return ring[slot(q)];
+  }
+  // len literal bytes from HBM, up to a chunk per step (16 loads per lane in flight)
+  __device__ void lit_global(gmem_u8* src, uint32_t len) {
+    const uint32_t lane = threadIdx.x & 63;
+    while (len) {
+      const uint32_t m = min(len, RING ? kChunk - (op & (kChunk - 1)) : kChunk);
+      uint32_t b[16];
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j++) b[j] = src[min(lane + 64 * j, m - 1)];
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j++)
+        if (lane + 64 * j < m) ring[slot(op + lane + 64 * j)] = (uint8_t)b[j];
+      src += m;
+      len -= m;
+      advance(m);
+    }
+  }
+};
+
+template <bool RING>
+__device__ uint32_t lz4_wave(WaveWin& w, uint32_t p, uint32_t pend, WaveOut<RING>& o) {
+  const uint32_t olen = o.olen;
+  if (p == pend) return olen == 0 ? ST_OK : ST_CODEC;
   for (;;) {
-    if (ip >= ilen) return ST_CODEC;
-    const uint32_t token = in[ip++];
+    w.slide(p);
+    const uint32_t token = w.byte(p++);
     uint32_t lit = token >> 4;
     if (lit == 15) {
       uint32_t b;
       do {
-        if (ip >= ilen) return ST_CODEC;
-        b = in[ip++];
+        if (p >= pend) return ST_CODEC;
+        b = w.byte(p++);
         lit += b;
       } while (b == 255);
     }
-    if (lit > ilen - ip || lit > olen - op) return ST_CODEC;
-    for (uint32_t i = lane; i < lit; i += 64) out[op + i] = in[ip + i];
-    ip += lit;
-    op += lit;
-    if (ip == ilen) break;  // the last sequence carries literals only
-    if (ip + 2 > ilen) return ST_CODEC;
-    const uint32_t off = in[ip] | ((uint32_t)in[ip + 1] << 8);
-    ip += 2;
-    if (off == 0 || off > op) return ST_CODEC;
+    if (lit > pend - p || lit > olen - o.op) return ST_CODEC;
+    while (lit) {
+      w.slide(p);
+      const uint32_t m = min(lit, o.room());
+      o.lit(w, p, m);
+      p += m;
+      lit -= m;
+    }
+    if (p == pend) break;  // the last sequence carries literals only
+    if (pend - p < 2) return ST_CODEC;
+    w.slide(p);
+    const uint32_t off = w.byte(p) | (w.byte(p + 1) << 8);
+    p += 2;
+    if (off == 0 || off > o.op) return ST_CODEC;
     uint32_t ml = (token & 15) + 4;
     if ((token & 15) == 15) {
       uint32_t b;
       do {
-        if (ip >= ilen) return ST_CODEC;
-        b = in[ip++];
+        if (p >= pend) return ST_CODEC;
+        b = w.byte(p++);
         ml += b;
       } while (b == 255);
     }
-    if (ml > olen - op) return ST_CODEC;
-    if (off >= ml) {
-      for (uint32_t i = lane; i < ml; i += 64) out[op + i] = out[op - off + i];
-    } else {
-      for (uint32_t i = lane; i < ml; i += 64) out[op + i] = out[op - off + i % off];
+    if (ml > olen - o.op) return ST_CODEC;
+    while (ml) {
+      const uint32_t m = min(ml, o.room());
+      o.match(off, m);
+      ml -= m;
     }
-    op += ml;
   }
-  return op == olen ? ST_OK : ST_CODEC;
+  if (o.op != olen) return ST_CODEC;
+  o.finish();
+  return ST_OK;
 }
 
-// Snappy raw (basic.rs:99-106, snap 1.1 raw::Decoder): varint length, then
-// literal / copy-1 / copy-2 / copy-4 elements.
-__device__ uint32_t snappy_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, uint32_t olen) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t ip = 0, op = 0;
+// Snappy raw: varint length, then literal / copy-1 / copy-2 / copy-4 elements.
+template <bool RING>
+__device__ uint32_t snappy_wave(WaveWin& w, uint32_t p, uint32_t pend, WaveOut<RING>& o) {
+  const uint32_t olen = o.olen;
   uint64_t ulen = 0;
   for (uint32_t sft = 0;; sft += 7) {
-    if (ip >= ilen || sft > 35) return ST_CODEC;
-    const uint32_t c = in[ip++];
+    if (p >= pend || sft > 35) return ST_CODEC;
+    const uint32_t c = w.byte(p++);
     ulen |= (uint64_t)(c & 0x7F) << sft;
     if (!(c & 0x80)) break;
   }
   if (ulen != olen) return ST_CODEC;
-  while (ip < ilen) {
-    const uint32_t tag = in[ip++];
+  while (p < pend) {
+    w.slide(p);
+    const uint32_t tag = w.byte(p++);
     const uint32_t type = tag & 3;
     if (type == 0) {
       uint32_t len = (tag >> 2) + 1;
       if (len > 60) {
         const uint32_t nb = len - 60;
-        if (ip + nb > ilen) return ST_CODEC;
+        if (pend - p < nb) return ST_CODEC;
         len = 0;
-        for (uint32_t i = 0; i < nb; i++) len |= (uint32_t)in[ip + i] << (8 * i);
+        for (uint32_t i = 0; i < nb; i++) len |= w.byte(p + i) << (8 * i);
         len += 1;
-        ip += nb;
+        p += nb;
       }
-      if (len > ilen - ip || len > olen - op) return ST_CODEC;
-      for (uint32_t i = lane; i < len; i += 64) out[op + i] = in[ip + i];
-      ip += len;
-      op += len;
+      if (len > pend - p || len > olen - o.op) return ST_CODEC;
+      while (len) {
+        w.slide(p);
+        const uint32_t m = min(len, o.room());
+        o.lit(w, p, m);
+        p += m;
+        len -= m;
+      }
     } else {
       uint32_t len, off;
       if (type == 1) {
-        if (ip + 1 > ilen) return ST_CODEC;
+        if (pend - p < 1) return ST_CODEC;
         len = ((tag >> 2) & 7) + 4;
-        off = ((tag >> 5) << 8) | in[ip];
-        ip += 1;
+        off = ((tag >> 5) << 8) | w.byte(p);
+        p += 1;
       } else if (type == 2) {
-        if (ip + 2 > ilen) return ST_CODEC;
+        if (pend - p < 2) return ST_CODEC;
         len = (tag >> 2) + 1;
-        off = in[ip] | ((uint32_t)in[ip + 1] << 8);
-        ip += 2;
+        off = w.byte(p) | (w.byte(p + 1) << 8);
+        p += 2;
       } else {
-        if (ip + 4 > ilen) return ST_CODEC;
+        if (pend - p < 4) return ST_CODEC;
         len = (tag >> 2) + 1;
-        off = in[ip] | ((uint32_t)in[ip + 1] << 8) | ((uint32_t)in[ip + 2] << 16) | ((uint32_t)in[ip + 3] << 24);
-        ip += 4;
+        off = w.byte(p) | (w.byte(p + 1) << 8) | (w.byte(p + 2) << 16) | (w.byte(p + 3) << 24);
+        p += 4;
       }
-      if (off == 0 || off > op || len > olen - op) return ST_CODEC;
-      if (off >= len) {
-        for (uint32_t i = lane; i < len; i += 64) out[op + i] = out[op - off + i];
-      } else {
-        for (uint32_t i = lane; i < len; i += 64) out[op + i] = out[op - off + i % off];
+      if (off == 0 || off > o.op || len > olen - o.op) return ST_CODEC;
+      while (len) {
+        const uint32_t m = min(len, o.room());
+        o.match(off, m);
+        len -= m;
       }
-      op += len;
     }
   }
-  return op == olen ? ST_OK : ST_CODEC;
+  if (o.op != olen) return ST_CODEC;
+  o.finish();
+  return ST_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// Batched LZ4 (k_inflate).  A serial token walk costs ~1000 cycles per
+// sequence on one wave, and the pages' streams hold a sequence every ~5
+// compressed bytes, so the walk is restated data-parallel per batch:
+//  1. every lane parses a sequence at 4 candidate positions p + 4 lane + k
+//     (k < 4) and packs the byte distance to its successor (0 = take the
+//     serial path: final literal-only sequence, literal > kLitFast, lengths
+//     past the staged input, a distance > 255);
+//  2. a scalar chase follows successors from p (one v_readlane per sequence)
+//     and deals the true sequence starts to lanes;
+//  3. lanes decode their sequence, a wave scan places the outputs (at most a
+//     chunk per batch), literals are copied lane-parallel, then matches whose
+//     source ends before the batch's first match byte are copied
+//     lane-parallel and the rest in sequence order, wave-wide.
+// The compressed stream is staged by LDS-DMA into a per-wave kIb ring.
+constexpr uint32_t kIb = 4096, kScan = 256, kLitFast = 64, kMatchFast = 32;
+
+struct InRing {
+  gmem_u32* g;   // dword-aligned stream base
+  uint32_t nd;   // stream dwords
+  lds_u8* ib;    // kIb bytes: stream byte x at ib[x % kIb]
+  uint32_t base; // [base, base + 3 KiB) staged and complete; base % 1 KiB == 0
+
+  __device__ __forceinline__ void dma(uint32_t b) {  // [b, b + 1 KiB) -> ib
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t dw = min((b >> 2) + 64 * k + lane, nd - 1);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g + dw),
+                                       (__attribute__((address_space(3))) void*)(ib + (b & (kIb - 1)) + 256 * k), 4,
+                                       0, 0);
+    }
+  }
+  __device__ void seek(uint32_t x) {
+    base = x & ~1023u;
+    for (uint32_t k = 0; k < 4; k++) dma(base + 1024 * k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __device__ __forceinline__ void slide(uint32_t p) {
+    if (p - base < 1024) return;
+    if (p - base >= 3072) { seek(p); return; }
+    do {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the in-flight KiB is complete
+      dma(base + 4096);                                    // into the slot of base
+      base += 1024;
+    } while (p - base >= 1024);
+  }
+  __device__ __forceinline__ uint32_t ubyte(uint32_t x) const {  // uniform
+    if (x - base < 3072) return ib[x & (kIb - 1)];
+    return ((gmem_u8*)g)[x];
+  }
+};
+
+struct Seq {
+  uint32_t lit_pos, lit, off, ml, next;
+};
+
+// Lane-parallel parse of the sequence at x from the staged input; false when
+// it must take the serial path.  lim: end of the staged, complete input.
+__device__ __forceinline__ bool seq_at(const lds_u8* ib, uint32_t x, uint32_t lim, uint32_t pend, Seq& s) {
+  if (x >= lim) return false;
+  const uint32_t t = ib[x & (kIb - 1)];
+  uint32_t y = x + 1, lit = t >> 4;
+  if (lit == 15) {
+    uint32_t b;
+    do {
+      if (y >= lim) return false;
+      b = ib[y & (kIb - 1)];
+      y++;
+      lit += b;
+    } while (b == 255 && lit <= kLitFast);
+  }
+  if (lit > kLitFast) return false;
+  const uint32_t le = y + lit;
+  if (le + 2 > lim || le >= pend) return false;  // (le == pend: the final sequence)
+  s.lit_pos = y;
+  s.lit = lit;
+  s.off = ib[le & (kIb - 1)] | ((uint32_t)ib[(le + 1) & (kIb - 1)] << 8);
+  y = le + 2;
+  uint32_t ml = (t & 15) + 4;
+  if ((t & 15) == 15) {
+    uint32_t b;
+    do {
+      if (y >= lim) return false;
+      b = ib[y & (kIb - 1)];
+      y++;
+      ml += b;
+    } while (b == 255);
+  }
+  s.ml = ml;
+  s.next = y;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += y;
+  }
+  return v;
+}
+
+// One sequence at *pp, serially (the liblz4 checks of lz4_wave).
+__device__ uint32_t lz4_one(InRing& in, uint32_t* pp, uint32_t pend, WaveOut<true>& o, bool* ended) {
+  uint32_t p = *pp;
+  const uint32_t olen = o.olen;
+  const uint32_t token = in.ubyte(p++);
+  uint32_t lit = token >> 4;
+  if (lit == 15) {
+    uint32_t b;
+    do {
+      if (p >= pend) return ST_CODEC;
+      b = in.ubyte(p++);
+      lit += b;
+    } while (b == 255);
+  }
+  if (lit > pend - p || lit > olen - o.op) return ST_CODEC;
+  o.lit_global((gmem_u8*)in.g + p, lit);
+  p += lit;
+  if (p == pend) {  // the last sequence carries literals only
+    *ended = true;
+    *pp = p;
+    return ST_OK;
+  }
+  if (pend - p < 2) return ST_CODEC;
+  const uint32_t off = in.ubyte(p) | (in.ubyte(p + 1) << 8);
+  p += 2;
+  if (off == 0 || off > o.op) return ST_CODEC;
+  uint32_t ml = (token & 15) + 4;
+  if ((token & 15) == 15) {
+    uint32_t b;
+    do {
+      if (p >= pend) return ST_CODEC;
+      b = in.ubyte(p++);
+      ml += b;
+    } while (b == 255);
+  }
+  if (ml > olen - o.op) return ST_CODEC;
+  while (ml) {
+    const uint32_t m = min(ml, o.room());
+    o.match(off, m);
+    ml -= m;
+  }
+  *pp = p;
+  return ST_OK;
+}
+
+__device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<true>& o) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t olen = o.olen;
+  if (p == pend) return olen == 0 ? ST_OK : ST_CODEC;
+  bool ended = false;
+  while (p < pend && !ended) {
+    in.slide(p);
+    const uint32_t lim = min(in.base + 3072, pend);
+    // 1. successor distances of the candidate starts
+    uint32_t packed = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t x = p + 4 * lane + k;
+      Seq s;
+      if (seq_at(in.ib, x, lim, pend, s) && s.next - x <= 255) packed |= (s.next - x) << (8 * k);
+    }
+    // 2. chase from p
+    uint32_t q = p, j = 0, starts = 0;
+    while (j < 64 && q - p < kScan) {
+      const uint32_t r = q - p;
+      const uint32_t d = (__builtin_amdgcn_readlane(packed, r >> 2) >> ((r & 3) * 8)) & 0xFFu;
+      if (!d) break;
+      starts = lane == j ? q : starts;
+      q += d;
+      j++;
+    }
+    // 3. decode and place
+    Seq s{0, 0, 0, 0, 0};
+    const bool v0 = lane < j && seq_at(in.ib, starts, lim, pend, s);
+    const uint32_t len = v0 ? s.lit + s.ml : 0u;
+    const uint32_t incl = wave_incl_scan(len), excl = incl - len;
+    const uint32_t cap = min(kChunk, olen - o.op);
+    const uint32_t dl = o.op + excl, dm = dl + s.lit;  // literal and match destinations
+    const bool ok = v0 && incl <= cap && s.off != 0 && s.off <= dm;
+    const uint64_t okm = __ballot(ok);
+    const uint32_t k = okm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);
+    if (k == 0) {  // the serial path takes one sequence (and reports errors)
+      const uint32_t st = lz4_one(in, &p, pend, o, &ended);
+      if (st) return st;
+      continue;
+    }
+    const bool v = lane < k;
+    for (uint32_t i = 0; __ballot(v && i < s.lit); i++)
+      if (v && i < s.lit) o.ring[(dl + i) & (kRing - 1)] = in.ib[(s.lit_pos + i) & (kIb - 1)];
+    const uint32_t d_first = __builtin_amdgcn_readfirstlane(dm);
+    const uint32_t src = dm - s.off;
+    const bool hazard = v && (src + s.ml > d_first || s.ml > kMatchFast);
+    const bool freel = v && !hazard;
+    const uint32_t farlim = o.far_limit();
+    for (uint32_t i = 0; __ballot(freel && i < s.ml); i++) {
+      if (freel && i < s.ml) {
+        const uint32_t qq = src + i;
+        const uint32_t b = qq < farlim ? __builtin_amdgcn_raw_buffer_load_b8(o.rs, qq, 0, 16) : o.ring[qq & (kRing - 1)];
+        o.ring[(dm + i) & (kRing - 1)] = (uint8_t)b;
+      }
+    }
+    for (uint64_t hm = __ballot(hazard); hm; hm &= hm - 1) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(hm);
+      const uint32_t D = __builtin_amdgcn_readlane(dm, l), O = __builtin_amdgcn_readlane(s.off, l),
+                     M = __builtin_amdgcn_readlane(s.ml, l);
+      for (uint32_t c = 0; c < M; c += 64) {
+        if (lane < M - c) {
+          const uint32_t x = D + c;
+          const uint32_t qq = x - O + (O >= 64 ? lane : lane % O);
+          const uint32_t b = qq < farlim ? __builtin_amdgcn_raw_buffer_load_b8(o.rs, qq, 0, 16) : o.ring[qq & (kRing - 1)];
+          o.ring[(x + lane) & (kRing - 1)] = (uint8_t)b;
+        }
+      }
+    }
+    const uint32_t nop = o.op + __builtin_amdgcn_readlane(incl, k - 1);
+    p = k == j ? q : __builtin_amdgcn_readlane(starts, k);
+    if ((nop / kChunk) != (o.op / kChunk)) o.flush(o.op & ~(kChunk - 1), kChunk);
+    o.op = nop;
+  }
+  if (!ended || o.op != olen) return ST_CODEC;
+  o.finish();
+  return ST_OK;
+}
+
+// One wave expands the general-codec stream [src, src + csize) of `olen`
+// bytes into LDS (FULL mode).  Returns a status code.
+__device__ uint32_t expand_to_lds(uint32_t codec, const uint8_t* src, uint32_t csize, lds_u8* out, uint32_t olen) {
+  WaveWin w;
+  w.init(src, csize);
+  WaveOut<false> o;
+  o.ring = out;
+  o.dst = nullptr;
+  o.olen = olen;
+  o.op = 0;
+  const uint32_t p0 = (uint32_t)((uintptr_t)src & 3);
+  if (codec == 1) return lz4_wave<false>(w, p0, p0 + csize, o);
+  if (codec == 3) return snappy_wave<false>(w, p0, p0 + csize, o);
+  return ST_NYI;  // Zstd: host-only for now
 }
 
 // Patas (double/patas.rs:107-132): first value raw, then per value a u16
@@ -826,6 +1243,7 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
   if (tid == 0) {
     uint32_t p = 0;
     sh.has_valid = 0;
+    sh.defer = 0;
     do {
       if (a.nullable && !parse_validity(s, sh, len, n, &p)) break;
       Stream st;
@@ -864,15 +1282,27 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
       sh.defer = 0;
       if (inner.codec == 1 || inner.codec == 2 || inner.codec == 3 || inner.codec == 16) {
         if (MODE == 0) {
-          sh.defer = 1;
-          const uint32_t slot = atomicAdd(a.defer_count + a.parity, 1u);
-          a.defer_list[slot] = page;
+          if (chain == CH_LEAF && (inner.codec == 1 || inner.codec == 3)) {
+            // plain values under LZ4 / Snappy: k_inflate writes them straight
+            // into the column (the decompressed bytes are the values)
+            sh.defer = 2;
+            const uint32_t slot = atomicAdd(a.job_count + a.parity, 1u);
+            a.jobs[slot] = InflateJob{pd.byte_off + inner.body, pd.row_off * W, inner.csize, inner.n * (uint32_t)W,
+                                      inner.codec, page};
+          } else {
+            sh.defer = 1;
+            const uint32_t slot = atomicAdd(a.defer_count + a.parity, 1u);
+            a.defer_list[slot] = page;
+          }
         }
       }
     } while (0);
   }
   __syncthreads();
-  if (sh.err || sh.defer) return;
+  if (sh.err) return;
+  // validity is written by the main pass, deferred pages included
+  if (MODE == 0 && sh.has_valid) write_validity(s, sh.vb_pos, n, pd.row_off, a.out_validity);
+  if (sh.defer) return;
 
   if constexpr (MODE == 1) {
     Stream lf = sh.sub;
@@ -886,8 +1316,8 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
         const lds_u8* in = (const lds_u8*)((const uint8_t*)s.w + s.base + lf.body);
         lds_u8* xo = (lds_u8*)xbuf;
         uint32_t st = ST_OK;
-        if (lf.codec == 1) st = lz4_expand(in, lf.csize, xo, (uint32_t)bytes);
-        else if (lf.codec == 3) st = snappy_expand(in, lf.csize, xo, (uint32_t)bytes);
+        if (lf.codec == 1 || lf.codec == 3)
+          st = expand_to_lds(lf.codec, a.chunk + pd.byte_off + lf.body, lf.csize, xo, (uint32_t)bytes);
         else if (lf.codec == 16) {
           if (!FLT || idx_stream) st = ST_OUT_OF_SPEC;  // Patas only in decompress_double
           else st = patas_expand<W>(in, lf.csize, xo, lf.n);
@@ -900,8 +1330,6 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
       __syncthreads();
     }
   }
-
-  if (sh.has_valid) write_validity(s, sh.vb_pos, n, pd.row_off, a.out_validity);
 
   uint8_t* obase = a.out_values + pd.row_off * W;
   GSink<W> out{obase, ((uintptr_t)obase & (uintptr_t)(W == 8 ? 15 : 4 * W - 1)) == 0};
@@ -1006,13 +1434,16 @@ __global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
   const PageDesc pd = a.pages[page];
   if (threadIdx.x == 0) {
     sh.err = 0;
-    if (blockIdx.x == 0) a.defer_count[a.parity ^ 1] = 0;  // the next decode's work list
+    if (blockIdx.x == 0) {  // the next decode's work lists
+      a.defer_count[a.parity ^ 1] = 0;
+      a.job_count[a.parity ^ 1] = 0;
+    }
   }
   const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
   LdsSrc s{(const uint32_t*)stage, base};
   decode_page<W, FLT, 0>(s, sh, pd, a, page);
   __syncthreads();
-  if (threadIdx.x == 0 && !sh.defer) a.status[page] = sh.err;
+  if (threadIdx.x == 0 && sh.defer != 1) a.status[page] = sh.err;
 }
 
 template <int W, bool FLT>
@@ -1022,11 +1453,14 @@ __global__ __launch_bounds__(NT) void k_decode_global(LaunchArgs a) {
   const PageDesc pd = a.pages[page];
   if (threadIdx.x == 0) sh.err = 0;
   __syncthreads();
-  if (threadIdx.x == 0 && blockIdx.x == 0) a.defer_count[a.parity ^ 1] = 0;
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    a.defer_count[a.parity ^ 1] = 0;
+    a.job_count[a.parity ^ 1] = 0;
+  }
   GlbSrc s{a.chunk + pd.byte_off};
   decode_page<W, FLT, 0>(s, sh, pd, a, page);
   __syncthreads();
-  if (threadIdx.x == 0 && !sh.defer) a.status[page] = sh.err;
+  if (threadIdx.x == 0 && sh.defer != 1) a.status[page] = sh.err;
 }
 
 // Deferred pages (general codecs, Patas): one workgroup per listed page, the
@@ -1079,6 +1513,45 @@ static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// General-codec streams expanded straight into HBM, one wave per stream, each
+// wave with its own kRing-byte LDS history ring: 4 waves x 4 KiB per
+// workgroup, so 8 waves per SIMD can be resident and the serial token streams
+// of many pages overlap.
+__global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) {
+  __shared__ u32x4 rings[kInfWaves][kRing / 16];
+  __shared__ u32x4 ibufs[kInfWaves][kIb / 16];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t n = a.count ? *a.count : a.n_jobs;
+  for (uint32_t j = blockIdx.x * kInfWaves + wv; j < n; j += gridDim.x * kInfWaves) {
+    const InflateJob jb = a.jobs[j];
+    const uint64_t kind = jb.dst >> 62, off = jb.dst & kDstMask;
+    uint8_t* dst = kind == 1 ? a.scratch + off : a.out + (kind == 2 ? a.bases[off] : off);
+    const uint8_t* src = a.chunk + jb.src;
+    WaveOut<true> o;
+    o.ring = (lds_u8*)&rings[wv][0];
+    o.dst = dst;
+    o.rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)jb.usize, 0x00020000);
+    o.olen = jb.usize;
+    o.op = 0;
+    const uint32_t p0 = (uint32_t)((uintptr_t)src & 3);
+    uint32_t st = ST_NYI;
+    if (jb.codec == 1) {
+      InRing in;
+      in.g = (gmem_u32*)((uintptr_t)src & ~(uintptr_t)3);
+      in.nd = (p0 + jb.csize + 3) >> 2;
+      in.ib = (lds_u8*)&ibufs[wv][0];
+      in.seek(p0);
+      st = lz4_inflate(in, p0, p0 + jb.csize, o);
+    } else if (jb.codec == 3) {
+      WaveWin w;
+      w.init(src, jb.csize);
+      st = snappy_wave<true>(w, p0, p0 + jb.csize, o);
+    }
+    if (st && lane == 0) a.status[jb.page] = st;
+  }
+}
+
 // ===========================================================================
 // Binary / Utf8 pages (compression/binary/mod.rs:95-183, dict.rs:95-141,
 // freq.rs:102-145, one_value.rs:71-99), assembled as read_binary does
@@ -1102,6 +1575,9 @@ struct BinArgs {
   uint32_t* out_validity;
   uint32_t* status;
   uint32_t lds_bytes;
+  InflateJob* jobs;
+  uint32_t* job_count;
+  uint8_t* scratch;
 };
 
 enum : uint32_t { BIN_BASIC = 0, BIN_ONE = 12, BIN_DICT = 11, BIN_FREQ = 13 };
@@ -1146,7 +1622,7 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     const uint32_t xb = ((n + 1) * OW + 15) & ~15u;
     bi.yoff = bi.xoff + xb;
     bi.tab = bi.yoff;
-    if (bi.codec != 0 && bi.yoff + bi.S + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
+    if (bi.codec == 2) { set_err(sh, ST_NYI); return false; }  // Zstd: host-only for now
     return true;
   }
   if (bi.codec == BIN_ONE) {
@@ -1251,13 +1727,11 @@ __device__ void copy_lds_to_global(const uint8_t* lds, uint32_t src, uint8_t* ds
 // Materializes a binary Dict's u32 index stream (n values) into LDS xi: leaf
 // codecs via run_leaf, LZ4 / Snappy expanded straight into xi, Freq (top +
 // roaring-placed exceptions of a leaf stream) filled then scattered.
-__device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, uint32_t* xi) {
+__device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, uint32_t* xi, const uint8_t* gpage) {
   const uint32_t tid = threadIdx.x, n = ix.n;
   if (ix.codec == 1 || ix.codec == 3) {
     if (tid < 64) {
-      const lds_u8* in = (const lds_u8*)((const uint8_t*)s.w + s.base + ix.body);
-      const uint32_t st = ix.codec == 1 ? lz4_expand(in, ix.csize, (lds_u8*)xi, 4 * n)
-                                        : snappy_expand(in, ix.csize, (lds_u8*)xi, 4 * n);
+      const uint32_t st = expand_to_lds(ix.codec, gpage + ix.body, ix.csize, (lds_u8*)xi, 4 * n);
       if (st) set_err(sh, st);
     }
     __syncthreads();
@@ -1308,13 +1782,21 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
     }
     const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
     LdsSrc s{(const uint32_t*)stage, base};
-    if (threadIdx.x == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, &idx);
+    if (threadIdx.x == 0 && bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, &idx) &&
+        (bi.codec == 1 || bi.codec == 3)) {
+      // Basic under LZ4 / Snappy: the offsets stream expands into scratch, the
+      // values stream straight into the values buffer at the page's base
+      const uint32_t slot = atomicAdd(a.job_count, 2u);
+      a.jobs[slot] = InflateJob{pd.byte_off + bi.ob, kDstScratch | ((pd.row_off + page) * OW), bi.ocs,
+                                (pd.num_values + 1) * (uint32_t)OW, bi.codec, page};
+      a.jobs[slot + 1] = InflateJob{pd.byte_off + bi.vb, kDstBinBase | page, bi.vcs, (uint32_t)bi.S, bi.codec, page};
+    }
     __syncthreads();
     if (!sh.err && bi.codec == BIN_DICT) {
       const uint2* tab = (const uint2*)(lds + bi.tab);
       const uint32_t k = bi.k;
       uint32_t* xi = (uint32_t*)(lds + bi.xoff);
-      materialize_idx(s, sh, idx, xi);
+      materialize_idx(s, sh, idx, xi, a.chunk + pd.byte_off);
       uint64_t part = 0;
       for (uint32_t i = threadIdx.x; i < pd.num_values; i += NT) {
         if (xi[i] < k) part += tab[xi[i]].y;
@@ -1413,38 +1895,29 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
       if (bi.codec <= 3) {
         // offsets: rows 1..n at V + p[i] (mod.rs:136-144 rebase); p[0] must be
         // 0 and p[n] the values length (the writer rebases, mod.rs:45-55)
-        uint32_t opos = bi.ob;  // stream position of p[0]
         if (bi.codec != 0) {
-          const uint32_t ob = (n + 1) * OW;
-          if (tid < 64) {
-            const lds_u8* in = (const lds_u8*)(lds + base + bi.ob);
-            lds_u8* xo = (lds_u8*)(lds + bi.xoff);
-            uint32_t st = ST_NYI;
-            if (bi.codec == 1) st = lz4_expand(in, bi.ocs, xo, ob);
-            else if (bi.codec == 3) st = snappy_expand(in, bi.ocs, xo, ob);
-            if (st) set_err(sh, st);
-            if (!st) {
-              const lds_u8* vin = (const lds_u8*)(lds + base + bi.vb);
-              lds_u8* yo = (lds_u8*)(lds + bi.yoff);
-              uint32_t st2 = bi.codec == 1 ? lz4_expand(vin, bi.vcs, yo, (uint32_t)bi.S)
-                                            : snappy_expand(vin, bi.vcs, yo, (uint32_t)bi.S);
-              if (st2) set_err(sh, st2);
-            }
-          }
-          opos = bi.xoff - base;
+          // expanded by k_inflate: offsets in scratch, values already at V
+          const uint8_t* xo = a.scratch + (R + page) * OW;
+          auto po = [&](uint32_t i) -> uint64_t {
+            if constexpr (OW == 8) return ((const uint64_t*)xo)[i];
+            else return (uint64_t)(int64_t)((const int32_t*)xo)[i];
+          };
+          if (tid == 0 && (po(0) != 0 || po(n) != bi.S)) set_err(sh, ST_OUT_OF_SPEC);
           __syncthreads();
-        } else if (tid == 0 && (bi.ocs != (n + 1) * OW || bi.vcs != bi.S)) {
-          set_err(sh, ST_OUT_OF_SPEC);  // copy_from_slice length mismatch
-        }
-        __syncthreads();
-        if (!sh.err && tid == 0) {
-          if (ldo<OW>(s, opos) != 0 || ldo<OW>(s, opos + n * OW) != bi.S) set_err(sh, ST_OUT_OF_SPEC);
-        }
-        __syncthreads();
-        if (!sh.err) {
-          for (uint32_t i = tid + 1; i <= n; i += NT) bin_put_off(a.out_offsets, R + i, V + ldo<OW>(s, opos + i * OW), OW);
-          const uint32_t vsrc = bi.codec != 0 ? bi.yoff : base + bi.vb;
-          copy_lds_to_global(lds, vsrc, a.out_values + V, bi.S);
+          if (!sh.err)
+            for (uint32_t i = tid + 1; i <= n; i += NT) bin_put_off(a.out_offsets, R + i, V + po(i), OW);
+        } else {
+          const uint32_t opos = bi.ob;  // stream position of p[0]
+          if (tid == 0 && (bi.ocs != (n + 1) * OW || bi.vcs != bi.S)) set_err(sh, ST_OUT_OF_SPEC);  // copy_from_slice
+          __syncthreads();
+          if (!sh.err && tid == 0) {
+            if (ldo<OW>(s, opos) != 0 || ldo<OW>(s, opos + n * OW) != bi.S) set_err(sh, ST_OUT_OF_SPEC);
+          }
+          __syncthreads();
+          if (!sh.err) {
+            for (uint32_t i = tid + 1; i <= n; i += NT) bin_put_off(a.out_offsets, R + i, V + ldo<OW>(s, opos + i * OW), OW);
+            copy_lds_to_global(lds, base + bi.vb, a.out_values + V, bi.S);
+          }
         }
       } else if (bi.codec == BIN_ONE) {
         const uint32_t L = bi.L, top = base + bi.top;
@@ -1452,7 +1925,7 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
         for (uint64_t j = tid; j < (uint64_t)n * L; j += NT) a.out_values[V + j] = lds[top + (uint32_t)(j % L)];
       } else if (bi.codec == BIN_DICT) {
         uint32_t* xi = (uint32_t*)(lds + bi.xoff);
-        materialize_idx(s, sh, idx, xi);
+        materialize_idx(s, sh, idx, xi, a.chunk + pd.byte_off);
         const uint2* tab = (const uint2*)(lds + bi.tab);
         const uint32_t k = bi.k;
         if (!sh.err)
@@ -1519,7 +1992,7 @@ int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a,
 namespace sb {
 int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream) {
   sbk::BinArgs a{L.chunk, L.pages, L.n_pages, L.nullable, L.sizes, L.bases, L.total, L.out_offsets, L.out_values,
-                 L.values_cap, L.out_validity, L.status, kDeferredLds};
+                 L.values_cap, L.out_validity, L.status, kDeferredLds, L.jobs, L.job_count, L.scratch};
   hipStream_t st = (hipStream_t)stream;
   const dim3 block(sbk::NT);
   const dim3 grid(std::min<uint32_t>(L.n_pages ? L.n_pages : 1, kDeferredGrid));
@@ -1539,6 +2012,15 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
     if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, kDeferredLds, st, a);
     else hipLaunchKernelGGL(sbk::k_bin_decode<4>, grid, block, kDeferredLds, st, a);
   }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}  // namespace sb
+
+namespace sb {
+int launch_inflate(const InflateLaunch& a, void* stream) {
+  if (a.n_jobs == 0) return 0;
+  const uint32_t grid = std::min<uint32_t>((a.n_jobs + sbk::kInfWaves - 1) / sbk::kInfWaves, kInflateGrid);
+  hipLaunchKernelGGL(sbk::k_inflate, dim3(grid), dim3(64 * sbk::kInfWaves), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb

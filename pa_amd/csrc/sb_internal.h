@@ -32,6 +32,31 @@ enum : uint32_t {
 constexpr uint32_t kStageMaxBytes = 48 * 1024;
 constexpr uint32_t kStagePad = 64;  // LDS slack for unaligned over-reads
 
+// A general-codec (LZ4 / Snappy) stream expanded by k_inflate, one wave per
+// job.  dst: kind in bits 62-63 -- 0 = out + off, 1 = scratch + off,
+// 2 = out + bases[off] (a binary page's values base).
+struct InflateJob {
+  uint64_t src;  // byte offset of the compressed body in the column chunk
+  uint64_t dst;
+  uint32_t csize, usize;
+  uint32_t codec, page;
+};
+static_assert(sizeof(InflateJob) == 32, "inflate job is 32 bytes");
+constexpr uint64_t kDstScratch = 1ull << 62, kDstBinBase = 2ull << 62, kDstMask = (1ull << 62) - 1;
+
+struct InflateLaunch {
+  const uint8_t* chunk;
+  const InflateJob* jobs;
+  const uint32_t* count;  // device job count, or nullptr = n_jobs
+  uint32_t n_jobs;        // upper bound of the count (sizes the grid)
+  uint8_t* out;
+  uint8_t* scratch;
+  const uint64_t* bases;
+  uint32_t* status;
+};
+int launch_inflate(const InflateLaunch& a, void* stream);
+constexpr uint32_t kInflateGrid = 2048;  // 4-wave workgroups: 8 waves per SIMD on 256 CUs
+
 // Launch entry points (sb_decode.hip).
 struct LaunchArgs {
   const uint8_t* chunk;
@@ -46,6 +71,8 @@ struct LaunchArgs {
   uint32_t* defer_count;  // [2]: work-list lengths, double-buffered by decode parity
   uint32_t* defer_list;   // page indices deferred to k_decode_deferred
   uint32_t parity;
+  uint32_t* job_count;    // [2]: inflate job counts, double-buffered like defer_count
+  InflateJob* jobs;       // CH_LEAF LZ4 / Snappy pages, expanded by k_inflate
 };
 
 // kind: 0 = LDS-staged pages, 1 = pages read from HBM, 2 = deferred work list
@@ -69,6 +96,9 @@ struct BinLaunch {
   uint64_t values_cap;
   uint32_t* out_validity;
   uint32_t* status;
+  InflateJob* jobs;       // sizing pass out: Basic LZ4 / Snappy streams (2 per page)
+  uint32_t* job_count;
+  uint8_t* scratch;       // expanded offsets streams, (row_off + page) * offset width
 };
 int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
 
