@@ -68,6 +68,7 @@ typedef enum {
   SB_T_LARGE_BINARY = 12, /* i64 offsets */
   SB_T_UTF8 = 13,         /* i32 offsets (bytes; UTF-8 validation is the caller's) */
   SB_T_LARGE_UTF8 = 14,   /* i64 offsets */
+  SB_T_BOOLEAN = 15,      /* values are an LSB-first bitmap (read_boolean, read/array/boolean.rs:191-219) */
 } sb_physical_type;
 
 /* PageMeta (src/lib.rs:75-80): compressed page length and num_values. */
@@ -85,7 +86,8 @@ typedef struct {
 } sb_column_desc;
 
 /* Output buffers of a primitive column (caller-allocated, device):
- * values: sum(num_values) * sizeof(T) bytes;
+ * values: sum(num_values) * sizeof(T) bytes (Boolean: a bitmap laid out like
+ * the validity below);
  * validity: 4*ceil(sum(num_values)/32) bytes (LSB-first Arrow bitmap, written
  * as 32-bit words; bits past the last row are zero) or NULL when the column is
  * not nullable.  Both 16-byte aligned for vector stores. */
@@ -201,7 +203,9 @@ sb_status sb_encode_page(int32_t physical_type, const void* h_values, const uint
                          uint64_t* out_len);
 /* NativeWriter::encode_chunk (write/common.rs:49-119) for one flat leaf:
  * pages of max_page_rows rows (0 = one page), encoded on n_threads host
- * threads (0 = all).  Page p samples with sb_page_seed(opts->seed, p). */
+ * threads (0 = all).  Page p samples with sb_page_seed(opts->seed, p).
+ * Boolean: h_values is the column's LSB-first values bitmap and page p is
+ * its slice (compress_boolean, compression/boolean/mod.rs:22-61). */
 sb_status sb_encode_column(int32_t physical_type, const void* h_values, const uint8_t* h_validity,
                            uint64_t n_rows, int32_t nullable, const sb_write_options* opts,
                            uint64_t max_page_rows, int32_t n_threads, uint8_t** h_out, uint64_t* out_len,

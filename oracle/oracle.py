@@ -93,6 +93,11 @@ def lib():
         L.orc_hybrid_decode.argtypes = [P, S, ctypes.c_uint32, S, P]
         L.orc_common_decompress.argtypes = [I, P, S, P, S]
         L.orc_common_compress.argtypes = [I, P, S, ctypes.POINTER(_Buf)]
+        L.orc_compress_boolean.argtypes = [P, S, P, S, ctypes.POINTER(WriteOptions), ctypes.POINTER(_Buf)]
+        L.orc_decompress_boolean.argtypes = [P, S, PS, S, P]
+        L.orc_write_bool_page.argtypes = [P, S, P, S, I, ctypes.POINTER(WriteOptions), ctypes.POINTER(_Buf)]
+        L.orc_read_bool_page.argtypes = [P, S, S, I, P, P]
+        L.orc_read_bool_column.argtypes = [P, S, P, S, I, P, P]
         _lib = L
     return _lib
 
@@ -431,3 +436,50 @@ def read_list_column(chunk, metas, dtype, list_nullable, item_nullable):
     offsets = np.concatenate(offs_all)
     return (offsets, np.concatenate(lv_all) if list_nullable else None, np.concatenate(vals_all),
             np.concatenate(leafv_all) if item_nullable else None)
+
+
+# ---- boolean pages (compression/boolean/*.rs, read/array/boolean.rs) ---------
+def _pack(b) -> np.ndarray:
+    return np.packbits(np.asarray(b, bool), bitorder="little")
+
+
+def write_bool_page(values, validity=None, nullable=False, opts: WriteOptions | None = None, offset: int = 0,
+                    n: int | None = None) -> bytes:
+    """One flat boolean page.  values = the whole column's bools; the page is
+    rows [offset, offset + n) (array.slice), so the Basic codec sees the
+    parent bitmap's bytes when offset % 8 == 0 (boolean/mod.rs:35-46).
+    validity (page-relative) has n entries."""
+    vals = np.asarray(values, bool)
+    n = len(vals) - offset if n is None else n
+    bits = _pack(vals)
+    if len(bits) == 0:
+        bits = np.zeros(1, np.uint8)
+    vb = None if validity is None else _pack(validity)
+    buf = _Buf()
+    rc = lib().orc_write_bool_page(_ptr(bits), offset, _ptr(vb), n, int(nullable), ctypes.byref(opts or WriteOptions.make()),
+                                   ctypes.byref(buf))
+    data = _take(buf)
+    _check(rc, "write_bool_page")
+    return data
+
+
+def read_bool_page(page: bytes, n: int, nullable=False):
+    src = _bytes_arr(page)
+    vb = np.zeros((n + 7) // 8 + 1, np.uint8)
+    mb = np.zeros((n + 7) // 8 + 1, np.uint8)
+    _check(lib().orc_read_bool_page(_ptr(src), len(page), n, int(nullable), _ptr(vb), _ptr(mb)), "read_bool_page")
+    vals = np.unpackbits(vb, bitorder="little")[:n].astype(bool)
+    return vals, (np.unpackbits(mb, bitorder="little")[:n].astype(bool) if nullable else None)
+
+
+def read_bool_column(chunk: bytes, metas, nullable=False):
+    """read_boolean (read/array/boolean.rs:191-219) -> (values bits, validity bits|None) as bool arrays."""
+    n = sum(int(m[1]) for m in metas)
+    flat = np.asarray([int(x) for m in metas for x in m], np.uint64)
+    src = _bytes_arr(chunk)
+    vb = np.zeros((n + 7) // 8 + 1, np.uint8)
+    mb = np.zeros((n + 7) // 8 + 1, np.uint8)
+    _check(lib().orc_read_bool_column(_ptr(src), len(chunk), _ptr(flat), len(metas), int(nullable), _ptr(vb), _ptr(mb)),
+           "read_bool_column")
+    vals = np.unpackbits(vb, bitorder="little")[:n].astype(bool)
+    return vals, (np.unpackbits(mb, bitorder="little")[:n].astype(bool) if nullable else None)

@@ -1816,3 +1816,246 @@ int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int l
   *out_leaves = leaves;
   return rc;
 }
+
+/* ======================================================================= */
+/* boolean pages (compression/boolean/{mod,rle,one_value}.rs,               */
+/* read/array/boolean.rs:59-79, 191-219, write/boolean.rs:24-33)            */
+/* ======================================================================= */
+typedef struct {
+  size_t rows, null_count, false_count, true_count, total_bytes;
+} bstats_t;
+
+/* gen_stats (boolean/mod.rs:178-220); total_bytes = values().len() / 8 */
+static void bool_stats(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n, bstats_t* s) {
+  memset(s, 0, sizeof *s);
+  s->rows = n;
+  s->total_bytes = n / 8;
+  for (size_t i = 0; i < n; i++) {
+    if (!is_valid(validity, i)) { s->null_count++; continue; }
+    if (get_bit(bits, off + i)) s->true_count++; else s->false_count++;
+  }
+}
+
+/* RLE::compress_integer over the bits as u8 (boolean/rle.rs:31-39 ->
+ * integer/rle.rs:64-104): nulls extend the current run. */
+static void bool_rle_encode(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n, orc_buf* out) {
+  uint32_t seen = 0;
+  uint8_t last = 0;
+  int all_null = 1;
+  for (size_t i = 0; i < n; i++) {
+    uint8_t v = (uint8_t)get_bit(bits, off + i);
+    if (is_valid(validity, i)) {
+      if (all_null) { all_null = 0; last = v; seen++; }
+      else if (last != v) { buf_u32(out, seen); buf_u8(out, last); last = v; seen = 1; }
+      else seen++;
+    } else {
+      seen++;
+    }
+  }
+  if (seen) { buf_u32(out, seen); buf_u8(out, last); }
+}
+
+/* compress_sample_ratio (boolean/mod.rs:282-321) for RLE: 10 windows of 64
+ * rows at seeded offsets when n / 10 > 64.  The sample is rebuilt from
+ * Option<bool> (MutableBooleanArray), so null slots read false. */
+static double bool_rle_ratio(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n, orc_rng* rng) {
+  const size_t SC = 10, SS = 64;
+  orc_buf tmp = {0};
+  size_t total_bytes;
+  if (n / SC <= SS) {
+    total_bytes = n / 8;
+    bool_rle_encode(bits, off, validity, n, &tmp);
+  } else {
+    uint8_t sb[(10 * 64) / 8], sv[(10 * 64) / 8];
+    memset(sb, 0, sizeof sb);
+    memset(sv, 0, sizeof sv);
+    size_t sep = n / SC, rem = n % SC;
+    for (size_t k = 0; k < SC; k++) {
+      size_t range_end = (k == SC - 1 ? sep + rem : sep) - SS;
+      size_t begin = k * sep + (size_t)(rng_next(rng) % range_end);
+      for (size_t j = 0; j < SS; j++) {
+        size_t q = k * SS + j;
+        int valid = is_valid(validity, begin + j);
+        if (valid) sv[q >> 3] |= (uint8_t)(1u << (q & 7));
+        if (valid && get_bit(bits, off + begin + j)) sb[q >> 3] |= (uint8_t)(1u << (q & 7));
+      }
+    }
+    total_bytes = SC * SS / 8;
+    bool_rle_encode(sb, 0, validity ? sv : NULL, SC * SS, &tmp);
+  }
+  double r = (double)total_bytes / (double)tmp.len;
+  orc_buf_free(&tmp);
+  return r;
+}
+
+/* choose_compressor (boolean/mod.rs:222-280) */
+static int bool_choose(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n, const bstats_t* s,
+                       const orc_write_options* opt, orc_rng* rng) {
+  uint32_t fm = opt->forbidden_mask;
+  if (opt->forced_codec == ORC_RLE && !(fm & (1u << ORC_RLE))) return ORC_RLE; /* check_rle_env */
+  int result = opt->default_codec;
+  if (!opt->has_ratio) return result;
+  double maxr = opt->ratio;
+  static const int cands[] = {ORC_ONE_VALUE, ORC_RLE};
+  for (int k = 0; k < 2; k++) {
+    if (fm & (1u << cands[k])) continue;
+    double r = cands[k] == ORC_ONE_VALUE ? ((s->true_count == 0 || s->false_count == 0) ? (double)s->rows : 0.0)
+                                         : bool_rle_ratio(bits, off, validity, n, rng);
+    if (r > maxr) {
+      maxr = r;
+      result = cands[k];
+      if (r == (double)s->rows) break;
+    }
+  }
+  return result;
+}
+
+/* compress_boolean (boolean/mod.rs:22-61).  bits = the column's values
+ * bitmap, off = the page's first row (the page is array.slice(off, n)):
+ * Basic compresses bitmap.as_slice() -- the parent's bytes verbatim when
+ * off % 8 == 0 (trailing bits of the last byte belong to the next rows),
+ * else a rebuilt, zero-padded bitmap.  validity is page-relative. */
+int orc_compress_boolean(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n,
+                         const orc_write_options* opt, orc_buf* out) {
+  bstats_t s;
+  orc_rng rng = {opt->seed};
+  bool_stats(bits, off, validity, n, &s);
+  int codec = bool_choose(bits, off, validity, n, &s, opt, &rng);
+  buf_u8(out, (uint8_t)codec);
+  size_t hpos = out->len;
+  buf_u64(out, 0);
+  size_t before = out->len;
+  int rc = ORC_OK;
+  if (codec <= ORC_SNAPPY) {
+    size_t nb = (n + 7) / 8;
+    if (off % 8 == 0) {
+      rc = orc_common_compress(codec, bits + off / 8, nb, out);
+    } else {
+      uint8_t* tmp = (uint8_t*)calloc(nb ? nb : 1, 1);
+      for (size_t i = 0; i < n; i++)
+        if (get_bit(bits, off + i)) tmp[i >> 3] |= (uint8_t)(1u << (i & 7));
+      rc = orc_common_compress(codec, tmp, nb, out);
+      free(tmp);
+    }
+  } else if (codec == ORC_RLE) {
+    bool_rle_encode(bits, off, validity, n, out);
+  } else if (codec == ORC_ONE_VALUE) { /* boolean/one_value.rs:44-52: first valid value, else false */
+    uint8_t v = 0;
+    for (size_t i = 0; i < n; i++)
+      if (is_valid(validity, i)) { v = (uint8_t)get_bit(bits, off + i); break; }
+    buf_u8(out, v);
+  } else {
+    rc = ORC_E_ARG;
+  }
+  if (rc) return rc;
+  uint32_t csize = (uint32_t)(out->len - before), usize = (uint32_t)n;
+  memcpy(out->data + hpos, &csize, 4);
+  memcpy(out->data + hpos + 4, &usize, 4);
+  return ORC_OK;
+}
+
+/* decompress_boolean (boolean/mod.rs:63-102) of `length` bits into out_bits
+ * (page-relative, LSB first).  Basic: (length+7)/8 bytes through the common
+ * codec.  RLE (boolean/rle.rs:41-55) and OneValue (one_value.rs:54-61) are
+ * handed the rest of the buffer, not csize bytes.  A run total that passes
+ * `length` would push extra bits into the next rows (BooleanArray::try_new
+ * then fails): OutOfSpec; input ending before `length` bits: Io. */
+int orc_decompress_boolean(const uint8_t* buf, size_t len, size_t* pos, size_t length, uint8_t* out_bits) {
+  int codec;
+  size_t csize, usize;
+  int rc = read_header(buf, len, pos, &codec, &csize, &usize);
+  if (rc) return rc;
+  const uint8_t* body = buf + *pos;
+  const size_t rest = len - *pos;
+  (void)usize;
+  size_t nb = (length + 7) / 8;
+  switch (codec) {
+    case ORC_NONE: case ORC_LZ4: case ORC_ZSTD: case ORC_SNAPPY: {
+      uint8_t* tmp = (uint8_t*)malloc(nb ? nb : 1);
+      rc = orc_common_decompress(codec, body, csize, tmp, nb);
+      if (!rc)
+        for (size_t i = 0; i < length; i++) {
+          if (get_bit(tmp, i)) out_bits[i >> 3] |= (uint8_t)(1u << (i & 7));
+          else out_bits[i >> 3] &= (uint8_t)~(1u << (i & 7));
+        }
+      free(tmp);
+      break;
+    }
+    case ORC_RLE: {
+      size_t p = 0, produced = 0;
+      while (produced < length) {
+        if (p + 5 > rest) { rc = ORC_E_IO; break; }
+        uint32_t cnt = rd_u32(body + p);
+        int v = body[p + 4] != 0;
+        p += 5;
+        if (produced + cnt > length) { rc = ORC_E_OUT_OF_SPEC; break; }
+        for (uint32_t i = 0; i < cnt; i++) {
+          size_t q = produced + i;
+          if (v) out_bits[q >> 3] |= (uint8_t)(1u << (q & 7));
+          else out_bits[q >> 3] &= (uint8_t)~(1u << (q & 7));
+        }
+        produced += cnt;
+      }
+      break;
+    }
+    case ORC_ONE_VALUE: {
+      if (rest < 1) { rc = ORC_E_IO; break; }
+      int v = body[0] > 0;
+      for (size_t i = 0; i < length; i++) {
+        if (v) out_bits[i >> 3] |= (uint8_t)(1u << (i & 7));
+        else out_bits[i >> 3] &= (uint8_t)~(1u << (i & 7));
+      }
+      break;
+    }
+    default: rc = ORC_E_OUT_OF_SPEC; break;
+  }
+  if (rc) return rc;
+  *pos += csize;
+  return ORC_OK;
+}
+
+/* one flat boolean page: [validity?][boolean stream] (BooleanIter::deserialize) */
+int orc_write_bool_page(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n, int nullable,
+                        const orc_write_options* opt, orc_buf* out) {
+  if (nullable) orc_write_validity(validity, n, out);
+  return orc_compress_boolean(bits, off, validity, n, opt, out);
+}
+
+int orc_read_bool_page(const uint8_t* page, size_t page_len, size_t n, int nullable, uint8_t* out_bits,
+                       uint8_t* out_valid) {
+  size_t pos = 0;
+  int rc;
+  if (nullable) {
+    rc = orc_read_validity(page, page_len, &pos, n, out_valid);
+    if (rc) return rc;
+  }
+  return orc_decompress_boolean(page, page_len, &pos, n, out_bits);
+}
+
+/* read_boolean (read/array/boolean.rs:191-219): pages appended bitwise. */
+int orc_read_bool_column(const uint8_t* chunk, size_t len, const uint64_t* metas, size_t n_pages, int nullable,
+                         uint8_t* out_bits, uint8_t* out_valid) {
+  size_t pos = 0, row = 0;
+  int rc = ORC_OK;
+  for (size_t p = 0; p < n_pages && !rc; p++) {
+    size_t plen = (size_t)metas[2 * p], nv = (size_t)metas[2 * p + 1];
+    if (pos + plen > len) return ORC_E_IO;
+    uint8_t* vb = (uint8_t*)calloc((nv + 7) / 8 + 1, 1);
+    uint8_t* mb = (uint8_t*)calloc((nv + 7) / 8 + 1, 1);
+    rc = orc_read_bool_page(chunk + pos, plen, nv, nullable, vb, mb);
+    for (size_t i = 0; !rc && i < nv; i++) {
+      size_t r = row + i;
+      if (get_bit(vb, i)) out_bits[r >> 3] |= (uint8_t)(1u << (r & 7));
+      else out_bits[r >> 3] &= (uint8_t)~(1u << (r & 7));
+      if (nullable) {
+        if (get_bit(mb, i)) out_valid[r >> 3] |= (uint8_t)(1u << (r & 7));
+        else out_valid[r >> 3] &= (uint8_t)~(1u << (r & 7));
+      }
+    }
+    free(vb);
+    free(mb);
+    pos += plen;
+    row += nv;
+  }
+  return rc;
+}

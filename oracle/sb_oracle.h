@@ -135,6 +135,19 @@ int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int l
                        int kind, int width, int64_t* out_offsets, uint8_t* out_list_bits, uint8_t* out_values,
                        uint8_t* out_leaf_bits, size_t* out_rows, size_t* out_leaves);
 
+/* ---- boolean pages (compression/boolean/{mod,rle,one_value}.rs) ---- */
+/* bits = the column's values bitmap, off = the page's first row; validity is
+ * page-relative.  Bit buffers are LSB-first. */
+int orc_compress_boolean(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n,
+                         const orc_write_options* opt, orc_buf* out);
+int orc_decompress_boolean(const uint8_t* buf, size_t len, size_t* pos, size_t length, uint8_t* out_bits);
+int orc_write_bool_page(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n, int nullable,
+                        const orc_write_options* opt, orc_buf* out);
+int orc_read_bool_page(const uint8_t* page, size_t page_len, size_t n, int nullable, uint8_t* out_bits,
+                       uint8_t* out_valid);
+int orc_read_bool_column(const uint8_t* chunk, size_t len, const uint64_t* metas, size_t n_pages, int nullable,
+                         uint8_t* out_bits, uint8_t* out_valid);
+
 /* ---- roaring portable format (roaring 0.10.1) ---- */
 /* Deserializes into ascending positions.  *count set; positions may be NULL to
  * size.  cap = capacity of positions. */

@@ -18,6 +18,7 @@ OK, E_OUT_OF_SPEC, E_NYI, E_IO, E_CODEC, E_DEVICE, E_ARG = 0, 1, 2, 3, 4, 5, 6
 
 # sb_physical_type
 INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = range(1, 11)
+BOOLEAN = 15
 
 EXPORTED = [
     "sb_ctx_create", "sb_ctx_destroy", "sb_ctx_set_stream", "sb_ctx_stream", "sb_sync", "sb_last_error",

@@ -41,6 +41,7 @@ struct sb_plan {
   int deferred_state = -1;  // -1 unknown, 0 no deferred pages, 1 some
   int inflate_state = -1;   // same, for k_inflate jobs
   bool binary = false;
+  bool boolean = false;  // SB_T_BOOLEAN: values are a bitmap (k_bool_decode)
   int offset_width = 0;
   uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1]
   uint64_t values_bytes = 0;
@@ -163,14 +164,15 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   const int ptype = desc->physical_type;
   const int owidth = (ptype == SB_T_BINARY || ptype == SB_T_UTF8) ? 4
                      : (ptype == SB_T_LARGE_BINARY || ptype == SB_T_LARGE_UTF8) ? 8 : 0;
-  if (!width && !owidth) return fail(ctx, SB_E_NYI, "physical type %d not supported", desc->physical_type);
+  const bool is_bool = ptype == SB_T_BOOLEAN;
+  if (!width && !owidth && !is_bool) return fail(ctx, SB_E_NYI, "physical type %d not supported", desc->physical_type);
   if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
 
   std::vector<sb::PageDesc> pages(n_pages);
   std::vector<uint32_t> staged, global;
   uint64_t off = 0, rows = 0;
-  uint32_t max_stage = 0;
+  uint32_t max_stage = 0, max_bool = 0;
   bool needs_zero = false;
   for (uint64_t i = 0; i < n_pages; i++) {
     const sb_page_meta& m = h_metas[i];
@@ -181,6 +183,11 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     pages[i] = sb::PageDesc{off, rows, (uint32_t)m.length, (uint32_t)m.num_values, 0};
     // a 32-bit validity word shared by two pages is merged with atomics
     if ((rows & 31) || (m.num_values & 31)) needs_zero = true;
+    if (is_bool) {  // page + its expanded bitmap, as k_bool_decode lays them out in LDS
+      const uint64_t need = ((m.length + 15 + sb::kStagePad + 15) & ~15ull) + (((m.num_values + 7) / 8 + 15) & ~15ull) +
+                            sb::kStagePad;
+      max_bool = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(max_bool, need), sb::kDeferredLds);
+    }
     if (m.length + 16 <= sb::kStageMaxBytes) {
       staged.push_back((uint32_t)i);
       max_stage = std::max<uint32_t>(max_stage, (uint32_t)m.length);
@@ -205,6 +212,8 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   p->stage_bytes = ((max_stage + 16 + 15) & ~15u) + sb::kStagePad;
   p->validity_needs_zero = needs_zero;
   p->binary = owidth != 0;
+  p->boolean = is_bool;
+  if (is_bool) p->stage_bytes = std::max<uint32_t>(max_bool, 64);
   p->offset_width = owidth;
   size_t np = n_pages ? n_pages : 1;
   hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
@@ -299,6 +308,8 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   if (p->desc.nullable && p->validity_needs_zero)
     HIP_TRY(ctx, hipMemsetAsync(out->d_validity, 0, (p->n_rows + 31) / 32 * 4, ctx->stream));
+  if (p->boolean && p->validity_needs_zero)  // the values bitmap shares words across pages too
+    HIP_TRY(ctx, hipMemsetAsync(out->d_values, 0, (p->n_rows + 31) / 32 * 4, ctx->stream));
   if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
   sb::LaunchArgs a{};
   a.chunk = p->d_chunk;
@@ -314,6 +325,17 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   a.jobs = p->d_jobs;
   a.parity = (uint32_t)(p->decodes & 1);
   p->decodes++;
+  if (p->boolean) {
+    a.list = nullptr;
+    a.n_list = (uint32_t)p->n_pages;
+    if (sb::launch_bool(a, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "boolean decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (p->timing) {
+      HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
+      p->timed = true;
+    }
+    return SB_OK;
+  }
   a.list = p->staged_identity ? nullptr : p->d_lists;
   a.n_list = p->n_staged;
   if (sb::launch_decode_fixed(p->width, p->is_float, 0, a, ctx->stream))
@@ -352,7 +374,7 @@ sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
   if (!p->n_pages) return SB_OK;
   std::vector<uint32_t> st(p->n_pages);
   HIP_TRY(ctx, hipMemcpy(st.data(), p->d_status, p->n_pages * 4, hipMemcpyDeviceToHost));
-  if (!p->binary && p->decodes && (p->deferred_state == -1 || p->inflate_state == -1)) {
+  if (!p->binary && !p->boolean && p->decodes && (p->deferred_state == -1 || p->inflate_state == -1)) {
     // the plan's pages are fixed: learn once which passes they need
     uint32_t cnt[4] = {0, 0, 0, 0};
     HIP_TRY(ctx, hipMemcpy(cnt, p->d_defer, sizeof cnt, hipMemcpyDeviceToHost));

@@ -1969,6 +1969,107 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
   }
 }
 
+// ===========================================================================
+// Boolean pages (BooleanIter::deserialize / read_boolean,
+// read/array/boolean.rs:59-79, 191-219; decompress_boolean,
+// compression/boolean/mod.rs:63-102).  One workgroup per page: the page is
+// staged in LDS, the values bitmap is produced page-relative (None: the
+// staged bytes themselves; RLE / LZ4 / Snappy: expanded into an LDS bitmap)
+// and funnel-shifted to the page's first row like the validity.
+// ===========================================================================
+__device__ void fill_bits(uint32_t n, uint64_t row_off, bool v, uint32_t* out) {
+  if (n == 0) return;
+  const uint64_t fw = row_off >> 5, lw = (row_off + n - 1) >> 5;
+  for (uint64_t w = fw + threadIdx.x; w <= lw; w += NT) {
+    const int64_t pb = (int64_t)(w * 32) - (int64_t)row_off;
+    const uint32_t lo = pb < 0 ? (uint32_t)(-pb) : 0u;
+    const int64_t hi_ex = (int64_t)n - pb;
+    const uint32_t hi = hi_ex >= 32 ? 32u : (uint32_t)hi_ex;
+    const uint32_t m = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1)) & (0xFFFFFFFFu << lo);
+    if (m == 0xFFFFFFFFu) out[w] = v ? m : 0u;
+    else if (v) atomicOr(&out[w], m);
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
+  extern __shared__ u32x4 stage[];
+  __shared__ Shared sh;
+  __shared__ Stream bs;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = blockIdx.x; i < a.n_list; i += gridDim.x) {
+    const uint32_t page = a.list ? a.list[i] : i;
+    const PageDesc pd = a.pages[page];
+    const uint32_t n = pd.num_values, len = pd.byte_len;
+    const uint32_t need = (len + 15 + kStagePad + 15) & ~15u;
+    const uint32_t xb = ((n + 7) / 8 + 15) & ~15u;
+    if (tid == 0) sh.err = 0;
+    if (need + xb + kStagePad > a.stage_bytes) {  // page + bitmap larger than the LDS budget
+      __syncthreads();
+      if (tid == 0) a.status[page] = ST_NYI;
+      continue;
+    }
+    const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, len);
+    LdsSrc s{(const uint32_t*)stage, base};
+    if (tid == 0) {
+      uint32_t p = 0;
+      sh.has_valid = 0;
+      do {
+        if (a.nullable && !parse_validity(s, sh, len, n, &p)) break;
+        if (!parse_stream(s, p, len, n, &bs)) { set_err(sh, ST_IO); break; }
+      } while (0);
+    }
+    __syncthreads();
+    if (!sh.err) {
+      if (sh.has_valid) write_validity(s, sh.vb_pos, n, pd.row_off, a.out_validity);
+      const Stream st = bs;
+      uint32_t* xbits = (uint32_t*)((uint8_t*)stage + need);
+      const LdsSrc xs{(const uint32_t*)stage, need};
+      switch (st.codec) {
+        case 0:  // the page's bitmap bytes (basic.rs:68-71: exactly (n + 7) / 8 of them)
+          if (st.csize != (n + 7) / 8) { if (tid == 0) set_err(sh, ST_OUT_OF_SPEC); break; }
+          write_validity(s, st.body, n, pd.row_off, (uint32_t*)a.out_values);
+          break;
+        case 12:  // OneValue (boolean/one_value.rs:54-61): the rest of the page, not csize
+          if (st.body >= len) { if (tid == 0) set_err(sh, ST_IO); break; }
+          fill_bits(n, pd.row_off, s.u8(st.body) != 0, (uint32_t*)a.out_values);
+          break;
+        case 10: {  // RLE (boolean/rle.rs:41-55): (u32 count, u8 value) runs over the rest of the page
+          for (uint32_t w = tid; w < xb / 4; w += NT) xbits[w] = 0;
+          __syncthreads();
+          const Stream rs{10u, st.body, len - st.body, n};
+          run_leaf<1>(s, sh, rs, [&](uint32_t row, const uint32_t* v, uint32_t nv) {
+            uint32_t nib = 0;
+            for (uint32_t l = 0; l < nv; l++) nib |= (v[l] != 0 ? 1u : 0u) << l;
+            if (nib) atomicOr(&xbits[row >> 5], nib << (row & 31));
+          });
+          __syncthreads();
+          if (!sh.err) write_validity(xs, 0, n, pd.row_off, (uint32_t*)a.out_values);
+          break;
+        }
+        case 1:
+        case 3: {  // LZ4 / Snappy over the bitmap bytes, expanded into LDS by wave 0
+          if (tid < 64) {
+            const uint32_t r = expand_to_lds(st.codec, a.chunk + pd.byte_off + st.body, st.csize, (lds_u8*)xbits,
+                                             (n + 7) / 8);
+            if (r) set_err(sh, r);
+          }
+          __syncthreads();
+          if (!sh.err) write_validity(xs, 0, n, pd.row_off, (uint32_t*)a.out_values);
+          break;
+        }
+        case 2:
+          if (tid == 0) set_err(sh, ST_NYI);  // Zstd: not on device yet
+          break;
+        default:
+          if (tid == 0) set_err(sh, ST_OUT_OF_SPEC);  // Compression::from_codec / from_compression
+      }
+    }
+    __syncthreads();
+    if (tid == 0) a.status[page] = sh.err;
+    __syncthreads();
+  }
+}
+
 }  // namespace sbk
 
 namespace sb {
@@ -2021,6 +2122,20 @@ int launch_inflate(const InflateLaunch& a, void* stream) {
   if (a.n_jobs == 0) return 0;
   const uint32_t grid = std::min<uint32_t>((a.n_jobs + sbk::kInfWaves - 1) / sbk::kInfWaves, kInflateGrid);
   hipLaunchKernelGGL(sbk::k_inflate, dim3(grid), dim3(64 * sbk::kInfWaves), 0, (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}  // namespace sb
+
+namespace sb {
+int launch_bool(const LaunchArgs& a, void* stream) {
+  if (a.n_list == 0) return 0;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)sbk::k_bool_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
+    attr = true;
+  }
+  const uint32_t grid = std::min<uint32_t>(a.n_list, 65535u);
+  hipLaunchKernelGGL(sbk::k_bool_decode, dim3(grid), dim3(sbk::NT), a.stage_bytes, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb

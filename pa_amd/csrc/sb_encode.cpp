@@ -616,6 +616,113 @@ int encode_page(int phys, const void* values, const uint8_t* valid, size_t n, bo
   return SB_E_NYI;
 }
 
+// ---- boolean pages: compress_boolean (compression/boolean/mod.rs:22-61),
+// gen_stats (:178-220), choose_compressor (:222-280), RLE over the bits as u8
+// (boolean/rle.rs:31-39), OneValue (boolean/one_value.rs:44-52).
+static inline bool getb(const uint8_t* bm, size_t i) { return (bm[i >> 3] >> (i & 7)) & 1; }
+
+static void bool_rle(const uint8_t* bits, size_t off, const uint8_t* valid, size_t n, Bytes& o) {
+  uint32_t seen = 0;
+  uint8_t last = 0;
+  bool all_null = true;
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t v = getb(bits, off + i);
+    if (bit(valid, i)) {
+      if (all_null) { all_null = false; last = v; seen++; }
+      else if (last != v) { put<uint32_t>(o, seen); put<uint8_t>(o, last); last = v; seen = 1; }
+      else seen++;
+    } else {
+      seen++;
+    }
+  }
+  if (seen) { put<uint32_t>(o, seen); put<uint8_t>(o, last); }
+}
+
+// compress_sample_ratio (boolean/mod.rs:282-321): seeded windows stand in for
+// thread_rng; the rebuilt sample reads false under null slots.
+static double bool_rle_ratio(const uint8_t* bits, size_t off, const uint8_t* valid, size_t n, Rng& rng) {
+  constexpr size_t SC = 10, SS = 64;
+  Bytes tmp;
+  size_t total_bytes;
+  if (n / SC <= SS) {
+    total_bytes = n / 8;
+    bool_rle(bits, off, valid, n, tmp);
+  } else {
+    uint8_t sb[SC * SS / 8] = {0}, sv[SC * SS / 8] = {0};
+    const size_t sep = n / SC, rem = n % SC;
+    for (size_t k = 0; k < SC; k++) {
+      const size_t range_end = (k == SC - 1 ? sep + rem : sep) - SS;
+      const size_t begin = k * sep + (size_t)(rng.next() % range_end);
+      for (size_t j = 0; j < SS; j++) {
+        const size_t q = k * SS + j;
+        const bool v = bit(valid, begin + j);
+        if (v) sv[q >> 3] |= (uint8_t)(1u << (q & 7));
+        if (v && getb(bits, off + begin + j)) sb[q >> 3] |= (uint8_t)(1u << (q & 7));
+      }
+    }
+    total_bytes = SC * SS / 8;
+    bool_rle(sb, 0, valid ? sv : nullptr, SC * SS, tmp);
+  }
+  return (double)total_bytes / (double)tmp.size();
+}
+
+// bits = the column's bitmap, off = the page's first row (array.slice): the
+// Basic codec takes bitmap.as_slice() -- the parent's bytes when off % 8 == 0
+// (boolean/mod.rs:35-46), a rebuilt zero-padded bitmap otherwise.
+int encode_bool_page(const uint8_t* bits, size_t off, const uint8_t* valid, size_t n, bool nullable, const Opts& opt,
+                     uint64_t seed, Bytes& out) {
+  Rng rng{seed};
+  if (nullable) write_validity(valid, n, out);
+  size_t t = 0, f = 0;
+  for (size_t i = 0; i < n; i++)
+    if (bit(valid, i)) (getb(bits, off + i) ? t : f)++;
+  int codec = opt.default_codec;
+  if (opt.forced == kRle && !(opt.forbidden & (1u << kRle))) {
+    codec = kRle;  // check_rle_env
+  } else if (opt.has_ratio) {
+    double maxr = opt.ratio;
+    for (int c : {kOneValue, kRle}) {
+      if (opt.forbidden & (1u << c)) continue;
+      const double r = c == kOneValue ? ((t == 0 || f == 0) ? (double)n : 0.0) : bool_rle_ratio(bits, off, valid, n, rng);
+      if (r > maxr) {
+        maxr = r;
+        codec = c;
+        if (r == (double)n) break;
+      }
+    }
+  }
+  const size_t hpos = out.size();
+  put<uint8_t>(out, (uint8_t)codec);
+  put<uint64_t>(out, 0);
+  const size_t before = out.size();
+  int rc = 0;
+  if (codec <= kSnappy) {
+    const size_t nb = (n + 7) / 8;
+    if (off % 8 == 0) {
+      rc = common_compress(codec, bits + off / 8, nb, out);
+    } else {
+      std::vector<uint8_t> tmp(nb ? nb : 1, 0);
+      for (size_t i = 0; i < n; i++)
+        if (getb(bits, off + i)) tmp[i >> 3] |= (uint8_t)(1u << (i & 7));
+      rc = common_compress(codec, tmp.data(), nb, out);
+    }
+  } else if (codec == kRle) {
+    bool_rle(bits, off, valid, n, out);
+  } else if (codec == kOneValue) {
+    uint8_t v = 0;
+    for (size_t i = 0; i < n; i++)
+      if (bit(valid, i)) { v = getb(bits, off + i); break; }
+    put<uint8_t>(out, v);
+  } else {
+    rc = SB_E_ARG;
+  }
+  if (rc) return rc;
+  const uint32_t csize = (uint32_t)(out.size() - before), usize = (uint32_t)n;
+  std::memcpy(out.data() + hpos + 1, &csize, 4);
+  std::memcpy(out.data() + hpos + 5, &usize, 4);
+  return 0;
+}
+
 uint64_t page_seed(uint64_t seed, uint64_t page) {
   Rng r{seed ^ (page * 0xD1B54A32D192ED03ull)};
   return r.next();

@@ -24,6 +24,10 @@ int encode_page(int phys, const void* values, const uint8_t* validity, size_t n,
 int encode_binary_page(const uint8_t* values, const int64_t* offsets, const uint8_t* validity, size_t n,
                        bool nullable, int ow, uint64_t parent_len, const Opts& opt, uint64_t seed,
                        std::vector<uint8_t>& out);
+// One Boolean page: rows [off, off + n) of the column bitmap `bits`;
+// validity is page-relative.
+int encode_bool_page(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n, bool nullable,
+                     const Opts& opt, uint64_t seed, std::vector<uint8_t>& out);
 // Sampler seed of page `page` of a column written with `seed`.
 uint64_t page_seed(uint64_t seed, uint64_t page);
 int type_size(int phys);

@@ -78,6 +78,10 @@ struct LaunchArgs {
 // kind: 0 = LDS-staged pages, 1 = pages read from HBM, 2 = deferred work list
 int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a, void* stream);
 
+// Boolean pages: one workgroup per page (grid-strided), page + expanded
+// bitmap in a.stage_bytes of dynamic LDS.
+int launch_bool(const LaunchArgs& a, void* stream);
+
 // dynamic LDS of the deferred pass: page + expanded stream
 constexpr uint32_t kDeferredLds = 150 * 1024;
 constexpr uint32_t kDeferredGrid = 1024;

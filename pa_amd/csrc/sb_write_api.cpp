@@ -53,8 +53,9 @@ sb_status sb_encode_column(int32_t phys, const void* h_values, const uint8_t* h_
                            int32_t nullable, const sb_write_options* opts, uint64_t max_page_rows, int32_t n_threads,
                            uint8_t** h_out, uint64_t* out_len, sb_page_meta** h_metas, uint64_t* n_pages) {
   if (!h_out || !out_len || !h_metas || !n_pages || (n_rows && !h_values)) return SB_E_ARG;
+  const bool is_bool = phys == SB_T_BOOLEAN;  // h_values = the LSB-first values bitmap
   const int ts = sb::enc::type_size(phys);
-  if (!ts) return SB_E_NYI;
+  if (!ts && !is_bool) return SB_E_NYI;
   // page_size = max_page_size.unwrap_or(len).min(len) (common.rs:54-58)
   const uint64_t step = max_page_rows ? std::min<uint64_t>(max_page_rows, n_rows) : n_rows;
   const uint64_t np = step ? (n_rows + step - 1) / step : 0;
@@ -76,8 +77,12 @@ sb_status sb_encode_column(int32_t phys, const void* h_values, const uint8_t* h_
           if ((h_validity[(r0 + i) >> 3] >> ((r0 + i) & 7)) & 1) vb[i >> 3] |= (uint8_t)(1u << (i & 7));
         valid = vb.data();
       }
-      rcs[p] = sb::enc::encode_page(phys, (const uint8_t*)h_values + r0 * ts, valid, m, nullable != 0, o,
-                                    sb::enc::page_seed(seed, p), pages[p]);
+      if (is_bool)
+        rcs[p] = sb::enc::encode_bool_page((const uint8_t*)h_values, r0, valid, m, nullable != 0, o,
+                                           sb::enc::page_seed(seed, p), pages[p]);
+      else
+        rcs[p] = sb::enc::encode_page(phys, (const uint8_t*)h_values + r0 * ts, valid, m, nullable != 0, o,
+                                      sb::enc::page_seed(seed, p), pages[p]);
     }
   };
   int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());

@@ -24,7 +24,7 @@ _PHYS = {
     np.dtype(np.int8): N.INT8, np.dtype(np.int16): N.INT16, np.dtype(np.int32): N.INT32,
     np.dtype(np.int64): N.INT64, np.dtype(np.uint8): N.UINT8, np.dtype(np.uint16): N.UINT16,
     np.dtype(np.uint32): N.UINT32, np.dtype(np.uint64): N.UINT64, np.dtype(np.float32): N.FLOAT32,
-    np.dtype(np.float64): N.FLOAT64,
+    np.dtype(np.float64): N.FLOAT64, np.dtype(np.bool_): N.BOOLEAN,
 }
 
 
@@ -199,8 +199,12 @@ class ColumnDecoder:
     def alloc_outputs(self):
         torch = self._torch
         dev = f"cuda:{self.ctx.device}"
-        tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[self.dtype.itemsize]
-        values = torch.empty(max(self.num_rows, 1), dtype=tdt, device=dev)
+        if self.dtype == np.bool_:  # read_boolean: the values are a bitmap, laid out like the validity
+            nwords = (self.num_rows + 31) // 32
+            values = torch.zeros(max(nwords, 1) * 4, dtype=torch.uint8, device=dev)
+        else:
+            tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[self.dtype.itemsize]
+            values = torch.empty(max(self.num_rows, 1), dtype=tdt, device=dev)
         validity = None
         if self.nullable:
             nwords = (self.num_rows + 31) // 32
@@ -249,7 +253,8 @@ class ColumnDecoder:
 def batch_read_array(chunk, page_metas: Sequence[PageMeta], dtype, nullable: bool, ctx: Optional[Context] = None):
     """batch_read_array (batch_read.rs:190-209) for a flat primitive leaf:
     returns (values, validity_bitmap|None) as device tensors (values typed by
-    width; view as the logical dtype with values.view(...))."""
+    width; view as the logical dtype with values.view(...); Boolean values
+    are a bitmap like the validity)."""
     dec = ColumnDecoder(chunk, page_metas, dtype, nullable, ctx)
     try:
         return dec.decode()

@@ -58,6 +58,12 @@ def encode_column(values: np.ndarray, validity=None, nullable: bool = False,
     """encode_chunk for one flat leaf -> (column chunk bytes, page metas)."""
     options = options or WriteOptions()
     values = np.ascontiguousarray(values)
+    n = len(values)
+    phys = physical_type(values.dtype)
+    if phys == N.BOOLEAN:  # compress_boolean takes the column's bitmap; pages slice it
+        values = np.packbits(values, bitorder="little")
+        if len(values) == 0:
+            values = np.zeros(1, np.uint8)
     vb = None
     if validity is not None:
         vb = np.packbits(np.asarray(validity, bool), bitorder="little")
@@ -67,8 +73,8 @@ def encode_column(values: np.ndarray, validity=None, nullable: bool = False,
     npg = ctypes.c_uint64()
     opts = options.c()
     st = N.lib().sb_encode_column(
-        physical_type(values.dtype), values.ctypes.data_as(ctypes.c_void_p),
-        None if vb is None else vb.ctypes.data_as(ctypes.c_void_p), len(values), int(nullable),
+        phys, values.ctypes.data_as(ctypes.c_void_p),
+        None if vb is None else vb.ctypes.data_as(ctypes.c_void_p), n, int(nullable),
         ctypes.byref(opts), options.max_page_size or 0, n_threads, ctypes.byref(out), ctypes.byref(olen),
         ctypes.byref(metas), ctypes.byref(npg))
     if st:
