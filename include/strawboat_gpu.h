@@ -149,6 +149,39 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* plan, const sb_primitive_out* 
 uint64_t sb_plan_values_bytes(const sb_plan* plan);
 sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* plan, const sb_binary_out* out);
 
+/* List<primitive> columns (one list level over a primitive leaf): the
+ * nested page readers (read_nested_integer / read_nested_double,
+ * read/array/integer.rs:240-261) over read_validity_nested
+ * (read/read_basic.rs:65-173) + create_list (read/array/list.rs:48), pages
+ * concatenated as batch_read_array does.  PageMeta.num_values of a nested
+ * page is its level count. */
+typedef struct {
+  int32_t physical_type; /* leaf type (fixed width) */
+  int32_t list_nullable; /* the List field is nullable */
+  int32_t item_nullable; /* the item field is nullable */
+  int32_t offset_width;  /* 4 = List, 8 = LargeList */
+} sb_list_desc;
+
+/* offsets: rows + 1 entries of offset_width bytes; list validity over the
+ * rows and leaf validity over the leaves (4*ceil(n/32) bytes each, NULL when
+ * that level is not nullable); values: leaves * sizeof(T). */
+typedef struct {
+  void* d_offsets;
+  uint8_t* d_list_validity;
+  void* d_values;
+  uint8_t* d_leaf_validity;
+} sb_list_out;
+
+/* Plans a List column and sizes it on the device (synchronous): rows =
+ * sb_plan_num_rows, leaves = sb_plan_num_leaves; fails with the first bad
+ * page's status. */
+sb_status sb_plan_list_column(sb_ctx* ctx, const sb_list_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                              const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out);
+uint64_t sb_plan_num_leaves(const sb_plan* plan);
+/* Asynchronous decode: sizing pass + bases scan + levels (offsets, bitmaps)
+ * + the values streams at their leaf bases. */
+sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* plan, const sb_list_out* out);
+
 /* Waits for the plan's last decode and returns the first failing page's
  * status (SB_OK if every page decoded); *h_bad_page = its index or -1. */
 sb_status sb_plan_status(sb_ctx* ctx, sb_plan* plan, int64_t* h_bad_page);
@@ -219,6 +252,17 @@ sb_status sb_encode_binary_column(int32_t physical_type, const uint8_t* h_values
                                   int32_t nullable, const sb_write_options* opts, uint64_t max_page_rows,
                                   int32_t n_threads, uint8_t** h_out, uint64_t* out_len, sb_page_meta** h_metas,
                                   uint64_t* n_pages);
+/* encode_chunk for one List<primitive> leaf (write/common.rs:49-119,
+ * write_nested serialize.rs:133-146): pages of max_page_rows top-level rows;
+ * h_offsets = n_rows + 1 absolute int64 positions into h_child (the child
+ * column's values, sizeof(physical_type) each); h_list_validity is over the
+ * rows, h_child_validity over the child values (either may be NULL).
+ * PageMeta.num_values of each page is its level count (num_values(nested)). */
+sb_status sb_encode_list_column(int32_t physical_type, const int64_t* h_offsets, const uint8_t* h_list_validity,
+                                int32_t list_nullable, const void* h_child, const uint8_t* h_child_validity,
+                                int32_t item_nullable, uint64_t n_rows, const sb_write_options* opts,
+                                uint64_t max_page_rows, int32_t n_threads, uint8_t** h_out, uint64_t* out_len,
+                                sb_page_meta** h_metas, uint64_t* n_pages);
 uint64_t sb_page_seed(uint64_t seed, uint64_t page);
 /* NativeWriter::finish (write/writer.rs:128-167) footer bytes. */
 sb_status sb_write_footer(const uint8_t* h_schema, uint64_t schema_len, const uint64_t* h_col_offsets,

@@ -1704,6 +1704,13 @@ int orc_write_binary_page(const uint8_t* values, const int64_t* offsets, const u
 /* ======================================================================= */
 static uint32_t bit_width_of(uint32_t max_level) { uint32_t b = 0; while (max_level) { b++; max_level >>= 1; } return b; }
 
+/* parquet2 0.17 hybrid_rle::encode_u32 (one bit-packed run; header groups =
+ * ceil(n / 8)) -> bitpacked_encode_u32: 32-value chunks of 4*bw bytes, then
+ * the remainder chunk packed from a buffer that still holds the previous
+ * chunk's values past the remainder, truncated to ceil(rem * bw / 8) bytes --
+ * so the stream is ceil(n * bw / 8) bytes and the last byte's spare bits are
+ * stale levels.  Third-party (not in the reference tree): restated from the
+ * published crate, parity unpinned beyond round trips. */
 static void encode_levels(const uint32_t* lv, size_t n, uint32_t bw, orc_buf* out) {
   size_t groups = (n + 7) / 8;
   uint8_t hdr[10];
@@ -1711,13 +1718,19 @@ static void encode_levels(const uint32_t* lv, size_t n, uint32_t bw, orc_buf* ou
   uint64_t h = ((uint64_t)groups << 1) | 1;
   do { uint8_t c = h & 0x7F; h >>= 7; if (h) c |= 0x80; hdr[hl++] = c; } while (h);
   buf_put(out, hdr, hl);
-  size_t nbytes = groups * bw, at = out->len;
-  buf_reserve(out, nbytes);
-  memset(out->data + at, 0, nbytes);
-  for (size_t i = 0; i < n; i++)
-    for (uint32_t k = 0; k < bw; k++)
-      if ((lv[i] >> k) & 1) { size_t q = i * bw + k; out->data[at + (q >> 3)] |= (uint8_t)(1u << (q & 7)); }
-  out->len += nbytes;
+  uint32_t buffer[32] = {0};
+  size_t chunks = n / 32, rem = n % 32;
+  for (size_t c = 0; c <= chunks; c++) {
+    size_t take = c < chunks ? 32 : rem;
+    if (take == 0) break;
+    for (size_t j = 0; j < take; j++) buffer[j] = lv[c * 32 + j];
+    uint8_t packed[128];
+    memset(packed, 0, sizeof packed);
+    for (size_t j = 0; j < 32; j++)
+      for (uint32_t k = 0; k < bw; k++)
+        if ((buffer[j] >> k) & 1) { size_t q = j * bw + k; packed[q >> 3] |= (uint8_t)(1u << (q & 7)); }
+    buf_put(out, packed, (take * bw + 7) / 8);
+  }
 }
 
 int orc_write_list_page(const int64_t* list_offsets, const uint8_t* list_validity, size_t rows, int list_nullable,
@@ -1784,7 +1797,10 @@ int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int l
   if (!rc) rc = orc_hybrid_decode(page + pos + rep_len, def_len, bit_width_of(max_def), num_levels, def);
   if (rc) { free(rep); free(def); return rc; }
   pos += rep_len + def_len;
-  /* read_basic.rs:107-164 with cum_sum = [0, nl + 1, nl + 1 + ni], cum_rep = [0, 1, 1] */
+  /* A first level that does not start a row would push leaves outside any
+   * list; the ListArray built from it fails its offsets check (OutOfSpec).
+   * read_basic.rs:107-164 with cum_sum = [0, nl + 1, nl + 1 + ni], cum_rep = [0, 1, 1] */
+  if (num_levels > 0 && rep[0] != 0) { free(rep); free(def); return ORC_E_OUT_OF_SPEC; }
   const uint32_t cs1 = nl + 1;
   size_t rows = 0, leaves = 0;
   for (size_t l = 0; l < num_levels; l++) {

@@ -26,6 +26,7 @@ EXPORTED = [
     "sb_decode_planned", "sb_plan_status", "sb_decode_column", "sb_plan_last_kernel_ms", "sb_plan_enable_timing",
     "sb_decompress_values", "sb_read_meta", "sb_encode_page", "sb_encode_column", "sb_page_seed",
     "sb_write_footer", "sb_free", "sb_encode_binary_column", "sb_plan_values_bytes", "sb_decode_binary_planned",
+    "sb_encode_list_column", "sb_plan_list_column", "sb_plan_num_leaves", "sb_decode_list_planned",
 ]
 
 

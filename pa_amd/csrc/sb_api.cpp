@@ -42,6 +42,11 @@ struct sb_plan {
   int inflate_state = -1;   // same, for k_inflate jobs
   bool binary = false;
   bool boolean = false;  // SB_T_BOOLEAN: values are a bitmap (k_bool_decode)
+  bool list = false;     // List<primitive>: levels kernels + `inner` (the values streams as flat pages)
+  sb_list_desc ldesc{};
+  uint64_t* d_lc = nullptr;  // [counts n | row bases n | leaf bases n | totals 2]
+  sb_plan* inner = nullptr;
+  uint64_t n_leaves = 0;
   int offset_width = 0;
   uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1]
   uint64_t values_bytes = 0;
@@ -148,6 +153,8 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_jobs) (void)hipFree(p->d_jobs);
   if (p->d_scratch) (void)hipFree(p->d_scratch);
   if (p->d_bin) (void)hipFree(p->d_bin);
+  if (p->d_lc) (void)hipFree(p->d_lc);
+  if (p->inner) sb_plan_destroy(p->inner);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   delete p;
@@ -368,6 +375,13 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
 
 sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
   if (!ctx || !p) return fail(ctx, SB_E_ARG, "null argument");
+  if (p->list && p->inner) {  // levels first, then the values streams
+    p->list = false;
+    sb_status st = sb_plan_status(ctx, p, bad);
+    p->list = true;
+    if (st) return st;
+    return sb_plan_status(ctx, p->inner, bad);
+  }
   if (bad) *bad = -1;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -387,6 +401,102 @@ sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
       if (bad) *bad = (int64_t)i;
       return fail(ctx, (sb_status)st[i], "page %llu: %s", (unsigned long long)i, sb_status_str((int)st[i]));
     }
+  }
+  return SB_OK;
+}
+
+static sb::ListLaunch list_launch(sb_plan* p, const sb_list_out* out) {
+  const uint64_t n = p->n_pages;
+  return sb::ListLaunch{p->d_chunk, p->d_pages, (uint32_t)n, (uint32_t)p->ldesc.list_nullable,
+                        (uint32_t)p->ldesc.item_nullable, (uint32_t)p->ldesc.offset_width, p->d_lc, p->d_lc + n,
+                        p->d_lc + 3 * n, p->inner->d_pages, out ? (uint8_t*)out->d_offsets : nullptr,
+                        out ? (uint32_t*)out->d_list_validity : nullptr, out ? (uint32_t*)out->d_leaf_validity : nullptr,
+                        p->d_status};
+}
+
+sb_status sb_plan_list_column(sb_ctx* ctx, const sb_list_desc* d, const uint8_t* d_chunk, uint64_t chunk_len,
+                              const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out) {
+  if (!ctx || !d || !out) return fail(ctx, SB_E_ARG, "null argument");
+  bool is_float;
+  if (!type_width(d->physical_type, &is_float)) return fail(ctx, SB_E_NYI, "list leaf type %d not supported", d->physical_type);
+  if (d->offset_width != 4 && d->offset_width != 8) return fail(ctx, SB_E_ARG, "offset width must be 4 or 8");
+  sb_column_desc cd{d->physical_type, 0};
+  sb_plan* inner = nullptr;
+  sb_status st = sb_plan_column(ctx, &cd, d_chunk, chunk_len, h_metas, n_pages, &inner);
+  if (st) return st;
+  sb_plan* p = new sb_plan();
+  p->desc = cd;
+  p->list = true;
+  p->ldesc = *d;
+  p->inner = inner;
+  p->d_chunk = d_chunk;
+  p->chunk_len = chunk_len;
+  p->n_pages = n_pages;
+  p->width = inner->width;
+  p->is_float = is_float;
+  const size_t np = n_pages ? n_pages : 1;
+  hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
+  if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&p->d_lc, (3 * np + 2) * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipEventCreate(&p->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&p->ev1);
+  if (e == hipSuccess && n_pages)  // the level pages (inner's table becomes the values streams)
+    e = hipMemcpyAsync(p->d_pages, inner->d_pages, n_pages * sizeof(sb::PageDesc), hipMemcpyDeviceToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(p->d_lc, 0, (3 * np + 2) * sizeof(uint64_t), ctx->stream);
+  if (e != hipSuccess) {
+    sb_plan_destroy(p);
+    return fail(ctx, SB_E_DEVICE, "list plan alloc: %s", hipGetErrorString(e));
+  }
+  if (n_pages) {  // size once so the caller can allocate the outputs
+    sb::ListLaunch L = list_launch(p, nullptr);
+    if (sb::launch_list(0, L, ctx->stream) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "list sizing failed: %s", hipGetErrorString(hipGetLastError()));
+    }
+    std::vector<uint32_t> stv(n_pages);
+    uint64_t tot[2];
+    (void)hipMemcpy(stv.data(), p->d_status, n_pages * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(tot, p->d_lc + 3 * n_pages, sizeof tot, hipMemcpyDeviceToHost);
+    for (uint64_t i = 0; i < n_pages; i++) {
+      if (stv[i]) {
+        sb_plan_destroy(p);
+        return fail(ctx, (sb_status)stv[i], "page %llu: %s", (unsigned long long)i, sb_status_str((int)stv[i]));
+      }
+    }
+    p->n_rows = tot[0];
+    p->n_leaves = tot[1];
+  }
+  *out = p;
+  return SB_OK;
+}
+
+uint64_t sb_plan_num_leaves(const sb_plan* p) { return p ? p->n_leaves : 0; }
+
+sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* p, const sb_list_out* out) {
+  if (!ctx || !p || !out) return fail(ctx, SB_E_ARG, "null argument");
+  if (!p->list) return fail(ctx, SB_E_ARG, "not a list plan");
+  if (!out->d_offsets || (p->n_leaves && !out->d_values)) return fail(ctx, SB_E_ARG, "list output buffers are null");
+  if (p->ldesc.list_nullable && p->n_rows && !out->d_list_validity) return fail(ctx, SB_E_ARG, "list validity is null");
+  if (p->ldesc.item_nullable && p->n_leaves && !out->d_leaf_validity) return fail(ctx, SB_E_ARG, "leaf validity is null");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
+  if (p->ldesc.list_nullable && p->n_rows)
+    HIP_TRY(ctx, hipMemsetAsync(out->d_list_validity, 0, (p->n_rows + 31) / 32 * 4, ctx->stream));
+  if (p->ldesc.item_nullable && p->n_leaves)
+    HIP_TRY(ctx, hipMemsetAsync(out->d_leaf_validity, 0, (p->n_leaves + 31) / 32 * 4, ctx->stream));
+  if (!p->n_pages) {
+    HIP_TRY(ctx, hipMemsetAsync(out->d_offsets, 0, (size_t)p->ldesc.offset_width, ctx->stream));
+  } else {
+    sb::ListLaunch L = list_launch(p, out);
+    if (sb::launch_list(0, L, ctx->stream) || sb::launch_list(1, L, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "list levels launch failed: %s", hipGetErrorString(hipGetLastError()));
+    sb_primitive_out vo{out->d_values ? out->d_values : out->d_offsets, nullptr};  // (no leaves: nothing written)
+    sb_status st = sb_decode_planned(ctx, p->inner, &vo);
+    if (st) return st;
+  }
+  if (p->timing) {
+    HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
+    p->timed = true;
   }
   return SB_OK;
 }

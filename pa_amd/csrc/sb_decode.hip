@@ -2070,6 +2070,293 @@ __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
   }
 }
 
+// ===========================================================================
+// Nested List<primitive> pages: read_validity_nested (read/read_basic.rs:65-173)
+// + create_list (read/array/list.rs:48), one list level over a primitive leaf.
+// Page = [u32 rows][u32 rep_len][u32 def_len][rep hybrid][def hybrid][values].
+// Per level: rep == 0 starts a row (list offset = leaves so far, list valid =
+// def > 0); def >= cum_sum[1] = nl + 1 is a leaf (leaf valid = def > nl + 1);
+// decoding stops before the level that would start row `rows + 1`
+// (:158-162).  k_list_size counts each page's rows and leaves and fills the
+// page's values-stream descriptor, k_list_scan turns counts into bases,
+// k_list_levels writes offsets and both bitmaps; the values streams then go
+// through the flat decode kernels (k_decode_staged / global / deferred /
+// k_inflate) at their leaf bases.
+// ===========================================================================
+constexpr uint32_t kLvK = 8;                    // levels per thread per tile
+constexpr uint32_t kLvTile = NT * kLvK;         // levels per tile
+constexpr uint32_t kMaxRuns = 64;               // hybrid runs per level stream
+
+struct LvRuns {
+  uint32_t n;
+  uint32_t start[kMaxRuns + 1];  // first level of each run
+  uint32_t arg[kMaxRuns];        // bit-packed: 0x80000000 | payload position; RLE: the value
+};
+
+struct ListShared {
+  uint32_t rows, vpos, bw_def;
+  LvRuns rep, def;
+  uint32_t lbits[kLvTile / 32 + 4];  // tile list-validity bits (+ over-read pad)
+  uint32_t fbits[kLvTile / 32 + 4];  // tile leaf-validity bits
+};
+
+// parquet2 HybridRleDecoder (hybrid_rle/decoder.rs) run headers of one level
+// stream [p, end) covering L levels, bit width bw.  Thread 0.
+template <class Src>
+__device__ bool parse_runs(const Src& s, Shared& sh, uint32_t p, uint32_t end, uint32_t L, uint32_t bw, LvRuns& R) {
+  uint32_t covered = 0, n = 0;
+  while (covered < L) {
+    uint32_t h = 0, sft = 0;
+    for (;;) {  // ULEB128 header
+      if (p >= end || sft > 28) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      const uint32_t c = s.u8(p++);
+      h |= (c & 0x7Fu) << sft;
+      if (!(c & 0x80)) break;
+      sft += 7;
+    }
+    if (n == kMaxRuns) { set_err(sh, ST_NYI); return false; }
+    R.start[n] = covered;
+    if (h & 1) {  // bit-packed: h >> 1 groups of 8, clamped to the bytes present
+      const uint64_t want = (uint64_t)(h >> 1) * bw;
+      const uint32_t have = (uint32_t)min<uint64_t>(want, end - p);
+      const uint32_t vals = (uint32_t)min<uint64_t>((uint64_t)(h >> 1) * 8, (uint64_t)have * 8 / bw);
+      if (vals == 0) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      R.arg[n] = 0x80000000u | p;
+      p += have;
+      covered += vals;
+    } else {  // RLE: h >> 1 repeats of a ceil(bw / 8)-byte value
+      const uint32_t vb = (bw + 7) / 8;
+      if (p + vb > end) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      uint32_t v = 0;
+      for (uint32_t k = 0; k < vb; k++) v |= s.u8(p + k) << (8 * k);
+      R.arg[n] = v;
+      p += vb;
+      covered += h >> 1;
+    }
+    n++;
+  }
+  R.start[n] = covered;
+  R.n = n;
+  return true;
+}
+
+template <class Src>
+__device__ __forceinline__ uint32_t level_at(const Src& s, const LvRuns& R, uint32_t i, uint32_t bw) {
+  uint32_t r = 0;
+  if (R.n > 1) {  // last run starting at or before i
+    uint32_t lo = 0, hi = R.n;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (R.start[mid] <= i) lo = mid; else hi = mid;
+    }
+    r = lo;
+  }
+  const uint32_t a = R.arg[r];
+  if (!(a & 0x80000000u)) return a;
+  const uint32_t bit = (i - R.start[r]) * bw;
+  return (s.u32((a & 0x7FFFFFFFu) + (bit >> 3)) >> (bit & 7)) & ((1u << bw) - 1);
+}
+
+struct ListArgs {
+  const uint8_t* chunk;
+  const PageDesc* pages;  // num_values = the page's level count (PageMeta.num_values)
+  uint32_t n_pages;
+  uint32_t nl, ni, ow;    // list nullable, item nullable, offset width
+  uint64_t* counts;       // [n_pages] rows << 32 | leaves
+  uint64_t* bases;        // [2 * n_pages] row base, leaf base
+  uint64_t* totals;       // [2] rows, leaves
+  PageDesc* vpages;       // values stream of each page, as a flat page
+  uint8_t* out_offsets;
+  uint32_t* out_list_validity;
+  uint32_t* out_leaf_validity;
+  uint32_t* status;
+  uint32_t lds_bytes;
+};
+
+// Header + run tables (thread 0).  Levels region = [0, 12 + rep_len + def_len).
+template <class Src>
+__device__ bool list_parse(const Src& s, Shared& sh, ListShared& ls, const PageDesc& pd, const ListArgs& a) {
+  const uint32_t len = pd.byte_len, L = pd.num_values;
+  if (len < 12) { set_err(sh, ST_IO); return false; }
+  const uint32_t rows = s.u32(0), rl = s.u32(4), dl = s.u32(8);
+  if ((uint64_t)12 + rl + dl > len) { set_err(sh, ST_IO); return false; }
+  const uint32_t max_def = a.nl + 1 + a.ni;
+  ls.rows = rows;
+  ls.vpos = 12 + rl + dl;
+  ls.bw_def = 32 - __clz(max_def);
+  if (!parse_runs(s, sh, 12, 12 + rl, L, 1, ls.rep)) return false;
+  if (!parse_runs(s, sh, 12 + rl, 12 + rl + dl, L, ls.bw_def, ls.def)) return false;
+  if (L > 0 && rows == 0) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+  return true;
+}
+
+// Walks the page's levels tile by tile.  WRITE = false: *rows_out / *leaves_out
+// get the consumed counts.  WRITE = true: offsets and bitmaps at the bases.
+template <bool WRITE, class Src>
+__device__ void list_levels(const Src& s, Shared& sh, ListShared& ls, const PageDesc& pd, const ListArgs& a,
+                            uint64_t rbase, uint64_t lbase, uint32_t* rows_out, uint32_t* leaves_out) {
+  const uint32_t tid = threadIdx.x, L = pd.num_values, rows = ls.rows, bwd = ls.bw_def;
+  const uint32_t cs1 = a.nl + 1;
+  uint32_t carry_r = 0, carry_l = 0, my_leaves = 0;
+  for (uint32_t t0 = 0; t0 < L; t0 += kLvTile) {
+    uint32_t rsm = 0, lfm = 0, lvm = 0, fvm = 0;
+    const uint32_t i0 = t0 + tid * kLvK;
+#pragma unroll
+    for (uint32_t k = 0; k < kLvK; k++) {
+      const uint32_t i = i0 + k;
+      if (i < L) {
+        const uint32_t r = level_at(s, ls.rep, i, 1), d = level_at(s, ls.def, i, bwd);
+        if (r == 0) rsm |= 1u << k;
+        if (r <= 1 && d >= cs1) lfm |= 1u << k;
+        if (d > 0) lvm |= 1u << k;
+        if (d > cs1) fvm |= 1u << k;
+      }
+    }
+    if (t0 == 0 && tid == 0 && L > 0 && !(rsm & 1)) set_err(sh, ST_OUT_OF_SPEC);  // level 0 starts no row
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan<uint64_t>(((uint64_t)__popc(rsm) << 32) | __popc(lfm), sh, &tot);
+    const uint32_t rb = carry_r + (uint32_t)(ex >> 32), lb = carry_l + (uint32_t)ex;
+    // consumed: levels whose inclusive row count stays <= rows (a suffix of the page is dropped)
+    uint32_t cm = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kLvK; k++)
+      if (rb + __popc(rsm & ((2u << k) - 1)) <= rows) cm |= 1u << k;
+    const uint32_t tile_r0 = carry_r, tile_l0 = carry_l;
+    const uint32_t tile_rows = min(carry_r + (uint32_t)(tot >> 32), rows) - min(carry_r, rows);
+    my_leaves += __popc(lfm & cm);
+    if constexpr (WRITE) {
+      for (uint32_t w = tid; w < kLvTile / 32 + 4; w += NT) ls.lbits[w] = ls.fbits[w] = 0;
+      __syncthreads();
+#pragma unroll
+      for (uint32_t k = 0; k < kLvK; k++) {
+        if (!((cm >> k) & 1)) continue;
+        const uint32_t below = (1u << k) - 1;
+        if ((rsm >> k) & 1) {
+          const uint32_t r = rb + __popc(rsm & below);  // page row of this row start
+          const uint64_t off = lbase + lb + __popc(lfm & below);
+          bin_put_off(a.out_offsets, rbase + r, off, a.ow);
+          if (a.nl && ((lvm >> k) & 1)) atomicOr(&ls.lbits[(r - tile_r0) >> 5], 1u << ((r - tile_r0) & 31));
+        }
+        if (a.ni && ((lfm & fvm) >> k & 1)) {
+          const uint32_t f = lb + __popc(lfm & below) - tile_l0;
+          atomicOr(&ls.fbits[f >> 5], 1u << (f & 31));
+        }
+      }
+      uint32_t tile_leaves = __popc(lfm & cm);
+      uint64_t tl;
+      block_excl_scan<uint64_t>(tile_leaves, sh, &tl);  // (syncs: the tile bits are complete)
+      const LdsSrc lsrc{(const uint32_t*)ls.lbits, 0}, fsrc{(const uint32_t*)ls.fbits, 0};
+      if (a.nl) write_validity(lsrc, 0, tile_rows, rbase + tile_r0, a.out_list_validity);
+      if (a.ni) write_validity(fsrc, 0, (uint32_t)tl, lbase + tile_l0, a.out_leaf_validity);
+      __syncthreads();
+    }
+    carry_r += (uint32_t)(tot >> 32);
+    carry_l += (uint32_t)tot;
+    if (carry_r > rows) break;  // uniform: every later level is past the last row
+  }
+  uint64_t lt;
+  block_excl_scan<uint64_t>(my_leaves, sh, &lt);
+  if (tid == 0) {
+    const uint32_t rc = min(carry_r, rows);
+    if (rc != rows) set_err(sh, ST_OUT_OF_SPEC);  // levels ended before `rows` rows
+    *rows_out = rc;
+    *leaves_out = (uint32_t)lt;
+  }
+}
+
+template <bool WRITE>
+__device__ void list_page(const ListArgs& a, Shared& sh, ListShared& ls, uint32_t page, uint32_t* stage) {
+  const PageDesc pd = a.pages[page];
+  __shared__ uint32_t rows_c, leaves_c, region;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) {
+    sh.err = 0;
+    GlbSrc g{a.chunk + pd.byte_off};
+    region = 0;
+    if (pd.byte_len >= 12) {
+      const uint64_t r = 12ull + g.u32(4) + g.u32(8);
+      region = (uint32_t)min<uint64_t>(r, pd.byte_len);
+    }
+  }
+  __syncthreads();
+  uint64_t rbase = 0, lbase = 0;
+  if constexpr (WRITE) {
+    rbase = a.bases[page];
+    lbase = a.bases[a.n_pages + page];
+  }
+  const uint32_t need = (region + 15 + kStagePad + 15) & ~15u;
+  if (need <= a.lds_bytes) {  // levels staged in LDS
+    const uint32_t base = stage_page((u32x4*)stage, a.chunk + pd.byte_off, region);
+    LdsSrc s{stage, base};
+    if (tid == 0) list_parse(s, sh, ls, pd, a);
+    __syncthreads();
+    if (!sh.err) list_levels<WRITE>(s, sh, ls, pd, a, rbase, lbase, &rows_c, &leaves_c);
+  } else {
+    GlbSrc s{a.chunk + pd.byte_off};
+    if (tid == 0) list_parse(s, sh, ls, pd, a);
+    __syncthreads();
+    if (!sh.err) list_levels<WRITE>(s, sh, ls, pd, a, rbase, lbase, &rows_c, &leaves_c);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (!WRITE) {
+      const bool ok = sh.err == 0;
+      a.counts[page] = ok ? (((uint64_t)rows_c << 32) | leaves_c) : 0;
+      // the page's values stream, decoded as a flat non-nullable page of `leaves` values
+      a.vpages[page] = PageDesc{pd.byte_off + (ok ? ls.vpos : 0), 0, ok ? pd.byte_len - ls.vpos : 0,
+                                ok ? leaves_c : 0, 0};
+    }
+    if (sh.err) a.status[page] = sh.err;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(NT) void k_list_size(ListArgs a) {
+  extern __shared__ u32x4 lstage[];
+  __shared__ Shared sh;
+  __shared__ ListShared ls;
+  for (uint32_t page = blockIdx.x; page < a.n_pages; page += gridDim.x) {
+    if (threadIdx.x == 0) a.status[page] = 0;
+    list_page<false>(a, sh, ls, page, (uint32_t*)lstage);
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
+  extern __shared__ u32x4 lstage[];
+  __shared__ Shared sh;
+  __shared__ ListShared ls;
+  for (uint32_t page = blockIdx.x; page < a.n_pages; page += gridDim.x) {
+    if (a.status[page]) continue;  // (uniform) sizing errors stand
+    list_page<true>(a, sh, ls, page, (uint32_t*)lstage);
+  }
+}
+
+// Exclusive scans of the page row and leaf counts (one workgroup); the values
+// pages start at their leaf bases; the final list offset is the leaf total.
+__global__ __launch_bounds__(NT) void k_list_scan(ListArgs a) {
+  __shared__ Shared sh;
+  uint64_t cr = 0, cl = 0;
+  for (uint32_t p0 = 0; p0 < a.n_pages; p0 += NT) {
+    const uint32_t p = p0 + threadIdx.x;
+    const uint64_t c = p < a.n_pages ? a.counts[p] : 0;
+    uint64_t tr, tl;
+    const uint64_t er = block_excl_scan<uint64_t>(c >> 32, sh, &tr);
+    const uint64_t el = block_excl_scan<uint64_t>(c & 0xFFFFFFFFull, sh, &tl);
+    if (p < a.n_pages) {
+      a.bases[p] = cr + er;
+      a.bases[a.n_pages + p] = cl + el;
+      a.vpages[p].row_off = cl + el;
+    }
+    cr += tr;
+    cl += tl;
+  }
+  if (threadIdx.x == 0) {
+    a.totals[0] = cr;
+    a.totals[1] = cl;
+    if (a.out_offsets) bin_put_off(a.out_offsets, cr, cl, a.ow);
+  }
+}
+
 }  // namespace sbk
 
 namespace sb {
@@ -2136,6 +2423,28 @@ int launch_bool(const LaunchArgs& a, void* stream) {
   }
   const uint32_t grid = std::min<uint32_t>(a.n_list, 65535u);
   hipLaunchKernelGGL(sbk::k_bool_decode, dim3(grid), dim3(sbk::NT), a.stage_bytes, (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}  // namespace sb
+
+namespace sb {
+int launch_list(int stage, const ListLaunch& L, void* stream) {
+  sbk::ListArgs a{L.chunk, L.pages, L.n_pages, L.list_nullable, L.item_nullable, L.offset_width, L.counts, L.bases,
+                  L.totals, L.vpages, L.out_offsets, L.out_list_validity, L.out_leaf_validity, L.status, kListLds};
+  hipStream_t st = (hipStream_t)stream;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)sbk::k_list_size, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kListLds);
+    hipFuncSetAttribute((const void*)sbk::k_list_levels, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kListLds);
+    attr = true;
+  }
+  const dim3 grid(std::min<uint32_t>(L.n_pages ? L.n_pages : 1, 65535u)), block(sbk::NT);
+  if (stage == 0) {
+    hipLaunchKernelGGL(sbk::k_list_size, grid, block, kListLds, st, a);
+    hipLaunchKernelGGL(sbk::k_list_scan, dim3(1), block, 0, st, a);
+  } else {
+    hipLaunchKernelGGL(sbk::k_list_levels, grid, block, kListLds, st, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb

@@ -616,6 +616,82 @@ int encode_page(int phys, const void* values, const uint8_t* valid, size_t n, bo
   return SB_E_NYI;
 }
 
+// ---- nested List<primitive> pages: write_nested (serialize.rs:133-146) =
+// write_nested_validity (:217-232: u32 rows, u32 rep_len, u32 def_len, then
+// arrow2 write_rep_and_def V2 -> parquet2 encode_u32 per stream) + the leaf
+// values of the page's rows through compress_integer / compress_double.
+static void encode_levels_u32(const std::vector<uint32_t>& lv, uint32_t bw, Bytes& o) {
+  // one bit-packed hybrid run (groups = ceil(n / 8)); bitpacked_encode_u32
+  // packs 32-value chunks and truncates the last to ceil(rem * bw / 8) bytes,
+  // its spare bits holding the previous chunk's levels (the reused buffer)
+  const size_t n = lv.size();
+  uint64_t h = ((uint64_t)((n + 7) / 8) << 1) | 1;
+  do { uint8_t c = h & 0x7F; h >>= 7; if (h) c |= 0x80; o.push_back(c); } while (h);
+  uint32_t buffer[32] = {0};
+  for (size_t c0 = 0; c0 < n; c0 += 32) {
+    const size_t take = std::min<size_t>(32, n - c0);
+    for (size_t j = 0; j < take; j++) buffer[j] = lv[c0 + j];
+    uint8_t packed[128] = {0};
+    for (size_t j = 0; j < 32; j++) {
+      const uint64_t q = (uint64_t)j * bw;
+      const uint64_t v = (uint64_t)buffer[j] << (q & 7);
+      for (uint32_t k = 0; k < 3 && (q >> 3) + k < 128; k++) packed[(q >> 3) + k] |= (uint8_t)(v >> (8 * k));
+    }
+    o.insert(o.end(), packed, packed + (take * bw + 7) / 8);
+  }
+}
+
+static int compress_values(int phys, const void* v, const uint8_t* valid, size_t n, const Opts& opt, Rng& rng, Bytes& o) {
+  switch (phys) {
+#define SB_CV(E, T, S) case E: { Arr<T> a{(const T*)v, valid, n, S}; return compress_stream(a, opt, rng, o); }
+    SB_CV(SB_T_INT8, int8_t, true) SB_CV(SB_T_INT16, int16_t, true) SB_CV(SB_T_INT32, int32_t, true)
+    SB_CV(SB_T_INT64, int64_t, true) SB_CV(SB_T_UINT8, uint8_t, false) SB_CV(SB_T_UINT16, uint16_t, false)
+    SB_CV(SB_T_UINT32, uint32_t, false) SB_CV(SB_T_UINT64, uint64_t, false) SB_CV(SB_T_FLOAT32, float, false)
+    SB_CV(SB_T_FLOAT64, double, false)
+#undef SB_CV
+  }
+  return SB_E_NYI;
+}
+
+int encode_list_page(int phys, const int64_t* offsets, const uint8_t* list_valid, size_t rows, bool list_nullable,
+                     const void* child, const uint8_t* child_valid, bool item_nullable, const Opts& opt,
+                     uint64_t seed, Bytes& out, uint64_t* num_levels) {
+  const int ts = type_size(phys);
+  if (!ts) return SB_E_NYI;
+  Rng rng{seed};
+  const uint32_t nl = list_nullable, ni = item_nullable, max_def = nl + 1 + ni;
+  std::vector<uint32_t> rep, def;
+  rep.reserve(rows + (size_t)(offsets[rows] - offsets[0]));
+  def.reserve(rep.capacity());
+  for (size_t r = 0; r < rows; r++) {  // RepLevelsIter / DefLevelsIter of one list level
+    const int64_t b = offsets[r], e = offsets[r + 1];
+    if (nl && !bit(list_valid, r)) { rep.push_back(0); def.push_back(0); continue; }
+    if (e == b) { rep.push_back(0); def.push_back(nl); continue; }
+    for (int64_t j = b; j < e; j++) {
+      rep.push_back(j > b);
+      def.push_back(ni ? (bit(child_valid, (size_t)j) ? max_def : max_def - 1) : max_def);
+    }
+  }
+  Bytes lv;
+  encode_levels_u32(rep, 1, lv);
+  const size_t rep_len = lv.size();
+  encode_levels_u32(def, 32 - (uint32_t)__builtin_clz(max_def), lv);
+  put<uint32_t>(out, (uint32_t)rows);
+  put<uint32_t>(out, (uint32_t)rep_len);
+  put<uint32_t>(out, (uint32_t)(lv.size() - rep_len));
+  out.insert(out.end(), lv.begin(), lv.end());
+  *num_levels = rep.size();
+  // slice_parquet_array: the leaf values of rows [0, rows), validity re-based
+  const size_t v0 = (size_t)offsets[0], nv = (size_t)(offsets[rows] - offsets[0]);
+  std::vector<uint8_t> vb;
+  if (child_valid) {
+    vb.assign((nv + 7) / 8 + 1, 0);
+    for (size_t i = 0; i < nv; i++)
+      if (bit(child_valid, v0 + i)) vb[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  return compress_values(phys, (const uint8_t*)child + v0 * ts, child_valid ? vb.data() : nullptr, nv, opt, rng, out);
+}
+
 // ---- boolean pages: compress_boolean (compression/boolean/mod.rs:22-61),
 // gen_stats (:178-220), choose_compressor (:222-280), RLE over the bits as u8
 // (boolean/rle.rs:31-39), OneValue (boolean/one_value.rs:44-52).

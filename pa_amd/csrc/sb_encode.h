@@ -28,6 +28,12 @@ int encode_binary_page(const uint8_t* values, const int64_t* offsets, const uint
 // validity is page-relative.
 int encode_bool_page(const uint8_t* bits, size_t off, const uint8_t* validity, size_t n, bool nullable,
                      const Opts& opt, uint64_t seed, std::vector<uint8_t>& out);
+// One List<primitive> page of `rows` top-level rows: offsets are rows + 1
+// absolute positions into the child column; list_valid is page-relative,
+// child_valid column-level.  *num_levels = the page's PageMeta.num_values.
+int encode_list_page(int phys, const int64_t* offsets, const uint8_t* list_valid, size_t rows, bool list_nullable,
+                     const void* child, const uint8_t* child_valid, bool item_nullable, const Opts& opt,
+                     uint64_t seed, std::vector<uint8_t>& out, uint64_t* num_levels);
 // Sampler seed of page `page` of a column written with `seed`.
 uint64_t page_seed(uint64_t seed, uint64_t page);
 int type_size(int phys);

@@ -106,4 +106,23 @@ struct BinLaunch {
 };
 int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
 
+// List<primitive> columns: stage 0 = size pages + scan bases (+ the final
+// offset when out_offsets is set), stage 1 = offsets + bitmaps.
+struct ListLaunch {
+  const uint8_t* chunk;
+  const PageDesc* pages;
+  uint32_t n_pages;
+  uint32_t list_nullable, item_nullable, offset_width;
+  uint64_t* counts;
+  uint64_t* bases;
+  uint64_t* totals;
+  PageDesc* vpages;
+  uint8_t* out_offsets;
+  uint32_t* out_list_validity;
+  uint32_t* out_leaf_validity;
+  uint32_t* status;
+};
+constexpr uint32_t kListLds = 32 * 1024;  // staged level streams (larger ones are read from HBM)
+int launch_list(int stage, const ListLaunch& a, void* stream);
+
 }  // namespace sb

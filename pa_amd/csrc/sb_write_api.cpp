@@ -172,6 +172,69 @@ sb_status sb_encode_binary_column(int32_t phys, const uint8_t* h_values, uint64_
   return SB_OK;
 }
 
+// encode_chunk for one List<primitive> leaf (common.rs:49-119 with
+// slice_parquet_array per page of max_page_rows top-level rows; write_nested,
+// serialize.rs:133-146).  PageMeta.num_values = the page's level count.
+sb_status sb_encode_list_column(int32_t phys, const int64_t* h_offsets, const uint8_t* h_list_validity,
+                                int32_t list_nullable, const void* h_child, const uint8_t* h_child_validity,
+                                int32_t item_nullable, uint64_t n_rows, const sb_write_options* opts,
+                                uint64_t max_page_rows, int32_t n_threads, uint8_t** h_out, uint64_t* out_len,
+                                sb_page_meta** h_metas, uint64_t* n_pages) {
+  if (!h_out || !out_len || !h_metas || !n_pages || !h_offsets || (n_rows && h_offsets[n_rows] > h_offsets[0] && !h_child))
+    return SB_E_ARG;
+  if (!sb::enc::type_size(phys)) return SB_E_NYI;
+  const uint64_t step = max_page_rows ? std::min<uint64_t>(max_page_rows, n_rows) : n_rows;
+  const uint64_t np = step ? (n_rows + step - 1) / step : 0;
+  std::vector<std::vector<uint8_t>> pages(np);
+  std::vector<uint64_t> levels(np, 0);
+  std::vector<int> rcs(np, 0);
+  const Opts o = to_opts(opts);
+  const uint64_t seed = opts ? opts->seed : 0;
+  std::atomic<uint64_t> next{0};
+  auto work = [&]() {
+    std::vector<uint8_t> lb;
+    for (;;) {
+      const uint64_t p = next.fetch_add(1);
+      if (p >= np) return;
+      const uint64_t r0 = p * step, m = std::min(step, n_rows - r0);
+      const uint8_t* lv = nullptr;
+      if (list_nullable && h_list_validity) {
+        lb.assign((m + 7) / 8, 0);
+        for (uint64_t i = 0; i < m; i++)
+          if ((h_list_validity[(r0 + i) >> 3] >> ((r0 + i) & 7)) & 1) lb[i >> 3] |= (uint8_t)(1u << (i & 7));
+        lv = lb.data();
+      }
+      rcs[p] = sb::enc::encode_list_page(phys, h_offsets + r0, lv, m, list_nullable != 0, h_child, h_child_validity,
+                                         item_nullable != 0, o, sb::enc::page_seed(seed, p), pages[p], &levels[p]);
+    }
+  };
+  int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  nt = (int)std::min<uint64_t>((uint64_t)nt, std::max<uint64_t>(np, 1));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; t++) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  size_t total = 0;
+  for (uint64_t p = 0; p < np; p++) {
+    if (rcs[p]) return (sb_status)rcs[p];
+    total += pages[p].size();
+  }
+  uint8_t* buf = (uint8_t*)std::malloc(total ? total : 1);
+  sb_page_meta* metas = (sb_page_meta*)std::malloc((np ? np : 1) * sizeof(sb_page_meta));
+  if (!buf || !metas) { std::free(buf); std::free(metas); return SB_E_ARG; }
+  size_t at = 0;
+  for (uint64_t p = 0; p < np; p++) {
+    if (!pages[p].empty()) std::memcpy(buf + at, pages[p].data(), pages[p].size());
+    at += pages[p].size();
+    metas[p] = sb_page_meta{pages[p].size(), levels[p]};
+  }
+  *h_out = buf;
+  *out_len = total;
+  *h_metas = metas;
+  *n_pages = np;
+  return SB_OK;
+}
+
 // NativeWriter::finish (writer.rs:128-167): schema | meta | u32 schema_size |
 // u32 meta_size | FF FF FF FF 00 00 00 00; the body starts with
 // b"ARROW2" 00 00 (writer.rs:97-100).  Column chunks are given back to back.

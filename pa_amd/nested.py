@@ -1,0 +1,177 @@
+"""Nested List<primitive> columns (one list level over a primitive leaf).
+
+Reference (b41sh/pa @ 2025-01-17):
+  write_nested / write_nested_validity   src/write/serialize.rs:133-146, 217-232
+  read_validity_nested                   src/read/read_basic.rs:65-173
+  read_nested_integer / _double          src/read/array/integer.rs:240-261, double.rs
+  create_list                            src/read/array/list.rs:48
+  encode_chunk (paging by top-level rows) src/write/common.rs:49-119
+
+encode_list_column -> sb_encode_list_column (host encoder)
+ListColumnDecoder  -> sb_plan_list_column (device sizing) + sb_decode_list_planned
+batch_read_list    -> one ListArray per column: (offsets, list validity, values, leaf validity)
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .read import Context, PageMeta, default_context, physical_type, _as_device_bytes
+
+
+class ListDescC(ctypes.Structure):
+    _fields_ = [("physical_type", ctypes.c_int32), ("list_nullable", ctypes.c_int32),
+                ("item_nullable", ctypes.c_int32), ("offset_width", ctypes.c_int32)]
+
+
+class ListOutC(ctypes.Structure):
+    _fields_ = [("d_offsets", ctypes.c_void_p), ("d_list_validity", ctypes.c_void_p), ("d_values", ctypes.c_void_p),
+                ("d_leaf_validity", ctypes.c_void_p)]
+
+
+def _lib():
+    L = N.lib()
+    if not getattr(L, "_list_ready", False):
+        P, U64, I32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32
+        PU8 = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))
+        L.sb_encode_list_column.argtypes = [I32, P, P, I32, P, P, I32, U64, ctypes.POINTER(N.WriteOptionsC), U64, I32,
+                                            PU8, ctypes.POINTER(U64), ctypes.POINTER(ctypes.POINTER(N.PageMetaC)),
+                                            ctypes.POINTER(U64)]
+        L.sb_encode_list_column.restype = I32
+        L.sb_plan_list_column.argtypes = [P, ctypes.POINTER(ListDescC), P, U64, ctypes.POINTER(N.PageMetaC), U64,
+                                          ctypes.POINTER(ctypes.c_void_p)]
+        L.sb_plan_list_column.restype = I32
+        L.sb_plan_num_leaves.argtypes = [P]
+        L.sb_plan_num_leaves.restype = U64
+        L.sb_decode_list_planned.argtypes = [P, P, ctypes.POINTER(ListOutC)]
+        L.sb_decode_list_planned.restype = I32
+        L._list_ready = True
+    return L
+
+
+def encode_list_column(offsets: np.ndarray, child: np.ndarray, list_validity=None, child_validity=None,
+                       list_nullable: bool = False, item_nullable: bool = False, options=None,
+                       n_threads: int = 0) -> Tuple[bytes, List[PageMeta]]:
+    """encode_chunk for one List<T> leaf: pages of options.max_page_size
+    top-level rows; PageMeta.num_values = the page's level count."""
+    from .write import WriteOptions, _take
+
+    L = _lib()
+    options = options or WriteOptions()
+    offs = np.ascontiguousarray(offsets, np.int64)
+    child = np.ascontiguousarray(child)
+    if len(child) == 0:
+        child = np.zeros(1, child.dtype)
+    lvb = None if list_validity is None else np.packbits(np.asarray(list_validity, bool), bitorder="little")
+    cvb = None if child_validity is None else np.packbits(np.asarray(child_validity, bool), bitorder="little")
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_uint64()
+    metas = ctypes.POINTER(N.PageMetaC)()
+    npg = ctypes.c_uint64()
+    opts = options.c()
+    vp = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    st = L.sb_encode_list_column(physical_type(child.dtype), vp(offs), vp(lvb), int(list_nullable), vp(child), vp(cvb),
+                                 int(item_nullable), len(offs) - 1, ctypes.byref(opts), options.max_page_size or 0,
+                                 n_threads, ctypes.byref(out), ctypes.byref(olen), ctypes.byref(metas),
+                                 ctypes.byref(npg))
+    if st:
+        raise N.StrawboatError(st, "encode_list_column")
+    pm = [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
+    L.sb_free(metas)
+    return _take(out, olen.value), pm
+
+
+class ListColumnDecoder:
+    """A planned List<T> column chunk: rows and leaves are sized on the device
+    at plan time; decode() re-runs the sizing pass, the levels pass and the
+    values decode into caller- or self-allocated device buffers."""
+
+    def __init__(self, chunk, page_metas: Sequence[PageMeta], dtype, list_nullable: bool, item_nullable: bool,
+                 ctx: Optional[Context] = None, large: bool = False, timing: bool = False):
+        import torch
+
+        self._torch = torch
+        self.ctx = ctx or default_context()
+        self.dtype = np.dtype(dtype)
+        self.list_nullable, self.item_nullable = bool(list_nullable), bool(item_nullable)
+        self.offset_width = 8 if large else 4
+        self.chunk = _as_device_bytes(chunk, self.ctx.device)
+        self.metas = list(page_metas)
+        L = _lib()
+        metas = (N.PageMetaC * max(1, len(self.metas)))(*[N.PageMetaC(m.length, m.num_values) for m in self.metas])
+        desc = ListDescC(physical_type(self.dtype), int(self.list_nullable), int(self.item_nullable), self.offset_width)
+        h = ctypes.c_void_p()
+        st = L.sb_plan_list_column(self.ctx._h, ctypes.byref(desc), ctypes.c_void_p(self.chunk.data_ptr()),
+                                   self.chunk.numel(), metas, len(self.metas), ctypes.byref(h))
+        if st:
+            raise N.StrawboatError(st, self.ctx.error())
+        self._h = h
+        if timing:
+            L.sb_plan_enable_timing(h, 1)
+        self.num_rows = int(L.sb_plan_num_rows(h))
+        self.num_leaves = int(L.sb_plan_num_leaves(h))
+
+    def alloc_outputs(self):
+        torch = self._torch
+        dev = f"cuda:{self.ctx.device}"
+        odt = torch.int64 if self.offset_width == 8 else torch.int32
+        offsets = torch.empty(self.num_rows + 1, dtype=odt, device=dev)
+        tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[self.dtype.itemsize]
+        values = torch.empty(max(self.num_leaves, 1), dtype=tdt, device=dev)
+        bm = lambda n: torch.empty(max((n + 31) // 32, 1) * 4, dtype=torch.uint8, device=dev)  # noqa: E731
+        lv = bm(self.num_rows) if self.list_nullable else None
+        fv = bm(self.num_leaves) if self.item_nullable else None
+        return offsets, lv, values, fv
+
+    def decode_async(self, offsets=None, list_validity=None, values=None, leaf_validity=None):
+        if offsets is None:
+            offsets, list_validity, values, leaf_validity = self.alloc_outputs()
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        out = ListOutC(p(offsets), p(list_validity), p(values), p(leaf_validity))
+        st = _lib().sb_decode_list_planned(self.ctx._h, self._h, ctypes.byref(out))
+        if st:
+            raise N.StrawboatError(st, self.ctx.error())
+        return offsets, list_validity, values, leaf_validity
+
+    def check(self):
+        bad = ctypes.c_int64(-1)
+        st = N.lib().sb_plan_status(self.ctx._h, self._h, ctypes.byref(bad))
+        if st:
+            raise N.StrawboatError(st, self.ctx.error())
+
+    def decode(self, *bufs):
+        r = self.decode_async(*bufs)
+        self.check()
+        return r
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_float()
+        st = N.lib().sb_plan_last_kernel_ms(self.ctx._h, self._h, ctypes.byref(ms))
+        if st:
+            raise N.StrawboatError(st, self.ctx.error())
+        return ms.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().sb_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def batch_read_list(chunk, page_metas: Sequence[PageMeta], dtype, list_nullable: bool, item_nullable: bool,
+                    ctx: Optional[Context] = None, large: bool = False):
+    """batch_read_array for a List<T> leaf -> device tensors
+    (offsets, list validity bitmap|None, values, leaf validity bitmap|None)."""
+    dec = ListColumnDecoder(chunk, page_metas, dtype, list_nullable, item_nullable, ctx, large)
+    try:
+        return dec.decode()
+    finally:
+        dec.close()
