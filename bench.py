@@ -231,6 +231,53 @@ class WorkloadC3:
         return self.fdec + self.sdec
 
 
+class WorkloadC4:
+    """BASELINE.json configs[3]: List<Int32>, nullable lists (10 %) of
+    nullable items (20 %), lengths uniform in {0, 1, 2} (tests/it/io.rs:399-415
+    shape), items uniform in [0, 2^16), adaptive ratio 1.2, 8192-row pages.
+    A step = sizing pass + level decode (offsets, both bitmaps) + values."""
+
+    def __init__(self, torch, pa, rows, seed, device, threads):
+        rng = np.random.default_rng(seed)
+        self.rows = rows
+        lens = rng.integers(0, 3, rows)
+        lv = rng.random(rows) >= 0.1
+        lens[~lv] = 0
+        offs = np.zeros(rows + 1, np.int64)
+        np.cumsum(lens, out=offs[1:])
+        V = int(offs[-1])
+        child = rng.integers(0, 1 << 16, V).astype(np.int32)
+        cv = rng.random(V) >= 0.2
+        opts = pa.WriteOptions(default_compress_ratio=1.2, max_page_size=PAGE_ROWS, seed=seed)
+        self.chunk, self.metas = pa.encode_list_column(offs, child, lv, cv, True, True, opts, n_threads=threads)
+        self.mix = {}
+        dev = f"cuda:{device}"
+        h = torch.from_numpy(np.frombuffer(self.chunk, np.uint8).copy())
+        self.decs = [pa.ListColumnDecoder(h.to(dev), self.metas, np.int32, True, True) for _ in range(2)]
+        self.outs = [d.alloc_outputs() for d in self.decs]
+        self.leaves = V
+        self.in_bytes = len(self.chunk)
+        self.out_bytes = 4 * (rows + 1) + (rows + 7) // 8 + 4 * V + (V + 7) // 8
+        self.exp = (torch.from_numpy(offs.astype(np.int32)).to(dev), torch.from_numpy(np.packbits(lv, bitorder="little")).to(dev),
+                    torch.from_numpy(child).to(dev), torch.from_numpy(np.packbits(cv, bitorder="little")).to(dev),
+                    torch.from_numpy(cv).to(dev))
+        torch.cuda.synchronize()
+
+    def step(self, k):
+        self.decs[k & 1].decode_async(*self.outs[k & 1])
+
+    def verify(self, torch) -> bool:
+        ok = True
+        for d, (o, lv, v, fv) in zip(self.decs, self.outs):
+            d.check()
+            ok &= bool(torch.equal(o, self.exp[0]))
+            ok &= bool(torch.equal(lv[: self.exp[1].numel()], self.exp[1]))
+            ok &= bool(torch.equal(fv[: self.exp[3].numel()], self.exp[3]))
+            m = self.exp[4]
+            ok &= bool(torch.equal(v[: self.leaves][m], self.exp[2][m]))
+        return ok
+
+
 def load_traffic(workload: str):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -252,6 +299,8 @@ def main():
     ap.add_argument("--no-b12", action="store_true", help="skip the all-bitpack b=12 variant")
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 (Float64 + Utf8, LZ4) workload")
     ap.add_argument("--c3-rows", type=int, default=100_000_000)
+    ap.add_argument("--no-c4", action="store_true", help="skip the config-4 (List<Int32>) workload")
+    ap.add_argument("--c4-rows", type=int, default=50_000_000)
     args = ap.parse_args()
 
     import torch
@@ -313,6 +362,31 @@ def main():
             "kernels": "k_decode_staged<8,true> + k_decode_deferred<8,true> (LZ4) + k_bin_decode<4>",
         }
         del wl3
+
+    if not args.no_c4:
+        wl4 = WorkloadC4(torch, pa_amd, args.c4_rows, 99 + rank, local, threads)
+        steps4 = max(3, args.steps // 2)
+        w4, k4, ok4 = timed(torch, dist, wl4, steps4, args.warmup)
+        t4 = torch.tensor([w4], device=f"cuda:{local}", dtype=torch.float64)
+        if dist:
+            dist.all_reduce(t4, op=dist.ReduceOp.MAX)
+        k4avg = float(np.mean(k4))
+        a4 = (wl4.in_bytes + wl4.out_bytes) / (k4avg / 1e3) / 1e9
+        extra["c4_list_int32_nested"] = {
+            "rows_per_gpu": args.c4_rows,
+            "leaves_per_gpu": wl4.leaves,
+            "pages_per_gpu": len(wl4.metas),
+            "decoded_GBps": round(world * wl4.out_bytes * steps4 / float(t4[0]) / 1e9, 1),
+            "ms_per_step": round(float(t4[0]) / steps4 * 1e3, 3),
+            "step_traffic_GBps": round(a4, 1),
+            "roofline_frac": round(a4 / HBM_PEAK_GBPS, 4),
+            "compressed_bytes_per_gpu": wl4.in_bytes,
+            "decoded_bytes_per_gpu": wl4.out_bytes,
+            "bit_exact": bool(ok4),
+            "parallelism": f"page-shard x{world}",
+            "kernels": "k_list_size + k_list_scan + k_list_levels + k_decode_staged<4,false>",
+        }
+        del wl4
 
     if rank == 0:
         line = {

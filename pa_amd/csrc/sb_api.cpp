@@ -44,7 +44,8 @@ struct sb_plan {
   bool boolean = false;  // SB_T_BOOLEAN: values are a bitmap (k_bool_decode)
   bool list = false;     // List<primitive>: levels kernels + `inner` (the values streams as flat pages)
   sb_list_desc ldesc{};
-  uint64_t* d_lc = nullptr;  // [counts n | row bases n | leaf bases n | totals 2]
+  uint8_t* d_lc = nullptr;  // list state, see list_state_bytes
+  bool list_peek = false;   // sizes from the page headers (checked against the levels at plan time)
   sb_plan* inner = nullptr;
   uint64_t n_leaves = 0;
   int offset_width = 0;
@@ -405,13 +406,24 @@ sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
   return SB_OK;
 }
 
-static sb::ListLaunch list_launch(sb_plan* p, const sb_list_out* out) {
+// List state (u64 units): [counts n | block-local bases 2n | block totals
+// 2 nblk | totals 2 | level descriptors 4n]
+static uint64_t list_nblk(uint64_t n) { return (n + 255) / 256; }
+static size_t list_state_bytes(uint64_t n) { return (3 * n + 2 * list_nblk(n) + 2 + 4 * n) * sizeof(uint64_t); }
+static uint64_t* list_totals(sb_plan* p) { return (uint64_t*)p->d_lc + 3 * p->n_pages + 2 * list_nblk(p->n_pages); }
+
+static sb_status list_launch(sb_ctx* ctx, sb_plan* p, const sb_list_out* out, int stage, bool peek) {
   const uint64_t n = p->n_pages;
-  return sb::ListLaunch{p->d_chunk, p->d_pages, (uint32_t)n, (uint32_t)p->ldesc.list_nullable,
-                        (uint32_t)p->ldesc.item_nullable, (uint32_t)p->ldesc.offset_width, p->d_lc, p->d_lc + n,
-                        p->d_lc + 3 * n, p->inner->d_pages, out ? (uint8_t*)out->d_offsets : nullptr,
-                        out ? (uint32_t*)out->d_list_validity : nullptr, out ? (uint32_t*)out->d_leaf_validity : nullptr,
-                        p->d_status};
+  uint64_t* b = (uint64_t*)p->d_lc;
+  uint64_t* tot = list_totals(p);
+  sb::ListLaunch L{p->d_chunk, p->d_pages, (uint32_t)n, (uint32_t)p->ldesc.list_nullable,
+                   (uint32_t)p->ldesc.item_nullable, (uint32_t)p->ldesc.offset_width, (uint32_t)p->width,
+                   peek ? 1u : 0u, b, b + n, b + 3 * n, tot, tot + 2, p->inner->d_pages,
+                   out ? (uint8_t*)out->d_offsets : nullptr, out ? (uint32_t*)out->d_list_validity : nullptr,
+                   out ? (uint32_t*)out->d_leaf_validity : nullptr, p->d_status};
+  if (sb::launch_list(stage, L, ctx->stream))
+    return fail(ctx, SB_E_DEVICE, "list launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return SB_OK;
 }
 
 sb_status sb_plan_list_column(sb_ctx* ctx, const sb_list_desc* d, const uint8_t* d_chunk, uint64_t chunk_len,
@@ -437,34 +449,42 @@ sb_status sb_plan_list_column(sb_ctx* ctx, const sb_list_desc* d, const uint8_t*
   const size_t np = n_pages ? n_pages : 1;
   hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
   if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMalloc(&p->d_lc, (3 * np + 2) * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&p->d_lc, list_state_bytes(np));
   if (e == hipSuccess) e = hipEventCreate(&p->ev0);
   if (e == hipSuccess) e = hipEventCreate(&p->ev1);
   if (e == hipSuccess && n_pages)  // the level pages (inner's table becomes the values streams)
     e = hipMemcpyAsync(p->d_pages, inner->d_pages, n_pages * sizeof(sb::PageDesc), hipMemcpyDeviceToDevice, ctx->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(p->d_lc, 0, (3 * np + 2) * sizeof(uint64_t), ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(p->d_lc, 0, list_state_bytes(np), ctx->stream);
   if (e != hipSuccess) {
     sb_plan_destroy(p);
     return fail(ctx, SB_E_DEVICE, "list plan alloc: %s", hipGetErrorString(e));
   }
-  if (n_pages) {  // size once so the caller can allocate the outputs
-    sb::ListLaunch L = list_launch(p, nullptr);
-    if (sb::launch_list(0, L, ctx->stream) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+  if (n_pages) {  // exact sizing once, so the caller can allocate the outputs
+    if (list_launch(ctx, p, nullptr, 0, false) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "list sizing failed: %s", hipGetErrorString(hipGetLastError()));
     }
     std::vector<uint32_t> stv(n_pages);
-    uint64_t tot[2];
+    std::vector<uint64_t> exact(n_pages), peek(n_pages);
     (void)hipMemcpy(stv.data(), p->d_status, n_pages * 4, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(tot, p->d_lc + 3 * n_pages, sizeof tot, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(exact.data(), p->d_lc, n_pages * 8, hipMemcpyDeviceToHost);
     for (uint64_t i = 0; i < n_pages; i++) {
       if (stv[i]) {
         sb_plan_destroy(p);
         return fail(ctx, (sb_status)stv[i], "page %llu: %s", (unsigned long long)i, sb_status_str((int)stv[i]));
       }
+      p->n_rows += exact[i] >> 32;
+      p->n_leaves += exact[i] & 0xFFFFFFFFull;
     }
-    p->n_rows = tot[0];
-    p->n_leaves = tot[1];
+    // Do the page headers (rows, values usize) give the same counts?  Then
+    // decodes size from them instead of walking every level twice.
+    if (list_launch(ctx, p, nullptr, 1, true) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "list sizing failed: %s", hipGetErrorString(hipGetLastError()));
+    }
+    (void)hipMemcpy(peek.data(), p->d_lc, n_pages * 8, hipMemcpyDeviceToHost);
+    p->list_peek = peek == exact;
+    if (!p->list_peek) (void)hipMemcpy(p->d_lc, exact.data(), n_pages * 8, hipMemcpyHostToDevice);
   }
   *out = p;
   return SB_OK;
@@ -487,9 +507,10 @@ sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* p, const sb_list_out* out
   if (!p->n_pages) {
     HIP_TRY(ctx, hipMemsetAsync(out->d_offsets, 0, (size_t)p->ldesc.offset_width, ctx->stream));
   } else {
-    sb::ListLaunch L = list_launch(p, out);
-    if (sb::launch_list(0, L, ctx->stream) || sb::launch_list(1, L, ctx->stream))
-      return fail(ctx, SB_E_DEVICE, "list levels launch failed: %s", hipGetErrorString(hipGetLastError()));
+    sb_status lst = p->list_peek ? SB_OK : list_launch(ctx, p, out, 0, false);
+    if (!lst) lst = list_launch(ctx, p, out, 1, p->list_peek);
+    if (!lst) lst = list_launch(ctx, p, out, 2, p->list_peek);
+    if (lst) return lst;
     sb_primitive_out vo{out->d_values ? out->d_values : out->d_offsets, nullptr};  // (no leaves: nothing written)
     sb_status st = sb_decode_planned(ctx, p->inner, &vo);
     if (st) return st;

@@ -2083,8 +2083,8 @@ __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
 // through the flat decode kernels (k_decode_staged / global / deferred /
 // k_inflate) at their leaf bases.
 // ===========================================================================
-constexpr uint32_t kLvK = 8;                    // levels per thread per tile
-constexpr uint32_t kLvTile = NT * kLvK;         // levels per tile
+constexpr uint32_t kLvK = 32;                   // levels per thread per tile
+constexpr uint32_t kLvTile = NT * kLvK;         // 8192 levels per tile
 constexpr uint32_t kMaxRuns = 64;               // hybrid runs per level stream
 
 struct LvRuns {
@@ -2094,39 +2094,39 @@ struct LvRuns {
 };
 
 struct ListShared {
-  uint32_t rows, vpos, bw_def;
+  uint32_t rows, vpos, bw_def, region, fast;
   LvRuns rep, def;
-  uint32_t lbits[kLvTile / 32 + 4];  // tile list-validity bits (+ over-read pad)
-  uint32_t fbits[kLvTile / 32 + 4];  // tile leaf-validity bits
 };
 
+__device__ __forceinline__ void put_err(uint32_t* err, uint32_t code) { *err = max(*err, code); }
+
 // parquet2 HybridRleDecoder (hybrid_rle/decoder.rs) run headers of one level
-// stream [p, end) covering L levels, bit width bw.  Thread 0.
+// stream [p, end) covering L levels, bit width bw.  One lane.
 template <class Src>
-__device__ bool parse_runs(const Src& s, Shared& sh, uint32_t p, uint32_t end, uint32_t L, uint32_t bw, LvRuns& R) {
+__device__ bool parse_runs(const Src& s, uint32_t* err, uint32_t p, uint32_t end, uint32_t L, uint32_t bw, LvRuns& R) {
   uint32_t covered = 0, n = 0;
   while (covered < L) {
     uint32_t h = 0, sft = 0;
     for (;;) {  // ULEB128 header
-      if (p >= end || sft > 28) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      if (p >= end || sft > 28) { put_err(err, ST_OUT_OF_SPEC); return false; }
       const uint32_t c = s.u8(p++);
       h |= (c & 0x7Fu) << sft;
       if (!(c & 0x80)) break;
       sft += 7;
     }
-    if (n == kMaxRuns) { set_err(sh, ST_NYI); return false; }
+    if (n == kMaxRuns) { put_err(err, ST_NYI); return false; }
     R.start[n] = covered;
     if (h & 1) {  // bit-packed: h >> 1 groups of 8, clamped to the bytes present
       const uint64_t want = (uint64_t)(h >> 1) * bw;
       const uint32_t have = (uint32_t)min<uint64_t>(want, end - p);
       const uint32_t vals = (uint32_t)min<uint64_t>((uint64_t)(h >> 1) * 8, (uint64_t)have * 8 / bw);
-      if (vals == 0) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      if (vals == 0) { put_err(err, ST_OUT_OF_SPEC); return false; }
       R.arg[n] = 0x80000000u | p;
       p += have;
       covered += vals;
     } else {  // RLE: h >> 1 repeats of a ceil(bw / 8)-byte value
       const uint32_t vb = (bw + 7) / 8;
-      if (p + vb > end) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      if (p + vb > end) { put_err(err, ST_OUT_OF_SPEC); return false; }
       uint32_t v = 0;
       for (uint32_t k = 0; k < vb; k++) v |= s.u8(p + k) << (8 * k);
       R.arg[n] = v;
@@ -2162,198 +2162,450 @@ struct ListArgs {
   const PageDesc* pages;  // num_values = the page's level count (PageMeta.num_values)
   uint32_t n_pages;
   uint32_t nl, ni, ow;    // list nullable, item nullable, offset width
+  uint32_t width;         // leaf value width (the values header's usize / width = leaves)
+  uint32_t peek;          // sizes from the page headers (verified at plan time) instead of the levels
   uint64_t* counts;       // [n_pages] rows << 32 | leaves
-  uint64_t* bases;        // [2 * n_pages] row base, leaf base
+  uint64_t* local;        // [2 n_pages] row / leaf bases within the page's block of NT pages
+  uint64_t* blk;          // [2 ceil(n_pages / NT)] row / leaf totals of each block
   uint64_t* totals;       // [2] rows, leaves
-  PageDesc* vpages;       // values stream of each page, as a flat page
+  uint4* lvdesc;          // [2 n_pages] per page: the parse results the levels pass reuses
+  PageDesc* vpages;       // values stream of each page, as a flat page at its leaf base
   uint8_t* out_offsets;
   uint32_t* out_list_validity;
   uint32_t* out_leaf_validity;
   uint32_t* status;
-  uint32_t lds_bytes;
 };
 
-// Header + run tables (thread 0).  Levels region = [0, 12 + rep_len + def_len).
+// Header + run tables (one lane).
 template <class Src>
-__device__ bool list_parse(const Src& s, Shared& sh, ListShared& ls, const PageDesc& pd, const ListArgs& a) {
+__device__ bool list_parse(const Src& s, uint32_t* err, ListShared& ls, const PageDesc& pd, const ListArgs& a) {
   const uint32_t len = pd.byte_len, L = pd.num_values;
-  if (len < 12) { set_err(sh, ST_IO); return false; }
+  if (len < 12) { put_err(err, ST_IO); return false; }
   const uint32_t rows = s.u32(0), rl = s.u32(4), dl = s.u32(8);
-  if ((uint64_t)12 + rl + dl > len) { set_err(sh, ST_IO); return false; }
+  if ((uint64_t)12 + rl + dl > len) { put_err(err, ST_IO); return false; }
   const uint32_t max_def = a.nl + 1 + a.ni;
   ls.rows = rows;
   ls.vpos = 12 + rl + dl;
+  ls.region = 12 + rl + dl;
   ls.bw_def = 32 - __clz(max_def);
-  if (!parse_runs(s, sh, 12, 12 + rl, L, 1, ls.rep)) return false;
-  if (!parse_runs(s, sh, 12 + rl, 12 + rl + dl, L, ls.bw_def, ls.def)) return false;
-  if (L > 0 && rows == 0) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+  if (!parse_runs(s, err, 12, 12 + rl, L, 1, ls.rep)) return false;
+  if (!parse_runs(s, err, 12 + rl, 12 + rl + dl, L, ls.bw_def, ls.def)) return false;
+  if (L > 0 && rows == 0) { put_err(err, ST_OUT_OF_SPEC); return false; }
+  // the writer's shape: one bit-packed run per stream, def bit width <= 2
+  ls.fast = ls.rep.n == 1 && (ls.rep.arg[0] & 0x80000000u) && ls.def.n == 1 && (ls.def.arg[0] & 0x80000000u) &&
+            ls.bw_def <= 2;
   return true;
 }
 
-// Walks the page's levels tile by tile.  WRITE = false: *rows_out / *leaves_out
-// get the consumed counts.  WRITE = true: offsets and bitmaps at the bases.
+// Gathers the even bits of x (bit 2j -> bit j).
+__device__ __forceinline__ uint32_t compact_even(uint64_t x) {
+  x &= 0x5555555555555555ull;
+  x = (x | (x >> 1)) & 0x3333333333333333ull;
+  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+  return (uint32_t)x;
+}
+
+// little-endian bytes [p, p + nb) of the page, nb <= 8, never past `end`
+template <class Src>
+__device__ __forceinline__ uint64_t ld_bytes(const Src& s, uint32_t p, uint32_t nb, uint32_t end) {
+  if (p + 8 <= end) return s.u64(p) & (nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1));
+  uint64_t v = 0;
+  for (uint32_t k = 0; k < nb && p + k < end; k++) v |= (uint64_t)s.u8(p + k) << (8 * k);
+  return v;
+}
+
+// Level masks of 32 consecutive levels [i0, i0 + 32): rsm = row starts
+// (rep 0), lfm = leaves (def >= nl + 1), lvm = def > 0, fvm = def > nl + 1.
+struct LvMasks {
+  uint32_t vm, rsm, lfm, lvm, fvm;
+};
+
+template <class Src>
+__device__ __forceinline__ LvMasks level_masks(const Src& s, const ListShared& ls, uint32_t i0, uint32_t L,
+                                               uint32_t cs1) {
+  LvMasks m{0, 0, 0, 0, 0};
+  if (i0 >= L) return m;
+  m.vm = L - i0 >= 32 ? 0xFFFFFFFFu : ((1u << (L - i0)) - 1);
+  const uint32_t bw = ls.bw_def;
+  if (ls.fast) {  // direct bit slices of the single bit-packed runs
+    const uint32_t rp = ls.rep.arg[0] & 0x7FFFFFFFu, dp = ls.def.arg[0] & 0x7FFFFFFFu;
+    const uint32_t repw = (uint32_t)ld_bytes(s, rp + i0 / 8, 4, dp);  // the rep stream ends where def begins
+    m.rsm = ~repw & m.vm;
+    const uint64_t dw = ld_bytes(s, dp + i0 * bw / 8, 4 * bw, ls.region);
+    auto ge = [&](uint32_t t) -> uint32_t {
+      if (t == 0) return 0xFFFFFFFFu;
+      if (bw == 1) return t == 1 ? (uint32_t)dw : 0u;
+      const uint32_t lo = compact_even(dw), hi = compact_even(dw >> 1);
+      return t == 1 ? (lo | hi) : t == 2 ? hi : (hi & lo);
+    };
+    m.lfm = ge(cs1) & m.vm;
+    m.lvm = ge(1) & m.vm;
+    m.fvm = ge(cs1 + 1) & m.vm;
+    return m;
+  }
+  for (uint32_t k = 0; k < 32; k++) {
+    const uint32_t i = i0 + k;
+    if (i >= L) break;
+    const uint32_t r = level_at(s, ls.rep, i, 1), d = level_at(s, ls.def, i, bw);
+    if (r == 0) m.rsm |= 1u << k;
+    if (r <= 1 && d >= cs1) m.lfm |= 1u << k;
+    if (d > 0) m.lvm |= 1u << k;
+    if (d > cs1) m.fvm |= 1u << k;
+  }
+  return m;
+}
+
+// OR `nbits` (<= 32) bits of v into the LDS bitmap at bit position pos
+__device__ __forceinline__ void lds_or_bits(uint32_t* bm, uint32_t pos, uint64_t v, uint32_t nbits) {
+  if (!nbits || !v) return;
+  const uint32_t w = pos >> 5, sft = pos & 31;
+  const uint64_t lo = v << sft;
+  atomicOr(&bm[w], (uint32_t)lo);
+  if ((uint32_t)(lo >> 32)) atomicOr(&bm[w + 1], (uint32_t)(lo >> 32));
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// n bits of an LDS bitmap (bit 0 at word 0) to global bit position row_off,
+// one wave: whole words stored, edge words merged with atomicOr (zeroed bitmap).
+__device__ void wave_write_bits(const uint32_t* bm, uint32_t n, uint64_t row_off, uint32_t* out) {
+  if (n == 0) return;
+  const LdsSrc s{bm, 0};
+  const uint64_t fw = row_off >> 5, lw = (row_off + n - 1) >> 5;
+  for (uint64_t w = fw + (threadIdx.x & 63); w <= lw; w += 64) {
+    const int64_t pb = (int64_t)(w * 32) - (int64_t)row_off;
+    uint32_t v = pb >= 0 ? (uint32_t)(s.u64((uint32_t)(pb >> 3)) >> (pb & 7)) : s.u32(0) << (uint32_t)(-pb);
+    const uint32_t lo = pb < 0 ? (uint32_t)(-pb) : 0u;
+    const int64_t hi_ex = (int64_t)n - pb;
+    const uint32_t hi = hi_ex >= 32 ? 32u : (uint32_t)hi_ex;
+    const uint32_t m = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1)) & (0xFFFFFFFFu << lo);
+    if (m == 0xFFFFFFFFu) out[w] = v;
+    else if (v & m) atomicOr(&out[w], v & m);
+  }
+}
+
+// n bits of an LDS bitmap (bit 0 at word 0, zero past n, one spare zero word
+// before it at bm[-1]) to global bit position g0: the shift is uniform over
+// the wave, so output word i is a funnel of bm[i - 1] and bm[i]; interior
+// words are stored, the two edge words merged with atomicOr.
+__device__ __forceinline__ void wave_put_bits(const uint32_t* bm, uint32_t n, uint64_t g0, uint32_t* out) {
+  if (n == 0) return;
+  const uint32_t sh = (uint32_t)(g0 & 31), nw = (sh + n + 31) >> 5;
+  uint32_t* o = out + (g0 >> 5);
+  for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {
+    const uint32_t v = sh ? __builtin_amdgcn_alignbit(bm[i], bm[(int)i - 1], 32 - sh) : bm[i];
+    const bool edge = (i == 0 && sh) || (i == nw - 1 && ((sh + n) & 31));
+    if (edge) { if (v) atomicOr(&o[i], v); }
+    else o[i] = v;
+  }
+}
+
+constexpr uint32_t kLvStage = 4160;      // page bytes staged per wave (header + level streams)
+constexpr uint32_t kLvStep = 64 * kLvK;  // levels per wave step (2048)
+
+struct ListWave {
+  ListShared ls;
+  uint32_t err;
+  alignas(16) uint16_t obuf[kLvStep + 8];  // step-relative leaf offset of each row start, at row + (g0 & 3)
+  uint32_t lbits[kLvStep / 32 + 4];   // [0] = 0, then the list-validity bits of the step's rows
+  uint32_t fbits[kLvStep / 32 + 4];   // [0] = 0, then the leaf-validity bits of the step's leaves
+};
+
+// Page bytes: the staged prefix from LDS, the rest from HBM.
+struct StageSrc {
+  LdsSrc l;
+  GlbSrc g;
+  uint32_t lim;  // staged page bytes
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return i < lim ? l.u8(i) : g.u8(i); }
+  __device__ __forceinline__ uint32_t u32(uint32_t i) const { return i + 4 <= lim ? l.u32(i) : g.u32(i); }
+  __device__ __forceinline__ uint64_t u64(uint32_t i) const { return i + 8 <= lim ? l.u64(i) : g.u64(i); }
+};
+
+// Hacker's Delight 7-4 compress: the bits of x at the set positions of m,
+// packed to the low end (a branch-free pext).
+__device__ __forceinline__ uint32_t compress32(uint32_t x, uint32_t m) {
+  x &= m;
+  uint32_t mk = ~m << 1;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    uint32_t mp = mk ^ (mk << 1);
+    mp ^= mp << 2;
+    mp ^= mp << 4;
+    mp ^= mp << 8;
+    mp ^= mp << 16;
+    const uint32_t mv = mp & m;
+    m = (m ^ mv) | (mv >> (1 << i));
+    const uint32_t t = x & mv;
+    x = (x ^ t) | (t >> (1 << i));
+    mk &= ~mp;
+  }
+  return x;
+}
+
+// One wave walks its page's levels 2048 at a time.  WRITE = false: consumed
+// counts.  WRITE = true: offsets and bitmaps at (rbase, lbase).
 template <bool WRITE, class Src>
-__device__ void list_levels(const Src& s, Shared& sh, ListShared& ls, const PageDesc& pd, const ListArgs& a,
-                            uint64_t rbase, uint64_t lbase, uint32_t* rows_out, uint32_t* leaves_out) {
-  const uint32_t tid = threadIdx.x, L = pd.num_values, rows = ls.rows, bwd = ls.bw_def;
-  const uint32_t cs1 = a.nl + 1;
+__device__ void wave_levels(const Src& s, ListWave& w, const ListArgs& a, uint32_t L, uint64_t rbase, uint64_t lbase,
+                            uint32_t* rows_c, uint32_t* leaves_c) {
+  const uint32_t lane = threadIdx.x & 63, rows = w.ls.rows, cs1 = a.nl + 1;
   uint32_t carry_r = 0, carry_l = 0, my_leaves = 0;
-  for (uint32_t t0 = 0; t0 < L; t0 += kLvTile) {
-    uint32_t rsm = 0, lfm = 0, lvm = 0, fvm = 0;
-    const uint32_t i0 = t0 + tid * kLvK;
-#pragma unroll
-    for (uint32_t k = 0; k < kLvK; k++) {
-      const uint32_t i = i0 + k;
-      if (i < L) {
-        const uint32_t r = level_at(s, ls.rep, i, 1), d = level_at(s, ls.def, i, bwd);
-        if (r == 0) rsm |= 1u << k;
-        if (r <= 1 && d >= cs1) lfm |= 1u << k;
-        if (d > 0) lvm |= 1u << k;
-        if (d > cs1) fvm |= 1u << k;
+  for (uint32_t t0 = 0; t0 < L; t0 += kLvStep) {
+    const LvMasks m = level_masks(s, w.ls, t0 + lane * kLvK, L, cs1);
+    if (t0 == 0 && lane == 0 && !(m.rsm & 1)) put_err(&w.err, ST_OUT_OF_SPEC);  // level 0 starts no row
+    const uint32_t pk = ((uint32_t)__popc(m.rsm) << 16) | (uint32_t)__popc(m.lfm);
+    const uint32_t incl = wave_incl_scan(pk), tot = __builtin_amdgcn_readlane(incl, 63), ex = incl - pk;
+    const uint32_t rb = carry_r + (ex >> 16), lb = carry_l + (ex & 0xFFFFu);
+    // consumed: levels whose inclusive row count stays <= rows (read_basic.rs:158-162)
+    uint32_t cm = m.vm;
+    if (rb + __popc(m.rsm) > rows) {
+      if (rb >= rows + 1) cm = 0;
+      else {  // cut at the (rows - rb + 1)-th row start
+        uint32_t x = m.rsm;
+        for (uint32_t k = rows - rb; k; k--) x &= x - 1;
+        cm = (x & (0u - x)) - 1;
       }
     }
-    if (t0 == 0 && tid == 0 && L > 0 && !(rsm & 1)) set_err(sh, ST_OUT_OF_SPEC);  // level 0 starts no row
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan<uint64_t>(((uint64_t)__popc(rsm) << 32) | __popc(lfm), sh, &tot);
-    const uint32_t rb = carry_r + (uint32_t)(ex >> 32), lb = carry_l + (uint32_t)ex;
-    // consumed: levels whose inclusive row count stays <= rows (a suffix of the page is dropped)
-    uint32_t cm = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kLvK; k++)
-      if (rb + __popc(rsm & ((2u << k) - 1)) <= rows) cm |= 1u << k;
-    const uint32_t tile_r0 = carry_r, tile_l0 = carry_l;
-    const uint32_t tile_rows = min(carry_r + (uint32_t)(tot >> 32), rows) - min(carry_r, rows);
-    my_leaves += __popc(lfm & cm);
+    const uint32_t rsm = m.rsm & cm, lfm = m.lfm & cm;
+    my_leaves += __popc(lfm);
     if constexpr (WRITE) {
-      for (uint32_t w = tid; w < kLvTile / 32 + 4; w += NT) ls.lbits[w] = ls.fbits[w] = 0;
-      __syncthreads();
+      const uint32_t s_r0 = carry_r, s_l0 = carry_l;
+      const uint64_t g0 = rbase + s_r0, v0 = lbase + s_l0;
+      const uint32_t al = a.ow == 4 ? (uint32_t)(g0 & 3) : (uint32_t)(g0 & 1);  // obuf index of row 0
+      for (uint32_t i = lane; i < kLvStep / 32 + 4; i += 64) w.lbits[i] = w.fbits[i] = 0;
+      wave_sync();
+      const uint32_t nr = __popc(rsm), nf = __popc(lfm);
+      uint16_t* ob = w.obuf + al + (rb - s_r0);
+      const uint32_t lrel = lb - s_l0;
+      uint32_t j = 0;
+      for (uint32_t x = rsm; x; x &= x - 1, j++) ob[j] = (uint16_t)(lrel + __popc(m.lfm & ((x & (0u - x)) - 1)));
+      if (a.nl) lds_or_bits(w.lbits + 1, rb - s_r0, compress32(m.lvm, rsm), nr);
+      if (a.ni) lds_or_bits(w.fbits + 1, lrel, compress32(m.fvm, lfm), nf);
+      const uint32_t cpk = (nr << 16) | nf;
+      const uint32_t ctot = __builtin_amdgcn_readlane(wave_incl_scan(cpk), 63);
+      const uint32_t tr = ctot >> 16, tl = ctot & 0xFFFFu;
+      wave_sync();
+      if (a.ow == 4) {  // quads of rows on 16-byte boundaries: obuf[4q .. 4q + 3] -> o[4q - al ..]
+        uint32_t* o = (uint32_t*)a.out_offsets + (g0 - al);
+        const uint32_t v32 = (uint32_t)v0, nq = (al + tr + 3) >> 2;
+        for (uint32_t q = lane; q < nq; q += 64) {
+          const uint32_t* pr = (const uint32_t*)(w.obuf + 4 * q);
+          const uint32_t px = pr[0], py = pr[1];
+          const uint32_t e0 = v32 + (px & 0xFFFFu), e1 = v32 + (px >> 16), e2 = v32 + (py & 0xFFFFu), e3 = v32 + (py >> 16);
+          const uint32_t j0 = 4 * q;
+          if (j0 >= al && j0 + 4 <= al + tr) {
+            st_out((u32x4*)(o + j0), u32x4{e0, e1, e2, e3});
+          } else {
+            const uint32_t e[4] = {e0, e1, e2, e3};
 #pragma unroll
-      for (uint32_t k = 0; k < kLvK; k++) {
-        if (!((cm >> k) & 1)) continue;
-        const uint32_t below = (1u << k) - 1;
-        if ((rsm >> k) & 1) {
-          const uint32_t r = rb + __popc(rsm & below);  // page row of this row start
-          const uint64_t off = lbase + lb + __popc(lfm & below);
-          bin_put_off(a.out_offsets, rbase + r, off, a.ow);
-          if (a.nl && ((lvm >> k) & 1)) atomicOr(&ls.lbits[(r - tile_r0) >> 5], 1u << ((r - tile_r0) & 31));
+            for (uint32_t k = 0; k < 4; k++)
+              if (j0 + k >= al && j0 + k < al + tr) o[j0 + k] = e[k];
+          }
         }
-        if (a.ni && ((lfm & fvm) >> k & 1)) {
-          const uint32_t f = lb + __popc(lfm & below) - tile_l0;
-          atomicOr(&ls.fbits[f >> 5], 1u << (f & 31));
+      } else {
+        uint64_t* o = (uint64_t*)a.out_offsets + (g0 - al);
+        const uint32_t nq = (al + tr + 1) >> 1;
+        for (uint32_t q = lane; q < nq; q += 64) {
+          const uint32_t j0 = 2 * q;
+          const uint64_t x0 = v0 + w.obuf[j0], x1 = v0 + w.obuf[j0 + 1];
+          if (j0 >= al && j0 + 2 <= al + tr) {
+            st_out((u32x4*)(o + j0), u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)});
+          } else {
+            if (j0 >= al && j0 < al + tr) o[j0] = x0;
+            if (j0 + 1 >= al && j0 + 1 < al + tr) o[j0 + 1] = x1;
+          }
         }
       }
-      uint32_t tile_leaves = __popc(lfm & cm);
-      uint64_t tl;
-      block_excl_scan<uint64_t>(tile_leaves, sh, &tl);  // (syncs: the tile bits are complete)
-      const LdsSrc lsrc{(const uint32_t*)ls.lbits, 0}, fsrc{(const uint32_t*)ls.fbits, 0};
-      if (a.nl) write_validity(lsrc, 0, tile_rows, rbase + tile_r0, a.out_list_validity);
-      if (a.ni) write_validity(fsrc, 0, (uint32_t)tl, lbase + tile_l0, a.out_leaf_validity);
-      __syncthreads();
+      if (a.nl) wave_put_bits(w.lbits + 1, tr, g0, a.out_list_validity);
+      if (a.ni) wave_put_bits(w.fbits + 1, tl, v0, a.out_leaf_validity);
+      wave_sync();
     }
-    carry_r += (uint32_t)(tot >> 32);
-    carry_l += (uint32_t)tot;
+    carry_r += tot >> 16;
+    carry_l += tot & 0xFFFFu;
     if (carry_r > rows) break;  // uniform: every later level is past the last row
   }
-  uint64_t lt;
-  block_excl_scan<uint64_t>(my_leaves, sh, &lt);
-  if (tid == 0) {
-    const uint32_t rc = min(carry_r, rows);
-    if (rc != rows) set_err(sh, ST_OUT_OF_SPEC);  // levels ended before `rows` rows
-    *rows_out = rc;
-    *leaves_out = (uint32_t)lt;
-  }
+  const uint32_t lsum = (uint32_t)wave_sum64(my_leaves);
+  const uint32_t rc = min(carry_r, rows);
+  if (lane == 0 && rc != rows) put_err(&w.err, ST_OUT_OF_SPEC);  // levels ended before `rows` rows
+  *rows_c = rc;
+  *leaves_c = lsum;
 }
 
-template <bool WRITE>
-__device__ void list_page(const ListArgs& a, Shared& sh, ListShared& ls, uint32_t page, uint32_t* stage) {
-  const PageDesc pd = a.pages[page];
-  __shared__ uint32_t rows_c, leaves_c, region;
-  const uint32_t tid = threadIdx.x;
-  if (tid == 0) {
-    sh.err = 0;
-    GlbSrc g{a.chunk + pd.byte_off};
-    region = 0;
-    if (pd.byte_len >= 12) {
-      const uint64_t r = 12ull + g.u32(4) + g.u32(8);
-      region = (uint32_t)min<uint64_t>(r, pd.byte_len);
+// Per page setup of one wave: the page's first kLvStage bytes staged in LDS
+// in one round of loads (the header and, for the writer's pages, both level
+// streams), then the header parse -- or, on the levels pass of a fast page,
+// the descriptor the sizing pass left.  *staged: the level streams lie in
+// the staged prefix.  Returns false on a parse error.
+__device__ bool wave_page_setup(ListWave& w, uint32_t* stage, const ListArgs& a, uint32_t page, const PageDesc& pd, bool reuse,
+                                bool* staged, uint32_t* mis_out, uint32_t* lim_out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint8_t* pg = a.chunk + pd.byte_off;
+  const uintptr_t a0 = (uintptr_t)pg & ~(uintptr_t)3;
+  const uint32_t mis = (uint32_t)((uintptr_t)pg & 3);
+  const uint32_t lim = stage ? min(pd.byte_len, kLvStage) : 0u;
+  const uint32_t ndw = (mis + lim + 3) >> 2;
+  uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
+  if (reuse) {
+    d0 = a.lvdesc[2 * page];
+    d1 = a.lvdesc[2 * page + 1];
+  }
+  if (stage)
+    for (uint32_t d = lane; d < ndw; d += 64) stage[d] = __builtin_nontemporal_load((const uint32_t*)a0 + d);
+  if (lane == 0) w.err = 0;
+  wave_sync();
+  *mis_out = mis;
+  *lim_out = lim;
+  if (reuse && (d0.w & 1)) {  // fast page: one bit-packed run per stream
+    if (lane == 0) {
+      w.ls.rows = d0.x;
+      w.ls.vpos = d0.y;
+      w.ls.region = d0.y;
+      w.ls.bw_def = d0.w >> 1;
+      w.ls.fast = 1;
+      w.ls.rep.n = w.ls.def.n = 1;
+      w.ls.rep.start[0] = w.ls.def.start[0] = 0;
+      w.ls.rep.arg[0] = 0x80000000u | d0.z;
+      w.ls.def.arg[0] = 0x80000000u | d1.x;
     }
+  } else if (lane == 0) {
+    const StageSrc ss{LdsSrc{stage, mis}, GlbSrc{pg}, lim};
+    list_parse(ss, &w.err, w.ls, pd, a);
   }
-  __syncthreads();
-  uint64_t rbase = 0, lbase = 0;
-  if constexpr (WRITE) {
-    rbase = a.bases[page];
-    lbase = a.bases[a.n_pages + page];
-  }
-  const uint32_t need = (region + 15 + kStagePad + 15) & ~15u;
-  if (need <= a.lds_bytes) {  // levels staged in LDS
-    const uint32_t base = stage_page((u32x4*)stage, a.chunk + pd.byte_off, region);
-    LdsSrc s{stage, base};
-    if (tid == 0) list_parse(s, sh, ls, pd, a);
-    __syncthreads();
-    if (!sh.err) list_levels<WRITE>(s, sh, ls, pd, a, rbase, lbase, &rows_c, &leaves_c);
-  } else {
-    GlbSrc s{a.chunk + pd.byte_off};
-    if (tid == 0) list_parse(s, sh, ls, pd, a);
-    __syncthreads();
-    if (!sh.err) list_levels<WRITE>(s, sh, ls, pd, a, rbase, lbase, &rows_c, &leaves_c);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    if (!WRITE) {
-      const bool ok = sh.err == 0;
-      a.counts[page] = ok ? (((uint64_t)rows_c << 32) | leaves_c) : 0;
-      // the page's values stream, decoded as a flat non-nullable page of `leaves` values
-      a.vpages[page] = PageDesc{pd.byte_off + (ok ? ls.vpos : 0), 0, ok ? pd.byte_len - ls.vpos : 0,
-                                ok ? leaves_c : 0, 0};
-    }
-    if (sh.err) a.status[page] = sh.err;
-  }
-  __syncthreads();
+  wave_sync();
+  if (w.err) return false;
+  *staged = w.ls.region <= lim;
+  return true;
 }
 
+// Exact sizing pass: one wave per page (4 per workgroup) walks the levels:
+// consumed rows / leaves, and the parse results for the levels pass.
 __global__ __launch_bounds__(NT) void k_list_size(ListArgs a) {
-  extern __shared__ u32x4 lstage[];
-  __shared__ Shared sh;
-  __shared__ ListShared ls;
-  for (uint32_t page = blockIdx.x; page < a.n_pages; page += gridDim.x) {
-    if (threadIdx.x == 0) a.status[page] = 0;
-    list_page<false>(a, sh, ls, page, (uint32_t*)lstage);
-  }
-}
-
-__global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
-  extern __shared__ u32x4 lstage[];
-  __shared__ Shared sh;
-  __shared__ ListShared ls;
-  for (uint32_t page = blockIdx.x; page < a.n_pages; page += gridDim.x) {
-    if (a.status[page]) continue;  // (uniform) sizing errors stand
-    list_page<true>(a, sh, ls, page, (uint32_t*)lstage);
-  }
-}
-
-// Exclusive scans of the page row and leaf counts (one workgroup); the values
-// pages start at their leaf bases; the final list offset is the leaf total.
-__global__ __launch_bounds__(NT) void k_list_scan(ListArgs a) {
-  __shared__ Shared sh;
-  uint64_t cr = 0, cl = 0;
-  for (uint32_t p0 = 0; p0 < a.n_pages; p0 += NT) {
-    const uint32_t p = p0 + threadIdx.x;
-    const uint64_t c = p < a.n_pages ? a.counts[p] : 0;
-    uint64_t tr, tl;
-    const uint64_t er = block_excl_scan<uint64_t>(c >> 32, sh, &tr);
-    const uint64_t el = block_excl_scan<uint64_t>(c & 0xFFFFFFFFull, sh, &tl);
-    if (p < a.n_pages) {
-      a.bases[p] = cr + er;
-      a.bases[a.n_pages + p] = cl + el;
-      a.vpages[p].row_off = cl + el;
+  __shared__ ListWave waves[NW];
+  __shared__ uint32_t stages[NW][kLvStage / 4 + 16];  // the page's first bytes at byte `mis` (+ pad)
+  const uint32_t lane = threadIdx.x & 63;
+  ListWave& w = waves[threadIdx.x >> 6];
+  uint32_t* stage = stages[threadIdx.x >> 6];
+  for (uint32_t page = blockIdx.x * NW + (threadIdx.x >> 6); page < a.n_pages; page += gridDim.x * NW) {
+    const PageDesc pd = a.pages[page];
+    bool staged = false;
+    uint32_t mis = 0, lim = 0, rows_c = 0, leaves_c = 0;
+    if (wave_page_setup(w, stage, a, page, pd, false, &staged, &mis, &lim)) {
+      if (staged) wave_levels<false>(LdsSrc{stage, mis}, w, a, pd.num_values, 0, 0, &rows_c, &leaves_c);
+      else wave_levels<false>(GlbSrc{a.chunk + pd.byte_off}, w, a, pd.num_values, 0, 0, &rows_c, &leaves_c);
     }
-    cr += tr;
-    cl += tl;
+    wave_sync();
+    if (lane == 0) {
+      const bool ok = w.err == 0;
+      a.counts[page] = ok ? (((uint64_t)rows_c << 32) | leaves_c) : 0;
+      const uint32_t fast = ok && w.ls.fast;
+      a.lvdesc[2 * page] = make_uint4(w.ls.rows, w.ls.vpos, w.ls.rep.arg[0] & 0x7FFFFFFFu, fast | (w.ls.bw_def << 1));
+      a.lvdesc[2 * page + 1] = make_uint4(w.ls.def.arg[0] & 0x7FFFFFFFu, ok, 0, 0);
+      a.status[page] = w.err;
+    }
+    wave_sync();
+  }
+}
+
+// Block bases: one workgroup per NT pages, one thread per page.  a.peek:
+// the page's counts come straight from its headers -- rows from the nested
+// header (read_basic.rs:71, `additional`), leaves from the values stream's
+// usize = leaves * width (integer/mod.rs:62-63) -- two small reads per page
+// instead of a walk over its levels; the plan only takes this path after
+// checking it against the exact pass page by page.  Otherwise the counts of
+// k_list_size.  Writes each page's bases within its block and the block totals.
+__global__ __launch_bounds__(NT) void k_list_bscan(ListArgs a) {
+  __shared__ Shared sh;
+  const uint32_t p = blockIdx.x * NT + threadIdx.x;
+  uint64_t c = 0;
+  if (p < a.n_pages) {
+    if (a.peek) {
+      const PageDesc pd = a.pages[p];
+      const GlbSrc g{a.chunk + pd.byte_off};
+      if (pd.byte_len >= 12) {
+        const uint64_t vpos = 12ull + g.u32(4) + g.u32(8);
+        if (vpos + 9 <= pd.byte_len) c = ((uint64_t)g.u32(0) << 32) | (g.u32((uint32_t)vpos + 5) / a.width);
+      }
+      a.counts[p] = c;
+    } else {
+      c = a.counts[p];
+    }
+  }
+  uint64_t tr, tl;
+  const uint64_t er = block_excl_scan<uint64_t>(c >> 32, sh, &tr);
+  const uint64_t el = block_excl_scan<uint64_t>(c & 0xFFFFFFFFull, sh, &tl);
+  if (p < a.n_pages) {
+    a.local[2 * p] = er;
+    a.local[2 * p + 1] = el;
   }
   if (threadIdx.x == 0) {
-    a.totals[0] = cr;
-    a.totals[1] = cl;
-    if (a.out_offsets) bin_put_off(a.out_offsets, cr, cl, a.ow);
+    a.blk[2 * blockIdx.x] = tr;
+    a.blk[2 * blockIdx.x + 1] = tl;
+  }
+}
+
+// Levels pass: one wave per page.  Bases = the page's in-block bases + the
+// totals of the blocks before it (summed by the wave, 64 blocks per probe).
+// Writes offsets and both bitmaps, the page's values-stream descriptor, its
+// status; the last page also the totals and the final offset.
+__global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
+  __shared__ ListWave waves[NW];
+  __shared__ uint32_t stages[NW][kLvStage / 4 + 16];  // the page's first bytes at byte `mis` (+ pad)
+  const uint32_t lane = threadIdx.x & 63;
+  ListWave& w = waves[threadIdx.x >> 6];
+  uint32_t* stage = stages[threadIdx.x >> 6];
+  for (uint32_t page = blockIdx.x * NW + (threadIdx.x >> 6); page < a.n_pages; page += gridDim.x * NW) {
+    const PageDesc pd = a.pages[page];
+    const uint32_t nb = page / NT;
+    uint64_t br = 0, bl = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+      const uint32_t b = b0 + lane;
+      br += wave_sum64(b < nb ? a.blk[2 * b] : 0);
+      bl += wave_sum64(b < nb ? a.blk[2 * b + 1] : 0);
+    }
+    const uint64_t rbase = br + a.local[2 * page], lbase = bl + a.local[2 * page + 1];
+    const uint64_t cnt = a.counts[page];
+    bool staged = false;
+    uint32_t mis = 0, lim = 0, rows_c = 0, leaves_c = 0;
+    const bool sized = a.lvdesc[2 * page + 1].y != 0;  // the exact pass parsed this page
+    if (sized && wave_page_setup(w, stage, a, page, pd, true, &staged, &mis, &lim)) {
+      if (staged) wave_levels<true>(LdsSrc{stage, mis}, w, a, pd.num_values, rbase, lbase, &rows_c, &leaves_c);
+      else wave_levels<true>(GlbSrc{a.chunk + pd.byte_off}, w, a, pd.num_values, rbase, lbase, &rows_c, &leaves_c);
+    } else if (lane == 0) {
+      w.err = 0;
+      if (!sized) {  // re-parse for the status the reference would give
+        const StageSrc ss{LdsSrc{nullptr, 0}, GlbSrc{a.chunk + pd.byte_off}, 0};
+        list_parse(ss, &w.err, w.ls, pd, a);
+        if (!w.err) w.err = ST_OUT_OF_SPEC;
+      }
+    }
+    wave_sync();
+    if (lane == 0) {
+      uint32_t err = w.err;
+      if (!err && (rows_c != (uint32_t)(cnt >> 32) || leaves_c != (uint32_t)cnt)) err = ST_OUT_OF_SPEC;
+      const bool ok = err == 0;
+      // the page's values stream, decoded as a flat non-nullable page of `leaves` values
+      a.vpages[page] = PageDesc{pd.byte_off + (ok ? w.ls.vpos : 0), lbase, ok ? pd.byte_len - w.ls.vpos : 0,
+                                ok ? leaves_c : 0, 0};
+      a.status[page] = err;
+      if (page == a.n_pages - 1) {
+        const uint64_t tr = rbase + (cnt >> 32), tl = lbase + (uint32_t)cnt;
+        a.totals[0] = tr;
+        a.totals[1] = tl;
+        if (a.out_offsets) bin_put_off(a.out_offsets, tr, tl, a.ow);  // create_list appends values.len()
+      }
+    }
+    wave_sync();
   }
 }
 
@@ -2429,21 +2681,19 @@ int launch_bool(const LaunchArgs& a, void* stream) {
 
 namespace sb {
 int launch_list(int stage, const ListLaunch& L, void* stream) {
-  sbk::ListArgs a{L.chunk, L.pages, L.n_pages, L.list_nullable, L.item_nullable, L.offset_width, L.counts, L.bases,
-                  L.totals, L.vpages, L.out_offsets, L.out_list_validity, L.out_leaf_validity, L.status, kListLds};
+  sbk::ListArgs a{L.chunk, L.pages, L.n_pages, L.list_nullable, L.item_nullable, L.offset_width, L.width, L.peek,
+                  L.counts, L.local, L.blk, L.totals, (uint4*)L.lvdesc, L.vpages, L.out_offsets, L.out_list_validity,
+                  L.out_leaf_validity, L.status};
+  if (L.n_pages == 0) return 0;
+  const uint32_t grid = std::min<uint32_t>((L.n_pages + sbk::NW - 1) / sbk::NW, kListGrid);
+  const uint32_t nblk = (L.n_pages + sbk::NT - 1) / sbk::NT;
   hipStream_t st = (hipStream_t)stream;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)sbk::k_list_size, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kListLds);
-    hipFuncSetAttribute((const void*)sbk::k_list_levels, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kListLds);
-    attr = true;
-  }
-  const dim3 grid(std::min<uint32_t>(L.n_pages ? L.n_pages : 1, 65535u)), block(sbk::NT);
-  if (stage == 0) {
-    hipLaunchKernelGGL(sbk::k_list_size, grid, block, kListLds, st, a);
-    hipLaunchKernelGGL(sbk::k_list_scan, dim3(1), block, 0, st, a);
+  if (stage == 0) {  // exact sizing
+    hipLaunchKernelGGL(sbk::k_list_size, dim3(grid), dim3(sbk::NT), 0, st, a);
+  } else if (stage == 1) {  // block bases (+ header sizing when peek)
+    hipLaunchKernelGGL(sbk::k_list_bscan, dim3(nblk), dim3(sbk::NT), 0, st, a);
   } else {
-    hipLaunchKernelGGL(sbk::k_list_levels, grid, block, kListLds, st, a);
+    hipLaunchKernelGGL(sbk::k_list_levels, dim3(grid), dim3(sbk::NT), 0, st, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

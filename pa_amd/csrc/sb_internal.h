@@ -106,23 +106,27 @@ struct BinLaunch {
 };
 int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
 
-// List<primitive> columns: stage 0 = size pages + scan bases (+ the final
-// offset when out_offsets is set), stage 1 = offsets + bitmaps.
+// List<primitive> columns: stage 0 = exact sizing pass (one wave per page,
+// walks the levels); stage 1 = block bases (peek = 1: counts from the page
+// headers instead); stage 2 = offsets + bitmaps + values-stream descriptors.
 struct ListLaunch {
   const uint8_t* chunk;
   const PageDesc* pages;
   uint32_t n_pages;
   uint32_t list_nullable, item_nullable, offset_width;
+  uint32_t width, peek;
   uint64_t* counts;
-  uint64_t* bases;
+  uint64_t* local;
+  uint64_t* blk;
   uint64_t* totals;
+  void* lvdesc;  // 32 B per page
   PageDesc* vpages;
   uint8_t* out_offsets;
   uint32_t* out_list_validity;
   uint32_t* out_leaf_validity;
   uint32_t* status;
 };
-constexpr uint32_t kListLds = 32 * 1024;  // staged level streams (larger ones are read from HBM)
+constexpr uint32_t kListGrid = 2048;
 int launch_list(int stage, const ListLaunch& a, void* stream);
 
 }  // namespace sb
