@@ -193,7 +193,7 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     if ((rows & 31) || (m.num_values & 31)) needs_zero = true;
     if (is_bool) {  // page + its expanded bitmap, as k_bool_decode lays them out in LDS
       const uint64_t need = ((m.length + 15 + sb::kStagePad + 15) & ~15ull) + (((m.num_values + 7) / 8 + 15) & ~15ull) +
-                            sb::kStagePad;
+                            sb::kStagePad + sb::kZTablesBytes;  // (+ the Zstd decoder's tables)
       max_bool = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(max_bool, need), sb::kDeferredLds);
     }
     if (m.length + 16 <= sb::kStageMaxBytes) {

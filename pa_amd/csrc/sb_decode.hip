@@ -1144,6 +1144,8 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
   return ST_OK;
 }
 
+#include "sb_zstd.h"
+
 // One wave expands the general-codec stream [src, src + csize) of `olen`
 // bytes into LDS (FULL mode).  Returns a status code.
 __device__ uint32_t expand_to_lds(uint32_t codec, const uint8_t* src, uint32_t csize, lds_u8* out, uint32_t olen) {
@@ -1157,7 +1159,7 @@ __device__ uint32_t expand_to_lds(uint32_t codec, const uint8_t* src, uint32_t c
   const uint32_t p0 = (uint32_t)((uintptr_t)src & 3);
   if (codec == 1) return lz4_wave<false>(w, p0, p0 + csize, o);
   if (codec == 3) return snappy_wave<false>(w, p0, p0 + csize, o);
-  return ST_NYI;  // Zstd: host-only for now
+  return ST_NYI;  // Zstd reads its frame from LDS: zs::zstd_to_lds
 }
 
 // Patas (double/patas.rs:107-132): first value raw, then per value a u16
@@ -1310,7 +1312,8 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
       const bool idx_stream = sh.chain == CH_DICT || sh.chain == CH_FREQ_DICT || sh.chain == CH_DICT_FREQ;
       const uint32_t sw = idx_stream ? 4u : (uint32_t)W;
       const uint64_t bytes = (uint64_t)lf.n * sw;
-      if (bytes > xcap) {
+      const uint64_t zt = (bytes + 15) & ~15ull;  // Zstd: its tables after the expanded stream
+      if ((lf.codec == 2 ? zt + kZTablesBytes : bytes) > xcap) {
         if (tid == 0) set_err(sh, ST_NYI);  // decompressed stream larger than the LDS budget
       } else if (tid < 64) {
         const lds_u8* in = (const lds_u8*)((const uint8_t*)s.w + s.base + lf.body);
@@ -1321,7 +1324,10 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
         else if (lf.codec == 16) {
           if (!FLT || idx_stream) st = ST_OUT_OF_SPEC;  // Patas only in decompress_double
           else st = patas_expand<W>(in, lf.csize, xo, lf.n);
-        } else st = ST_NYI;  // Zstd: host-only for now
+        } else {
+          st = zs::zstd_to_lds(LdsSrc{s.w, s.base + lf.body}, lf.csize, xo, (uint32_t)bytes, xo + zt,
+                               (uint32_t)(xcap - zt));
+        }
         if (st) set_err(sh, st);
       }
       __syncthreads();
@@ -1591,6 +1597,7 @@ struct BinInfo {
   uint32_t k;          // Dict entries / Freq exceptions consumed (positions < n)
   uint32_t tab;        // LDS byte offset of the (pos, len) entry table
   uint32_t xoff, yoff; // LDS byte offsets of the X (offsets / indices) and Y (values) regions
+  uint32_t ztab;       // Zstd: LDS byte offset of the decoder's tables
 };
 
 // Thread 0: parse validity prefix + binary header; walk Dict entries / Freq
@@ -1622,7 +1629,11 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     const uint32_t xb = ((n + 1) * OW + 15) & ~15u;
     bi.yoff = bi.xoff + xb;
     bi.tab = bi.yoff;
-    if (bi.codec == 2) { set_err(sh, ST_NYI); return false; }  // Zstd: host-only for now
+    if (bi.codec == 2) {  // Zstd: offsets into X, values into Y, the decoder's tables after Y
+      const uint64_t zt = ((uint64_t)bi.yoff + bi.S + 15) & ~15ull;
+      if (zt + kZTablesBytes + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
+      bi.ztab = (uint32_t)zt;
+    }
     return true;
   }
   if (bi.codec == BIN_ONE) {
@@ -1638,14 +1649,18 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     Stream ix;
     if (!parse_stream(s, body, end, n, &ix)) { set_err(sh, ST_IO); return false; }
     if (ix.codec == 11) { set_err(sh, ST_OUT_OF_SPEC); return false; }
-    if (ix.codec == 2) { set_err(sh, ST_NYI); return false; }  // Zstd index stream: host-only for now
     *idx = ix;
     uint32_t q = ix.body + ix.csize;
     if (q + 4 > end) { set_err(sh, ST_IO); return false; }
     const uint32_t k = s.u32(q);
     q += 4;
     bi.tab = bi.xoff + ((n * 4 + 15) & ~15u);  // X = indices
-    if (bi.tab + 8 * (uint64_t)k + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
+    bi.ztab = (uint32_t)((bi.tab + 8 * (uint64_t)k + 15) & ~15ull);  // a Zstd index stream's tables
+    if (bi.tab + 8 * (uint64_t)k + kStagePad > lds_bytes ||
+        (ix.codec == 2 && (uint64_t)bi.ztab + kZTablesBytes + kStagePad > lds_bytes)) {
+      set_err(sh, ST_NYI);
+      return false;
+    }
     tab = (uint2*)(lds + bi.tab);
     for (uint32_t e = 0; e < k; e++) {  // u64 len + bytes per entry
       if (q + 8 > end) { set_err(sh, ST_IO); return false; }
@@ -1727,11 +1742,14 @@ __device__ void copy_lds_to_global(const uint8_t* lds, uint32_t src, uint8_t* ds
 // Materializes a binary Dict's u32 index stream (n values) into LDS xi: leaf
 // codecs via run_leaf, LZ4 / Snappy expanded straight into xi, Freq (top +
 // roaring-placed exceptions of a leaf stream) filled then scattered.
-__device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, uint32_t* xi, const uint8_t* gpage) {
+__device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, uint32_t* xi, const uint8_t* gpage,
+                                uint8_t* ztab, uint32_t ztcap) {
   const uint32_t tid = threadIdx.x, n = ix.n;
-  if (ix.codec == 1 || ix.codec == 3) {
+  if (ix.codec == 1 || ix.codec == 2 || ix.codec == 3) {
     if (tid < 64) {
-      const uint32_t st = expand_to_lds(ix.codec, gpage + ix.body, ix.csize, (lds_u8*)xi, 4 * n);
+      const uint32_t st =
+          ix.codec == 2 ? zs::zstd_to_lds(LdsSrc{s.w, s.base + ix.body}, ix.csize, (lds_u8*)xi, 4 * n, (lds_u8*)ztab, ztcap)
+                        : expand_to_lds(ix.codec, gpage + ix.body, ix.csize, (lds_u8*)xi, 4 * n);
       if (st) set_err(sh, st);
     }
     __syncthreads();
@@ -1796,7 +1814,7 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
       const uint2* tab = (const uint2*)(lds + bi.tab);
       const uint32_t k = bi.k;
       uint32_t* xi = (uint32_t*)(lds + bi.xoff);
-      materialize_idx(s, sh, idx, xi, a.chunk + pd.byte_off);
+      materialize_idx(s, sh, idx, xi, a.chunk + pd.byte_off, lds + bi.ztab, a.lds_bytes - bi.ztab - kStagePad);
       uint64_t part = 0;
       for (uint32_t i = threadIdx.x; i < pd.num_values; i += NT) {
         if (xi[i] < k) part += tab[xi[i]].y;
@@ -1892,7 +1910,28 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
     if (!sh.err) {
       if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
       if (R == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);
-      if (bi.codec <= 3) {
+      if (bi.codec == 2) {  // Zstd: wave 0 decodes both streams into LDS; they then read as a None page
+        if (tid < 64) {
+          const uint32_t tcap = a.lds_bytes - bi.ztab - kStagePad;
+          uint32_t r = zs::zstd_to_lds(LdsSrc{s.w, s.base + bi.ob}, bi.ocs, (lds_u8*)(lds + bi.xoff), (n + 1) * OW,
+                                       (lds_u8*)(lds + bi.ztab), tcap);
+          if (!r)
+            r = zs::zstd_to_lds(LdsSrc{s.w, s.base + bi.vb}, bi.vcs, (lds_u8*)(lds + bi.yoff), (uint32_t)bi.S,
+                                (lds_u8*)(lds + bi.ztab), tcap);
+          if (r) set_err(sh, r);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          bi.ob = bi.xoff - base;
+          bi.ocs = (n + 1) * OW;
+          bi.vb = bi.yoff - base;
+          bi.vcs = (uint32_t)bi.S;
+          bi.codec = 0;
+        }
+        __syncthreads();
+      }
+      if (sh.err) {
+      } else if (bi.codec <= 3) {
         // offsets: rows 1..n at V + p[i] (mod.rs:136-144 rebase); p[0] must be
         // 0 and p[n] the values length (the writer rebases, mod.rs:45-55)
         if (bi.codec != 0) {
@@ -1925,7 +1964,7 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
         for (uint64_t j = tid; j < (uint64_t)n * L; j += NT) a.out_values[V + j] = lds[top + (uint32_t)(j % L)];
       } else if (bi.codec == BIN_DICT) {
         uint32_t* xi = (uint32_t*)(lds + bi.xoff);
-        materialize_idx(s, sh, idx, xi, a.chunk + pd.byte_off);
+        materialize_idx(s, sh, idx, xi, a.chunk + pd.byte_off, lds + bi.ztab, a.lds_bytes - bi.ztab - kStagePad);
         const uint2* tab = (const uint2*)(lds + bi.tab);
         const uint32_t k = bi.k;
         if (!sh.err)
@@ -2057,8 +2096,18 @@ __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
           if (!sh.err) write_validity(xs, 0, n, pd.row_off, (uint32_t*)a.out_values);
           break;
         }
-        case 2:
-          if (tid == 0) set_err(sh, ST_NYI);  // Zstd: not on device yet
+        case 2:  // Zstd over the bitmap bytes: wave 0 decodes into LDS, its tables after the bitmap
+          if (need + xb + kZTablesBytes + kStagePad > a.stage_bytes) {
+            if (tid == 0) set_err(sh, ST_NYI);
+            break;
+          }
+          if (tid < 64) {
+            const uint32_t r = zs::zstd_to_lds(LdsSrc{s.w, s.base + st.body}, st.csize, (lds_u8*)xbits, (n + 7) / 8,
+                                               (lds_u8*)xbits + xb, a.stage_bytes - need - xb - kStagePad);
+            if (r) set_err(sh, r);
+          }
+          __syncthreads();
+          if (!sh.err) write_validity(xs, 0, n, pd.row_off, (uint32_t*)a.out_values);
           break;
         default:
           if (tid == 0) set_err(sh, ST_OUT_OF_SPEC);  // Compression::from_codec / from_compression

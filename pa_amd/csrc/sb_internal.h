@@ -83,7 +83,10 @@ int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a,
 int launch_bool(const LaunchArgs& a, void* stream);
 
 // dynamic LDS of the deferred pass: page + expanded stream
-constexpr uint32_t kDeferredLds = 150 * 1024;
+constexpr uint32_t kDeferredLds = 155 * 1024;  // + <= 4 KiB of static LDS = the 160 KiB limit
+// LDS table area of the one-wave Zstd decoder (sb_zstd.h), carved after the
+// expanded stream: the minimum, and enough for a 12-bit Huffman table
+constexpr uint32_t kZTablesBytes = 18 * 1024, kZTablesMax = 22 * 1024;
 constexpr uint32_t kDeferredGrid = 1024;
 
 // Binary / Utf8 columns: stage 0 = size pages + scan bases, stage 1 = decode.

@@ -70,6 +70,8 @@ OPTS = {
     "dict": dict(ratio=2.0, forced=O.DICT),
     "dict_snappy": dict(ratio=2.0, forced=O.DICT, default_codec=O.SNAPPY),
     "freq": dict(ratio=2.0, forced=O.FREQ),
+    "zstd": dict(default_codec=O.ZSTD),
+    "dict_zstd": dict(ratio=2.0, forced=O.DICT, default_codec=O.ZSTD),
 }
 
 

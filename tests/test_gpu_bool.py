@@ -65,6 +65,7 @@ OPTS = {
     "adaptive": dict(ratio=1.2),
     "lz4": dict(default_codec=O.LZ4),
     "snappy": dict(default_codec=O.SNAPPY),
+    "zstd": dict(default_codec=O.ZSTD),
     "rle": dict(forced=O.RLE),
 }
 

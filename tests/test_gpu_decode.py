@@ -63,6 +63,8 @@ OPTS = {
     "lz4_adaptive": dict(ratio=1.2, default_codec=O.LZ4),
     "snappy": dict(ratio=None, default_codec=O.SNAPPY),
     "snappy_dict": dict(ratio=2.0, default_codec=O.SNAPPY, forced=O.DICT),
+    "zstd": dict(ratio=None, default_codec=O.ZSTD),
+    "zstd_adaptive": dict(ratio=1.2, default_codec=O.ZSTD),
 }
 
 INT_TYPES = [np.int32, np.uint32, np.int64, np.uint64, np.int8, np.uint8, np.int16, np.uint16]
@@ -87,7 +89,7 @@ def test_int_columns(ctx, dtype, opt, nullable):
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64], ids=lambda d: np.dtype(d).name)
 @pytest.mark.parametrize("opt", ["plain", "adaptive12", "adaptive20", "force_freq", "force_dict", "force_rle",
-                                 "lz4", "lz4_adaptive", "snappy"])
+                                 "lz4", "lz4_adaptive", "snappy", "zstd"])
 @pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
 def test_float_columns(ctx, dtype, opt, nullable):
     rng = np.random.default_rng(7)
@@ -221,15 +223,3 @@ def test_lz4_compressible_and_long_matches(ctx):
         for dc in (O.LZ4, O.SNAPPY):
             check(ctx, v, None, False, 8192, O.WriteOptions.make(default_codec=dc))
             check(ctx, v, rng.random(len(v)) > 0.5, True, 2048, O.WriteOptions.make(default_codec=dc))
-
-
-def test_zstd_pages_report_nyi(ctx):
-    """Zstd is not on the device yet: its pages report NotYetImplemented
-    (never a wrong answer)."""
-    import pa_amd
-
-    v = np.arange(5000, dtype=np.int32)
-    chunk, metas, _ = build_column(v, None, False, 2048, O.WriteOptions.make(default_codec=O.ZSTD))
-    with pytest.raises(pa_amd.StrawboatError) as e:
-        gpu_decode(ctx, chunk, metas, np.int32, False)
-    assert e.value.status == 2

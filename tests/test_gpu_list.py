@@ -67,6 +67,7 @@ OPTS = {
     "adaptive": dict(ratio=1.2),
     "adaptive2": dict(ratio=2.0),
     "lz4": dict(default_codec=O.LZ4),
+    "zstd": dict(default_codec=O.ZSTD),
     "rle": dict(ratio=2.0, forced=O.RLE),
     "dict": dict(ratio=2.0, forced=O.DICT),
 }
