@@ -5,10 +5,10 @@ Workload (BASELINE.json configs[1]): a non-nullable
 Int32 column of 100M rows in 8192-row pages, written by the engine's writer
 with the reference's adaptive codec choice at default_compress_ratio 1.2
 (write/common.rs:49-119, compression/integer/mod.rs:231-308).  Page data
-is shaped so the adaptive choice lands on the two codecs the config names:
-80 % of pages uniform in [0, 2^b) with b cycling 12..24 (-> Bitpacking),
-20 % runs of length 2-3 of random 31-bit values (-> RLE).  The codec of
-every page is read back and reported.
+is shaped as SURVEY.md §8(d) specifies, so the adaptive choice lands on the
+two codecs the config names: 80 % of pages uniform in [0, 2^b) with b
+cycling 1..24 (-> Bitpacking), 20 % runs of 64-512 copies of random values
+in [0, 2^31) (-> RLE).  The codec of every page is read back and reported.
 
 A "step" = one batched decode of the whole column (compressed pages resident
 in HBM -> Arrow values buffer in HBM).  value = decoded bytes of all ranks /
@@ -16,8 +16,10 @@ max-over-ranks wall time of the timed steps.  Weak scaling: each rank owns a
 100M-row shard (its own page queue, no collectives on the data path).
 
 Also reported: the all-Bitpacking b=12 variant (the north star's >=60 %
-roofline target), the roofline of the decode kernel from HIP events on the
-launch stream, and the CPU restatement (oracle, 1 thread) on the same column.
+roofline target), a harder C2 mix (b 12..24, RLE runs of 2-3), configs 3-5
+(Float64 + Utf8 under LZ4; List<Int32>; the 64-column mixed table), the
+roofline of the decode kernel from HIP events on the launch stream, and the
+CPU restatement (oracle, 1 thread) on the same column.
 """
 from __future__ import annotations
 
@@ -39,19 +41,28 @@ PAGE_ROWS = 8192
 
 
 def gen_c2(rows: int, seed: int, variant: str) -> np.ndarray:
+    """variant "mix": SURVEY.md §8(d) C2 (b cycling 1..24 on 4 of 5 pages,
+    RLE runs of 64-512 on the fifth); "hard": b cycling 12..24 and RLE runs
+    of 2-3 (more input bytes and 8x the runs); "b12": every page 12-bit."""
     rng = np.random.default_rng(seed)
     v = np.empty(rows, np.int32)
     npg = (rows + PAGE_ROWS - 1) // PAGE_ROWS
+    nbp = 0
     for p in range(npg):
         n = min(PAGE_ROWS, rows - p * PAGE_ROWS)
         s = slice(p * PAGE_ROWS, p * PAGE_ROWS + n)
         if variant == "b12":
             v[s] = rng.integers(0, 1 << 12, n)
         elif p % 5 == 4:
-            lens = rng.choice(np.array([2, 3]), size=n // 2 + 2, p=[0.3, 0.7])
+            if variant == "hard":
+                lens = rng.choice(np.array([2, 3]), size=n // 2 + 2, p=[0.3, 0.7])
+            else:
+                lens = rng.integers(64, 513, n // 64 + 2)
             v[s] = np.repeat(rng.integers(0, 2**31, len(lens)), lens)[:n]
         else:
-            v[s] = rng.integers(0, 1 << (12 + (p * 7) % 13), n)
+            b = 12 + (p * 7) % 13 if variant == "hard" else 1 + nbp % 24
+            nbp += 1
+            v[s] = rng.integers(0, 1 << b, n)
     return v
 
 
@@ -105,6 +116,8 @@ class Workload:
 
 def timed(torch, dist, wl: Workload, steps: int, warmup: int):
     for k in range(warmup):
+        wl.step(k)
+    for k in range(warmup, 2):  # (untimed) every rotating buffer decoded once before the check
         wl.step(k)
     torch.cuda.synchronize()
     ok = wl.verify(torch)
@@ -278,6 +291,164 @@ class WorkloadC4:
         return ok
 
 
+def page_codecs(chunk: bytes, metas, nullable: bool) -> dict:
+    """Codec byte of every page's (first) value stream, after the validity prefix."""
+    mix, pos = {}, 0
+    for m in metas:
+        q = pos + (4 + int.from_bytes(chunk[pos:pos + 4], "little") if nullable else 0)
+        c = chunk[q] if q < pos + m.length else -1
+        mix[c] = mix.get(c, 0) + 1
+        pos += m.length
+    return mix
+
+
+class WorkloadC5:
+    """BASELINE.json configs[4]: a 64-column table of
+    `rows` rows -- 16 Int32, 16 Int64, 8 Float64, 8 Utf8, 8 Boolean, 8 UInt32
+    -- in 8192-row pages at default_compress_ratio 2.0 (tests/it/io.rs:433),
+    each column shaped for a codec of the adaptive cascade (the LZ4 / None
+    columns written with that default codec and no ratio); every fourth
+    fixed-width or Boolean column nullable (10 % nulls).  Encoding is the
+    engine's host C++ writer on the host threads (timed and reported; it is
+    not on the GPU).  A step decodes all 64 columns back to back on one
+    stream; each column is checked against its source values."""
+
+    I32 = ["bp4", "bp8", "bp12", "bp16", "bp20", "runs", "runs", "one", "one", "freq", "freq", "dict", "dict",
+           "sorted", "sorted", "sorted"]
+    I64 = ["runs"] * 4 + ["dict"] * 4 + ["freq"] * 4 + ["none"] * 4
+    F64 = ["slow", "slow", "dict", "dict", "runs", "runs", "lz4", "lz4"]
+    STR = ["dict", "dict", "freq", "freq", "one", "one", "lz4", "lz4"]
+    BOOL = ["runs", "runs", "runs", "one", "one", "none", "none", "none"]
+    U32 = ["bp6", "bp10", "bp14", "bp18", "sorted", "sorted", "sorted", "sorted"]
+
+    @staticmethod
+    def _values(dt, kind, n, rng):
+        if kind.startswith("bp"):
+            return rng.integers(0, 1 << int(kind[2:]), n).astype(dt)
+        if kind == "runs":
+            if dt == np.bool_:
+                return np.repeat(rng.random(n // 1000 + 1) > 0.5, 1000)[:n]
+            return np.repeat(rng.integers(0, 2**31, n // 200 + 1), 200)[:n].astype(dt)
+        if kind == "one":
+            return np.ones(n, dt) if dt == np.bool_ else np.full(n, 7, dt)
+        if kind == "freq":
+            return np.where(rng.random(n) < 0.95, 300, rng.integers(0, 10**6, n)).astype(dt)
+        if kind == "dict":
+            pool = rng.integers(0, 2**31, 500)
+            v = pool[rng.integers(0, 500, n)]
+            return (v.astype(np.float64) / 7.0).astype(dt) if dt == np.float64 else v.astype(dt)
+        if kind == "sorted":
+            return np.cumsum(rng.integers(0, 100, n)).astype(dt)
+        if kind == "slow":  # slowly varying with repeats (Patas / RLE friendly)
+            return (1000.0 + np.cumsum(rng.integers(-1, 2, n)) * 0.5).astype(dt)
+        if dt == np.bool_:  # "none"
+            return rng.random(n) > 0.5
+        if dt == np.float64:  # "lz4"
+            return np.round(rng.standard_normal(n) * 1e4, 2)
+        return rng.integers(-2**62, 2**62, n).astype(dt)  # "none": incompressible
+
+    @staticmethod
+    def _strings(kind, n, rng):
+        if kind == "dict":
+            pool = [f"category-{i:04d}".encode() for i in range(200)]
+            s = [pool[i] for i in rng.integers(0, 200, n)]
+        elif kind == "freq":
+            s = [b"common-value" if r < 0.95 else str(x).encode() for r, x in zip(rng.random(n), rng.integers(0, 10**6, n))]
+        elif kind == "one":
+            s = [b"constant"] * n
+        else:
+            return decimal_strings(rng.integers(0, 10**6, n))
+        offs = np.zeros(n + 1, np.int64)
+        np.cumsum([len(x) for x in s], out=offs[1:])
+        return b"".join(s), offs
+
+    def __init__(self, torch, pa, rows, seed, device, threads):
+        rng = np.random.default_rng(seed)
+        self.rows = rows
+        dev = f"cuda:{device}"
+        specs = ([(np.int32, k) for k in self.I32] + [(np.int64, k) for k in self.I64] +
+                 [(np.float64, k) for k in self.F64] + [("utf8", k) for k in self.STR] +
+                 [(np.bool_, k) for k in self.BOOL] + [(np.uint32, k) for k in self.U32])
+        self.cols = []
+        self.encode_s = 0.0
+        self.in_bytes = self.out_bytes = self.raw_bytes = 0
+        self.mix = {}
+        names = {0: "none", 1: "lz4", 2: "zstd", 3: "snappy", 10: "rle", 11: "dict", 12: "one_value", 13: "freq",
+                 14: "bitpacking", 15: "delta_bitpacking", 16: "patas"}
+        nb = (rows + 7) // 8
+        for ci, (dt, kind) in enumerate(specs):
+            nullable = dt != "utf8" and ci % 4 == 3
+            valid = (rng.random(rows) >= 0.1) if nullable else None
+            basic = kind in ("lz4", "none")
+            opts = pa.WriteOptions(default_compression=1 if kind == "lz4" else 0,
+                                   default_compress_ratio=None if basic else 2.0, max_page_size=PAGE_ROWS, seed=seed + ci)
+            if dt == "utf8":
+                svals, soffs = self._strings(kind, rows, rng)
+                t0 = time.perf_counter()
+                chunk, metas = pa.encode_binary_column(svals, soffs, None, False, opts, physical_type=pa.UTF8,
+                                                       n_threads=threads)
+                self.encode_s += time.perf_counter() - t0
+                h = torch.from_numpy(np.frombuffer(chunk, np.uint8).copy()).to(dev)
+                dec = pa.BinaryColumnDecoder(h, metas, pa.UTF8, False)
+                raw = len(svals) + 4 * (rows + 1)
+                exp = (torch.from_numpy(soffs.astype(np.int32)).to(dev),
+                       torch.from_numpy(np.frombuffer(svals, np.uint8).copy()).to(dev))
+            else:
+                v = self._values(dt, kind, rows, rng)
+                t0 = time.perf_counter()
+                chunk, metas = pa.encode_column(v, valid, nullable, opts, n_threads=threads)
+                self.encode_s += time.perf_counter() - t0
+                h = torch.from_numpy(np.frombuffer(chunk, np.uint8).copy()).to(dev)
+                dec = pa.ColumnDecoder(h, metas, dt, nullable)
+                raw = nb if dt == np.bool_ else v.nbytes
+                if dt == np.bool_:
+                    ev = torch.from_numpy(v).to(dev)
+                else:
+                    ev = torch.from_numpy(v.view(np.uint8).copy()).to(dev)
+                exp = (ev, None if valid is None else torch.from_numpy(valid).to(dev))
+            for c, k in page_codecs(chunk, metas, nullable).items():
+                self.mix[names.get(c, str(c))] = self.mix.get(names.get(c, str(c)), 0) + k
+            self.raw_bytes += raw
+            self.out_bytes += raw + (nb if nullable else 0)
+            self.in_bytes += len(chunk)
+            self.cols.append((dt, dec, dec.alloc_outputs(), exp))
+        torch.cuda.synchronize()
+
+    @property
+    def decs(self):
+        return [c[1] for c in self.cols]
+
+    def step(self, k):
+        for _, dec, outs, _ in self.cols:
+            dec.decode_async(*outs)
+
+    def verify(self, torch) -> bool:
+        ok = True
+        n = self.rows
+        for dt, dec, outs, exp in self.cols:
+            dec.check()
+            if dt == "utf8":
+                o, v, _ = outs
+                ok &= bool(torch.equal(o, exp[0])) and bool(torch.equal(v[: exp[1].numel()], exp[1]))
+                continue
+            vals, bm = outs
+            ev, valid = exp
+            if dt == np.bool_:
+                bits = ((vals[: (n + 7) // 8].unsqueeze(1) >> torch.arange(8, device=vals.device, dtype=torch.uint8)) & 1)
+                got = bits.reshape(-1)[:n].bool()
+            else:
+                got = vals.view(torch.uint8)[: ev.numel()]
+                if valid is not None:  # compare the valid rows only (values under nulls are the writer's choice)
+                    w = np.dtype(dt).itemsize
+                    got, ev = got.view(-1, w)[valid], ev.view(-1, w)[valid]
+                ok &= bool(torch.equal(got, ev))
+                continue
+            if valid is not None:
+                got, ev = got[valid], ev[valid]
+            ok &= bool(torch.equal(got, ev))
+        return ok
+
+
 def load_traffic(workload: str):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -297,10 +468,13 @@ def main():
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-b12", action="store_true", help="skip the all-bitpack b=12 variant")
+    ap.add_argument("--no-hard", action="store_true", help="skip the harder C2 mix (b 12..24, RLE runs of 2-3)")
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 (Float64 + Utf8, LZ4) workload")
     ap.add_argument("--c3-rows", type=int, default=100_000_000)
     ap.add_argument("--no-c4", action="store_true", help="skip the config-4 (List<Int32>) workload")
     ap.add_argument("--c4-rows", type=int, default=50_000_000)
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 (64-column mixed table) workload")
+    ap.add_argument("--c5-rows", type=int, default=8_388_608)
     args = ap.parse_args()
 
     import torch
@@ -331,6 +505,22 @@ def main():
     value = world * wl.out_bytes * args.steps / wall_max / 1e9
 
     extra = {}
+    if not args.no_hard:
+        wlh = Workload(torch, pa_amd, args.rows, 4343 + rank, "hard", local, threads)
+        wh, kh, okh = timed(torch, dist, wlh, args.steps, args.warmup)
+        khavg = float(np.mean(kh))
+        ah = (wlh.in_bytes + wlh.out_bytes) / (khavg / 1e3) / 1e9
+        extra["c2_hard_mix"] = {
+            "decoded_GBps": round(wlh.out_bytes * args.steps / wh / 1e9, 1),
+            "kernel_ms": round(khavg, 4),
+            "kernel_traffic_GBps": round(ah, 1),
+            "roofline_frac": round(ah / HBM_PEAK_GBPS, 4),
+            "codec_mix": wlh.mix,
+            "compressed_bytes": wlh.in_bytes,
+            "traffic": load_traffic("c2_hard_mix"),
+            "bit_exact": bool(okh),
+        }
+        del wlh
     if not args.no_b12:
         wl12 = Workload(torch, pa_amd, args.rows, 4242 + rank, "b12", local, threads)
         w12, k12, ok12 = timed(torch, dist, wl12, args.steps, args.warmup)
@@ -387,6 +577,31 @@ def main():
             "kernels": "k_list_size + k_list_scan + k_list_levels + k_decode_staged<4,false>",
         }
         del wl4
+
+    if not args.no_c5:
+        wl5 = WorkloadC5(torch, pa_amd, args.c5_rows, 555 + rank, local, threads)
+        steps5 = max(3, args.steps // 4)
+        w5, k5, ok5 = timed(torch, dist, wl5, steps5, args.warmup)
+        t5 = torch.tensor([w5], device=f"cuda:{local}", dtype=torch.float64)
+        if dist:
+            dist.all_reduce(t5, op=dist.ReduceOp.MAX)
+        k5avg = float(np.mean(k5))
+        extra["c5_mixed_64col"] = {
+            "rows_per_gpu": args.c5_rows,
+            "columns": len(wl5.cols),
+            "decoded_GBps": round(world * wl5.out_bytes * steps5 / float(t5[0]) / 1e9, 1),
+            "ms_per_step": round(float(t5[0]) / steps5 * 1e3, 3),
+            "step_traffic_GBps": round((wl5.in_bytes + wl5.out_bytes) / (k5avg / 1e3) / 1e9, 1),
+            "roofline_frac": round((wl5.in_bytes + wl5.out_bytes) / (k5avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "compressed_bytes_per_gpu": wl5.in_bytes,
+            "decoded_bytes_per_gpu": wl5.out_bytes,
+            "codec_mix_pages": wl5.mix,
+            "encode_host_GBps": round(wl5.raw_bytes / wl5.encode_s / 1e9, 2),
+            "encode": f"host C++ writer, {threads} threads (the GPU encode path is not built yet)",
+            "bit_exact": bool(ok5),
+            "parallelism": f"page-shard x{world} (each rank its own table)",
+        }
+        del wl5
 
     if rank == 0:
         line = {

@@ -290,12 +290,19 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   if (!p->n_pages) return SB_OK;
   if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
   const size_t np = p->n_pages;
+  // Every decode sizes its pages again (values bytes -> bases, and the list of
+  // LZ4 / Snappy streams): the plan-time pass only sized the caller's buffers.
+  HIP_TRY(ctx, hipMemsetAsync(p->d_defer + 2, 0, sizeof(uint32_t), ctx->stream));
+  sb::BinLaunch S{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
+                  nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr};
+  if (sb::launch_binary(0, p->offset_width, S, ctx->stream))
+    return fail(ctx, SB_E_DEVICE, "binary sizing launch failed: %s", hipGetErrorString(hipGetLastError()));
   sb::BinLaunch L{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
                   (uint8_t*)out->d_offsets, out->d_values, out->values_capacity, (uint32_t*)out->d_validity,
                   p->d_status, p->d_jobs, nullptr, p->d_scratch};
   if (p->n_bin_jobs) {  // Basic LZ4 / Snappy pages: streams expanded first, one wave each
-    sb::InflateLaunch I{p->d_chunk, p->d_jobs, nullptr, p->n_bin_jobs, out->d_values, p->d_scratch, p->d_bin + np,
-                        p->d_status};
+    sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2, p->n_bin_jobs, out->d_values, p->d_scratch,
+                        p->d_bin + np, p->d_status};
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
