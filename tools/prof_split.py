@@ -1,8 +1,8 @@
 """Per-workload kernel durations from a rocprofv3 kernel trace of bench.py.
 
-bench.py launches the decode kernel for the C2 mix (warmup + steps) and then
-for the b12 variant (warmup + steps); both use k_decode_staged<4,false>, so
-the --stats summary averages the two.  This splits the trace by dispatch
+bench.py launches the decode kernel for the C2 headline mix, the harder C2
+mix and the b12 variant (warmup + steps each, in that order); all use
+k_decode_staged<4,false>, so the --stats summary averages them.  This splits the trace by dispatch
 order and reports the timed launches of each workload.
 
 usage: python tools/prof_split.py <kernel_trace.csv> <warmup> <steps> [out.json]
@@ -19,7 +19,7 @@ def main():
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     per = warm + steps
     out = {}
-    for i, name in enumerate(["c2_int32_adaptive_bitpack_rle", "bitpack_b12"]):
+    for i, name in enumerate(["c2_int32_adaptive_bitpack_rle", "c2_hard_mix", "bitpack_b12"]):
         seg = dur[i * per:(i + 1) * per][warm:]
         if seg:
             out[name] = {"kernel": rows[0]["Kernel_Name"], "timed_dispatches": len(seg),
