@@ -189,6 +189,33 @@ def decimal_strings(vals: np.ndarray):
     return out.tobytes(), offs
 
 
+class StreamSet:
+    """Independent columns decode concurrently (the reference decodes columns
+    independently too, read/deserialize.rs:237-253): each column's context
+    launches on one of `n` side streams, forked from and joined back into the
+    current stream every step, so the HIP events of timed() span all of them."""
+
+    def __init__(self, torch, pa, device, n):
+        self.torch = torch
+        self.streams = [torch.cuda.Stream(device=device) for _ in range(n)]
+        self.ctxs = []
+        for st in self.streams:
+            c = pa.Context(device)
+            c.use_stream(st)
+            self.ctxs.append(c)
+        torch.cuda.synchronize()
+
+    def fork(self):
+        cur = self.torch.cuda.current_stream()
+        for st in self.streams:
+            st.wait_stream(cur)
+
+    def join(self):
+        cur = self.torch.cuda.current_stream()
+        for st in self.streams:
+            cur.wait_stream(st)
+
+
 class WorkloadC3:
     """BASELINE.json configs[2]: nullable Float64 + nullable Utf8, LZ4 pages,
     ratio None (always the general codec), 10 % nulls, 8192-row pages.
@@ -208,8 +235,11 @@ class WorkloadC3:
         dev = f"cuda:{device}"
         fh = torch.from_numpy(np.frombuffer(self.fchunk, np.uint8).copy())
         sh = torch.from_numpy(np.frombuffer(self.schunk, np.uint8).copy())
-        self.fdec = [pa.ColumnDecoder(fh.to(dev), self.fmetas, np.float64, True) for _ in range(2)]
-        self.sdec = [pa.BinaryColumnDecoder(sh.to(dev), self.smetas, pa.UTF8, True) for _ in range(2)]
+        self.ss = StreamSet(torch, pa, device, 2)  # Float64 and Utf8 columns on their own streams
+        fd, sd = [fh.to(dev) for _ in range(2)], [sh.to(dev) for _ in range(2)]
+        torch.cuda.synchronize()
+        self.fdec = [pa.ColumnDecoder(fd[i], self.fmetas, np.float64, True, ctx=self.ss.ctxs[0]) for i in range(2)]
+        self.sdec = [pa.BinaryColumnDecoder(sd[i], self.smetas, pa.UTF8, True, ctx=self.ss.ctxs[1]) for i in range(2)]
         self.fout = [d.alloc_outputs() for d in self.fdec]
         self.sout = [d.alloc_outputs() for d in self.sdec]
         self.in_bytes = len(self.fchunk) + len(self.schunk)
@@ -221,8 +251,10 @@ class WorkloadC3:
         torch.cuda.synchronize()
 
     def step(self, k):
+        self.ss.fork()
         self.fdec[k & 1].decode_async(*self.fout[k & 1])
         self.sdec[k & 1].decode_async(*self.sout[k & 1])
+        self.ss.join()
 
     def verify(self, torch) -> bool:
         ok = True
@@ -376,6 +408,10 @@ class WorkloadC5:
         names = {0: "none", 1: "lz4", 2: "zstd", 3: "snappy", 10: "rle", 11: "dict", 12: "one_value", 13: "freq",
                  14: "bitpacking", 15: "delta_bitpacking", 16: "patas"}
         nb = (rows + 7) // 8
+        # columns spread over 4 streams (GPU_MAX_HW_QUEUES), the LZ4 ones first so each gets its own
+        self.ss = StreamSet(torch, pa, device, 4)
+        order = sorted(range(len(specs)), key=lambda i: specs[i][1] != "lz4")
+        home = {ci: self.ss.ctxs[j % 4] for j, ci in enumerate(order)}
         for ci, (dt, kind) in enumerate(specs):
             nullable = dt != "utf8" and ci % 4 == 3
             valid = (rng.random(rows) >= 0.1) if nullable else None
@@ -389,7 +425,8 @@ class WorkloadC5:
                                                        n_threads=threads)
                 self.encode_s += time.perf_counter() - t0
                 h = torch.from_numpy(np.frombuffer(chunk, np.uint8).copy()).to(dev)
-                dec = pa.BinaryColumnDecoder(h, metas, pa.UTF8, False)
+                torch.cuda.synchronize()
+                dec = pa.BinaryColumnDecoder(h, metas, pa.UTF8, False, ctx=home[ci])
                 raw = len(svals) + 4 * (rows + 1)
                 exp = (torch.from_numpy(soffs.astype(np.int32)).to(dev),
                        torch.from_numpy(np.frombuffer(svals, np.uint8).copy()).to(dev))
@@ -399,7 +436,8 @@ class WorkloadC5:
                 chunk, metas = pa.encode_column(v, valid, nullable, opts, n_threads=threads)
                 self.encode_s += time.perf_counter() - t0
                 h = torch.from_numpy(np.frombuffer(chunk, np.uint8).copy()).to(dev)
-                dec = pa.ColumnDecoder(h, metas, dt, nullable)
+                torch.cuda.synchronize()
+                dec = pa.ColumnDecoder(h, metas, dt, nullable, ctx=home[ci])
                 raw = nb if dt == np.bool_ else v.nbytes
                 if dt == np.bool_:
                     ev = torch.from_numpy(v).to(dev)
@@ -419,8 +457,10 @@ class WorkloadC5:
         return [c[1] for c in self.cols]
 
     def step(self, k):
+        self.ss.fork()
         for _, dec, outs, _ in self.cols:
             dec.decode_async(*outs)
+        self.ss.join()
 
     def verify(self, torch) -> bool:
         ok = True

@@ -1584,6 +1584,7 @@ struct BinArgs {
   InflateJob* jobs;
   uint32_t* job_count;
   uint8_t* scratch;
+  uint32_t* lds_need;
 };
 
 enum : uint32_t { BIN_BASIC = 0, BIN_ONE = 12, BIN_DICT = 11, BIN_FREQ = 13 };
@@ -1688,9 +1689,14 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     uint32_t tot;
     if (!parse_roaring(s, sh, q, bm, &tot)) return false;
     q += bm;
-    // exceptions at rows < n are consumed in row order (freq.rs:127-141)
-    uint32_t ep = 0;
-    while (ep < tot && roaring_select(s, sh, ep) < n) ep++;
+    // exceptions at rows < n are consumed in row order (freq.rs:127-141);
+    // select is increasing: binary search for the first row >= n
+    uint32_t ep = 0, hi_e = tot;
+    while (ep < hi_e) {
+      const uint32_t mid = (ep + hi_e) / 2;
+      if (roaring_select(s, sh, mid) < n) ep = mid + 1;
+      else hi_e = mid;
+    }
     bi.tab = bi.xoff + ((((n + 31) / 32) * 8 + 15) & ~15u);  // X = row bitmap + prefix
     if (bi.tab + 8 * (uint64_t)ep + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
     tab = (uint2*)(lds + bi.tab);
@@ -1810,6 +1816,12 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
       a.jobs[slot + 1] = InflateJob{pd.byte_off + bi.vb, kDstBinBase | page, bi.vcs, (uint32_t)bi.S, bi.codec, page};
     }
     __syncthreads();
+    if (a.lds_need && threadIdx.x == 0 && !sh.err) {  // plan time: the LDS this page needs
+      uint32_t need = stage_end + 64;
+      if (bi.codec == 2 || (bi.codec == BIN_DICT && idx.codec == 2)) need = kDeferredLds;  // Zstd tables take the rest
+      else if (bi.codec == BIN_DICT || bi.codec == BIN_FREQ) need = max(need, bi.tab + 8 * bi.k + kStagePad);
+      atomicMax(a.lds_need, need);
+    }
     if (!sh.err && bi.codec == BIN_DICT) {
       const uint2* tab = (const uint2*)(lds + bi.tab);
       const uint32_t k = bi.k;
@@ -2680,11 +2692,13 @@ int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a,
 
 namespace sb {
 int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream) {
+  const uint32_t lds = L.lds_bytes ? std::min(L.lds_bytes, kDeferredLds) : kDeferredLds;
   sbk::BinArgs a{L.chunk, L.pages, L.n_pages, L.nullable, L.sizes, L.bases, L.total, L.out_offsets, L.out_values,
-                 L.values_cap, L.out_validity, L.status, kDeferredLds, L.jobs, L.job_count, L.scratch};
+                 L.values_cap, L.out_validity, L.status, lds, L.jobs, L.job_count, L.scratch, L.lds_need};
   hipStream_t st = (hipStream_t)stream;
   const dim3 block(sbk::NT);
-  const dim3 grid(std::min<uint32_t>(L.n_pages ? L.n_pages : 1, kDeferredGrid));
+  // one workgroup per page (grid-stride past 64 Ki pages): as many resident per CU as the LDS budget allows
+  const dim3 grid(std::min<uint32_t>(L.n_pages ? L.n_pages : 1, 65535u));
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)sbk::k_bin_size<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
@@ -2694,12 +2708,12 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
     attr = true;
   }
   if (stage == 0) {
-    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_size<8>, grid, block, kDeferredLds, st, a);
-    else hipLaunchKernelGGL(sbk::k_bin_size<4>, grid, block, kDeferredLds, st, a);
+    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_size<8>, grid, block, lds, st, a);
+    else hipLaunchKernelGGL(sbk::k_bin_size<4>, grid, block, lds, st, a);
     hipLaunchKernelGGL(sbk::k_bin_scan, dim3(1), block, 0, st, a);
   } else {
-    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, kDeferredLds, st, a);
-    else hipLaunchKernelGGL(sbk::k_bin_decode<4>, grid, block, kDeferredLds, st, a);
+    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, lds, st, a);
+    else hipLaunchKernelGGL(sbk::k_bin_decode<4>, grid, block, lds, st, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

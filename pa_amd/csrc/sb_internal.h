@@ -106,6 +106,8 @@ struct BinLaunch {
   InflateJob* jobs;       // sizing pass out: Basic LZ4 / Snappy streams (2 per page)
   uint32_t* job_count;
   uint8_t* scratch;       // expanded offsets streams, (row_off + page) * offset width
+  uint32_t lds_bytes;     // dynamic LDS per workgroup (0 = kDeferredLds)
+  uint32_t* lds_need;     // sizing pass at plan time: max LDS bytes any page needs
 };
 int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
 
