@@ -264,6 +264,21 @@ sb_status sb_encode_list_column(int32_t physical_type, const int64_t* h_offsets,
                                 uint64_t max_page_rows, int32_t n_threads, uint8_t** h_out, uint64_t* out_len,
                                 sb_page_meta** h_metas, uint64_t* n_pages);
 uint64_t sb_page_seed(uint64_t seed, uint64_t page);
+/* encode_chunk on the device (HIP, gfx950) for the options whose codec choice
+ * needs no trial compression: default_compress_ratio None (has_ratio = 0),
+ * default codec None, forced codec none or Bitpacking.  Pages of Int32 /
+ * UInt32 take Bitpacking when forced and eligible (all values >= 0, length a
+ * multiple of 128: bp.rs:92-100), every other page Compression::None --
+ * byte-identical to sb_encode_column with the same options.  d_values /
+ * d_validity (column LSB bitmap) / d_out are device memory; d_out holds at
+ * least sb_encode_device_bound() bytes; page p is rows [p*P, (p+1)*P), P =
+ * max_page_rows <= 16384 and a multiple of 128 unless it covers every row.
+ * Synchronizes the context's stream.  Other options: SB_E_NYI. */
+uint64_t sb_encode_device_bound(int32_t physical_type, uint64_t n_rows, int32_t nullable, uint64_t max_page_rows);
+sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type, const void* d_values, const uint8_t* d_validity,
+                                  uint64_t n_rows, int32_t nullable, const sb_write_options* opts,
+                                  uint64_t max_page_rows, uint8_t* d_out, uint64_t out_capacity, uint64_t* out_len,
+                                  sb_page_meta* h_metas, uint64_t metas_cap, uint64_t* n_pages);
 /* NativeWriter::finish (write/writer.rs:128-167) footer bytes. */
 sb_status sb_write_footer(const uint8_t* h_schema, uint64_t schema_len, const uint64_t* h_col_offsets,
                           const uint64_t* h_col_npages, uint64_t n_cols, const sb_page_meta* h_pages,

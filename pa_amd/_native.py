@@ -27,6 +27,7 @@ EXPORTED = [
     "sb_decompress_values", "sb_read_meta", "sb_encode_page", "sb_encode_column", "sb_page_seed",
     "sb_write_footer", "sb_free", "sb_encode_binary_column", "sb_plan_values_bytes", "sb_decode_binary_planned",
     "sb_encode_list_column", "sb_plan_list_column", "sb_plan_num_leaves", "sb_decode_list_planned",
+    "sb_encode_device_bound", "sb_encode_column_device",
 ]
 
 
@@ -123,6 +124,11 @@ def lib():
     L.sb_encode_column.argtypes = [I32, P, P, U64, I32, ctypes.POINTER(WriteOptionsC), U64, I32, PU8,
                                    ctypes.POINTER(U64), ctypes.POINTER(ctypes.POINTER(PageMetaC)), ctypes.POINTER(U64)]
     L.sb_encode_column.restype = I32
+    L.sb_encode_device_bound.argtypes = [I32, U64, I32, U64]
+    L.sb_encode_device_bound.restype = U64
+    L.sb_encode_column_device.argtypes = [P, I32, P, P, U64, I32, ctypes.POINTER(WriteOptionsC), U64, P, U64,
+                                          ctypes.POINTER(U64), ctypes.POINTER(PageMetaC), U64, ctypes.POINTER(U64)]
+    L.sb_encode_column_device.restype = I32
     L.sb_page_seed.argtypes = [U64, U64]
     L.sb_page_seed.restype = U64
     L.sb_write_footer.argtypes = [P, U64, P, P, U64, P, PU8, ctypes.POINTER(U64)]

@@ -84,6 +84,51 @@ def encode_column(values: np.ndarray, validity=None, nullable: bool = False,
     return _take(out, olen.value), pm
 
 
+def encode_column_device(values, validity=None, nullable: bool = False, options: Optional[WriteOptions] = None,
+                         ctx=None):
+    """encode_chunk on the GPU (sb_encode_column_device) for the options
+    whose codec choice needs no sampling (ratio None, default codec None,
+    forced codec none or Bitpacking): values is a device tensor of a fixed
+    width type, validity an optional device bool tensor.  Returns (device
+    uint8 tensor of the column chunk, page metas), byte-identical to
+    encode_column with the same options."""
+    import torch
+
+    from .read import default_context
+
+    options = options or WriteOptions()
+    ctx = ctx or default_context()
+    tdt = {torch.int8: np.int8, torch.int16: np.int16, torch.int32: np.int32, torch.int64: np.int64,
+           torch.uint8: np.uint8, torch.uint16: np.uint16, torch.uint32: np.uint32, torch.uint64: np.uint64,
+           torch.float32: np.float32, torch.float64: np.float64}[values.dtype]
+    phys = physical_type(np.dtype(tdt))
+    values = values.contiguous()
+    n = values.numel()
+    vb = None
+    if nullable:
+        v = validity.to(torch.bool).reshape(-1)
+        pad = (-n) % 8
+        if pad:
+            v = torch.cat([v, torch.zeros(pad, dtype=torch.bool, device=v.device)])
+        w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=v.device)
+        vb = (v.view(-1, 8).to(torch.uint8) * w).sum(1, dtype=torch.uint8) if n else torch.zeros(1, dtype=torch.uint8,
+                                                                                                 device=v.device)
+    P = options.max_page_size or n
+    cap = N.lib().sb_encode_device_bound(phys, n, int(nullable), P)
+    out = torch.empty(max(cap, 16), dtype=torch.uint8, device=values.device)
+    npages = (n + P - 1) // P if n else 0
+    metas = (N.PageMetaC * max(npages, 1))()
+    olen, npg = ctypes.c_uint64(), ctypes.c_uint64()
+    opts = options.c()
+    st = N.lib().sb_encode_column_device(
+        ctx._h, phys, ctypes.c_void_p(values.data_ptr()), None if vb is None else ctypes.c_void_p(vb.data_ptr()), n,
+        int(nullable), ctypes.byref(opts), P, ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(olen),
+        metas, max(npages, 1), ctypes.byref(npg))
+    if st:
+        raise N.StrawboatError(st, "encode_column_device")
+    return out[: olen.value], [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
+
+
 def encode_page(values: np.ndarray, validity=None, nullable: bool = False,
                 options: Optional[WriteOptions] = None, seed: Optional[int] = None) -> bytes:
     options = options or WriteOptions()
