@@ -119,6 +119,8 @@ void sb_ctx_destroy(sb_ctx* ctx);
  * context uses a non-blocking stream of its own. */
 sb_status sb_ctx_set_stream(sb_ctx* ctx, void* hip_stream);
 void* sb_ctx_stream(sb_ctx* ctx);
+/* The device the context binds (-1 for NULL). */
+int32_t sb_ctx_device(const sb_ctx* ctx);
 sb_status sb_sync(sb_ctx* ctx);
 const char* sb_last_error(const sb_ctx* ctx);
 const char* sb_status_str(int status);
@@ -264,6 +266,13 @@ sb_status sb_encode_list_column(int32_t physical_type, const int64_t* h_offsets,
                                 uint64_t max_page_rows, int32_t n_threads, uint8_t** h_out, uint64_t* out_len,
                                 sb_page_meta** h_metas, uint64_t* n_pages);
 uint64_t sb_page_seed(uint64_t seed, uint64_t page);
+/* The block compressors the device encoder runs for the Basic codecs
+ * (CommonCompression::compress, basic.rs:108-152), built for the host:
+ * LZ4 = liblz4 1.9.3 LZ4_compress_default restated (dst holds n + n/255 + 16
+ * bytes), Snappy = the engine's raw-snappy writer (dst holds n + n/20 + 16).
+ * Return the compressed size. */
+uint64_t sb_lz4_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst);
+uint64_t sb_snappy_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst);
 /* encode_chunk on the device (HIP, gfx950) for the options whose codec choice
  * needs no trial compression: default_compress_ratio None (has_ratio = 0),
  * default codec None, forced codec none or Bitpacking.  Pages of Int32 /

@@ -21,13 +21,13 @@ INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = ran
 BOOLEAN = 15
 
 EXPORTED = [
-    "sb_ctx_create", "sb_ctx_destroy", "sb_ctx_set_stream", "sb_ctx_stream", "sb_sync", "sb_last_error",
+    "sb_ctx_create", "sb_ctx_destroy", "sb_ctx_set_stream", "sb_ctx_stream", "sb_ctx_device", "sb_sync", "sb_last_error",
     "sb_status_str", "sb_plan_column", "sb_plan_destroy", "sb_plan_num_rows", "sb_plan_num_pages",
     "sb_decode_planned", "sb_plan_status", "sb_decode_column", "sb_plan_last_kernel_ms", "sb_plan_enable_timing",
     "sb_decompress_values", "sb_read_meta", "sb_encode_page", "sb_encode_column", "sb_page_seed",
     "sb_write_footer", "sb_free", "sb_encode_binary_column", "sb_plan_values_bytes", "sb_decode_binary_planned",
     "sb_encode_list_column", "sb_plan_list_column", "sb_plan_num_leaves", "sb_decode_list_planned",
-    "sb_encode_device_bound", "sb_encode_column_device",
+    "sb_encode_device_bound", "sb_encode_column_device", "sb_lz4_compress_host", "sb_snappy_compress_host",
 ]
 
 
@@ -89,6 +89,8 @@ def lib():
     L.sb_ctx_set_stream.restype = I32
     L.sb_ctx_stream.argtypes = [P]
     L.sb_ctx_stream.restype = P
+    L.sb_ctx_device.argtypes = [P]
+    L.sb_ctx_device.restype = I32
     L.sb_sync.argtypes = [P]
     L.sb_sync.restype = I32
     L.sb_last_error.argtypes = [P]

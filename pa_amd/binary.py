@@ -12,7 +12,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native as N
-from .read import Context, PageMeta, default_context, _as_device_bytes
+from .read import Context, PageMeta, resolve_context, _as_device_bytes
 
 BINARY, LARGE_BINARY, UTF8, LARGE_UTF8 = 11, 12, 13, 14
 
@@ -83,7 +83,7 @@ class BinaryColumnDecoder:
         import torch
 
         L = _lib()
-        self.ctx = ctx or default_context()
+        self.ctx = resolve_context(ctx, chunk)
         self.phys = physical_type
         self.nullable = bool(nullable)
         self.chunk = _as_device_bytes(chunk, self.ctx.device)

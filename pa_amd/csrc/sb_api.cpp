@@ -21,7 +21,26 @@ struct sb_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
+  void* scr[4] = {nullptr, nullptr, nullptr, nullptr};  // sb::ctx_scratch
+  size_t scr_bytes[4] = {0, 0, 0, 0};
 };
+
+namespace sb {
+void* ctx_scratch(sb_ctx* c, size_t bytes, int slot) {
+  if (!c || slot < 0 || slot >= 4) return nullptr;
+  if (c->scr_bytes[slot] < bytes) {
+    if (c->scr[slot]) {
+      (void)hipStreamSynchronize(c->stream);  // earlier work on the stream may still use it
+      (void)hipFree(c->scr[slot]);
+    }
+    c->scr[slot] = nullptr;
+    c->scr_bytes[slot] = 0;
+    if (hipMalloc(&c->scr[slot], bytes) != hipSuccess) return nullptr;
+    c->scr_bytes[slot] = bytes;
+  }
+  return c->scr[slot];
+}
+}  // namespace sb
 
 struct sb_plan {
   sb_column_desc desc{};
@@ -125,6 +144,12 @@ sb_status sb_ctx_create(int device, sb_ctx** out) {
 
 void sb_ctx_destroy(sb_ctx* ctx) {
   if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  for (int i = 0; i < 4; i++)
+    if (ctx->scr[i]) {
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipFree(ctx->scr[i]);
+    }
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -136,6 +161,8 @@ sb_status sb_ctx_set_stream(sb_ctx* ctx, void* s) {
 }
 
 void* sb_ctx_stream(sb_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int32_t sb_ctx_device(const sb_ctx* ctx) { return ctx ? ctx->device : -1; }
 
 sb_status sb_sync(sb_ctx* ctx) {
   if (!ctx) return SB_E_ARG;

@@ -1500,12 +1500,7 @@ template <int W, bool FLT>
 static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
   dim3 block(NT);
   if (kind == 2) {
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void*)k_decode_deferred<W, FLT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)a.stage_bytes);
-      attr = true;
-    }
+    ensure_lds_attr(k_decode_deferred<W, FLT>, (int)kDeferredLds);
     hipLaunchKernelGGL((k_decode_deferred<W, FLT>), dim3(a.n_list), block, a.stage_bytes, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
@@ -2699,14 +2694,10 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
   const dim3 block(sbk::NT);
   // one workgroup per page (grid-stride past 64 Ki pages): as many resident per CU as the LDS budget allows
   const dim3 grid(std::min<uint32_t>(L.n_pages ? L.n_pages : 1, 65535u));
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)sbk::k_bin_size<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
-    hipFuncSetAttribute((const void*)sbk::k_bin_size<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
-    hipFuncSetAttribute((const void*)sbk::k_bin_decode<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
-    hipFuncSetAttribute((const void*)sbk::k_bin_decode<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
-    attr = true;
-  }
+  ensure_lds_attr(sbk::k_bin_size<4>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_size<8>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_decode<4>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_decode<8>, (int)kDeferredLds);
   if (stage == 0) {
     if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_size<8>, grid, block, lds, st, a);
     else hipLaunchKernelGGL(sbk::k_bin_size<4>, grid, block, lds, st, a);
@@ -2731,11 +2722,7 @@ int launch_inflate(const InflateLaunch& a, void* stream) {
 namespace sb {
 int launch_bool(const LaunchArgs& a, void* stream) {
   if (a.n_list == 0) return 0;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)sbk::k_bool_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDeferredLds);
-    attr = true;
-  }
+  ensure_lds_attr(sbk::k_bool_decode, (int)kDeferredLds);
   const uint32_t grid = std::min<uint32_t>(a.n_list, 65535u);
   hipLaunchKernelGGL(sbk::k_bool_decode, dim3(grid), dim3(sbk::NT), a.stage_bytes, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;

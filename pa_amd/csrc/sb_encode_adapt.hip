@@ -1,0 +1,1162 @@
+// sb_encode_adapt.hip -- the writer's adaptive codec cascade on MI355X
+// (gfx950): NativeWriter::encode_chunk (write/common.rs:49-119) ->
+// write_simple (write/serialize.rs:52-132) -> compress_integer /
+// compress_double (compression/integer/mod.rs:35-347,
+// compression/double/mod.rs:32-347) for every page of a fixed-width column,
+// one 256-thread workgroup per page, byte-identical to the host writer
+// (sb_encode.cpp) and the oracle (oracle/sb_oracle.c orc_write_flat_page).
+//
+// Per value stream (compress_stream below, recursive through Dict / Freq):
+//   gen_stats (integer/mod.rs:179-229): null count, min / max and
+//     sortedness by the type's total order, distinct count and the most
+//     frequent value (first occurrence breaks ties: the seeded, tie-broken
+//     selection that replaces the reference's HashMap order) -- an LDS
+//     open-addressing table of (count << 16 | first row + 1) words, filled
+//     with atomicCAS and lowered to the smallest row;
+//   choose_compressor (:231-308) with the seeded splitmix64 trial-window
+//     sampler (:310-347, 10 windows x 64 rows) standing in for thread_rng;
+//   the codecs: RLE (rle.rs:64-104; runs from a boundary flag scan), Dict
+//     (dict.rs:34-73; first-occurrence ids from a flag scan over rows, the
+//     index stream cascades), Freq (freq.rs:34-86; exception compaction,
+//     roaring 0.10.1 array / bitmap container, the exception stream
+//     cascades), OneValue, Bitpacking / DeltaBitpacking (bp.rs:37-65,
+//     delta_bp.rs:37-67; BitPacker4x words computed per lane word), Patas
+//     (double/patas.rs:37-105; the back reference found by a 127-row window
+//     search), and the Basic codecs None / LZ4 / Snappy (sb_lz4c.h, one lane;
+//     Zstd level 3 is not restated: NotYetImplemented).
+// Pages are written into per-page slots of a batch, then compacted.
+// Integer work; bound by the per-page hash/scan work, not by MFMA.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/strawboat_gpu.h"
+#include "sb_internal.h"
+#include "sb_lz4c.h"
+
+namespace sba {
+
+constexpr int NT = 256, NW = NT / 64;
+constexpr uint32_t kMaxRows = 16384;
+constexpr uint32_t SC = 10, SS = 64, kSample = SC * SS;
+
+enum : int { C_NONE = 0, C_LZ4 = 1, C_ZSTD = 2, C_SNAPPY = 3, C_RLE = 10, C_DICT = 11, C_ONE = 12, C_FREQ = 13, C_BP = 14,
+             C_DBP = 15, C_PATAS = 16 };
+enum : uint32_t { E_OK = 0, E_SPEC = 1, E_NYI = 2, E_CAP = 6 };
+
+struct Opts {
+  int32_t dflt, has_ratio;
+  double ratio;
+  uint32_t forbidden;
+  int32_t forced;
+};
+
+// ---------------------------------------------------------------------------
+// element traits: raw bits, total-order key (Tr::key in sb_encode.cpp), as_i64
+// ---------------------------------------------------------------------------
+template <int W> struct UT;
+template <> struct UT<1> { using U = uint8_t; };
+template <> struct UT<2> { using U = uint16_t; };
+template <> struct UT<4> { using U = uint32_t; };
+template <> struct UT<8> { using U = uint64_t; };
+
+template <int W>
+__device__ __forceinline__ uint64_t ld(const uint8_t* p, uint32_t i) {
+  return (uint64_t)((const typename UT<W>::U*)p)[i];
+}
+
+template <int W, bool FLT, bool SGN>
+__device__ __forceinline__ uint64_t key_of(uint64_t b) {
+  if constexpr (FLT) {
+    constexpr int nb = 8 * W;
+    constexpr uint64_t sign = 1ull << (nb - 1);
+    constexpr uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+    bool nan;
+    if constexpr (W == 8) nan = ((b >> 52) & 0x7FF) == 0x7FF && (b & 0xFFFFFFFFFFFFFull);
+    else nan = ((b >> 23) & 0xFF) == 0xFF && (b & 0x7FFFFFull);
+    if (nan) return all;  // OrderedFloat: NaN is the largest and equal to itself
+    if ((b & (all >> 1)) == 0) b = 0;  // -0.0 == 0.0
+    return (b & sign) ? (~b & all) : (b | sign);
+  } else if constexpr (SGN) {
+    const int64_t s = W == 1 ? (int64_t)(int8_t)b : W == 2 ? (int64_t)(int16_t)b : W == 4 ? (int64_t)(int32_t)b : (int64_t)b;
+    return (uint64_t)s ^ 0x8000000000000000ull;
+  } else {
+    return b;
+  }
+}
+// IntegerType::as_i64 of the value with this key (floats: unused, 0)
+template <int W, bool FLT, bool SGN>
+__device__ __forceinline__ int64_t key_as_i64(uint64_t k) {
+  if constexpr (FLT) return 0;
+  else if constexpr (SGN) return (int64_t)(k ^ 0x8000000000000000ull);
+  else return (int64_t)k;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xFF51AFD7ED558CCDull;
+  k ^= k >> 33;
+  k *= 0xC4CEB9FE1A85EC53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// ---------------------------------------------------------------------------
+// array view: n elements of W bytes + optional LSB validity bitmap
+// ---------------------------------------------------------------------------
+struct Av {
+  const uint8_t* p;
+  const uint8_t* vb;  // nullptr = all valid
+  uint64_t vbit;      // bit of row 0 in vb
+  uint32_t n;
+};
+__device__ __forceinline__ bool valid_at(const Av& a, uint32_t i) {
+  if (!a.vb) return true;
+  const uint64_t b = a.vbit + i;
+  return (a.vb[b >> 3] >> (b & 7)) & 1;
+}
+
+// ---------------------------------------------------------------------------
+// per-workgroup state
+// ---------------------------------------------------------------------------
+struct Sh {
+  uint64_t red[NW];
+  uint32_t redu[NW];
+  uint64_t rng;
+  uint32_t win[SC];
+  uint32_t err;
+  // stats of the current stream
+  uint32_t nulls, unique, top_count, top_row;
+  uint32_t sorted;
+  uint64_t kmin, kmax;
+  uint32_t first_valid;
+  uint32_t pfail;  // Patas: an f32 value equal to its reference
+};
+
+struct Ctx {
+  uint32_t* work;   // LDS work area: hash tables, run starts, bitmaps, LZ4 / Snappy tables
+  uint32_t work_bytes;
+  uint8_t* samp;    // LDS: kSample * 8 value bytes + kSample / 8 validity bytes
+  uint8_t* scratch; // global: 2 levels x nmax x 8 bytes
+  uint32_t nmax;
+  uint8_t* out;     // global: the page slot
+  uint32_t cap;
+  Opts o;
+};
+
+__device__ __forceinline__ void set_err(Sh& sh, uint32_t e) { atomicMax(&sh.err, e); }
+
+__device__ __forceinline__ uint64_t rng_next(uint64_t& s) {  // splitmix64 (sb_encode.cpp Rng)
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// ---------------------------------------------------------------------------
+// block primitives (all NT threads call them)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d; d >>= 1) v = max(v, (uint64_t)__shfl_xor(v, d, 64));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d; d >>= 1) v = min(v, (uint64_t)__shfl_xor(v, d, 64));
+  return v;
+}
+__device__ uint64_t bsum(Sh& sh, uint64_t v) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh.red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) t += sh.red[k];
+  __syncthreads();
+  return t;
+}
+__device__ uint64_t bmax(Sh& sh, uint64_t v) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) sh.red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) t = max(t, sh.red[k]);
+  __syncthreads();
+  return t;
+}
+__device__ uint64_t bmin(Sh& sh, uint64_t v) {
+  v = wave_min(v);
+  if ((threadIdx.x & 63) == 0) sh.red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = ~0ull;
+#pragma unroll
+  for (int k = 0; k < NW; k++) t = min(t, sh.red[k]);
+  __syncthreads();
+  return t;
+}
+// exclusive prefix sum over threads; *tot = block total
+__device__ uint32_t bscan(Sh& sh, uint32_t v, uint32_t* tot) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) sh.redu[wv] = x;
+  __syncthreads();
+  uint32_t pre = 0, t = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    pre += (uint32_t)k < wv ? sh.redu[k] : 0u;
+    t += sh.redu[k];
+  }
+  __syncthreads();
+  *tot = t;
+  return pre + x - v;
+}
+// exclusive prefix max over threads (0 for thread 0); *tot = block max
+__device__ uint32_t bexcl_max(Sh& sh, uint32_t v, uint32_t* tot) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x = max(x, y);
+  }
+  if (lane == 63) sh.redu[wv] = x;
+  __syncthreads();
+  uint32_t pre = 0, t = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    if ((uint32_t)k < wv) pre = max(pre, sh.redu[k]);
+    t = max(t, sh.redu[k]);
+  }
+  __syncthreads();
+  const uint32_t xl = __shfl_up(x, 1, 64);
+  *tot = t;
+  return max(pre, lane ? xl : 0u);
+}
+// inclusive prefix max over threads
+__device__ uint32_t bscan_max(Sh& sh, uint32_t v, uint32_t* tot) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x = max(x, y);
+  }
+  if (lane == 63) sh.redu[wv] = x;
+  __syncthreads();
+  uint32_t pre = 0, t = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    if ((uint32_t)k < wv) pre = max(pre, sh.redu[k]);
+    t = max(t, sh.redu[k]);
+  }
+  __syncthreads();
+  *tot = t;
+  return max(pre, x);
+}
+
+__device__ __forceinline__ void put8(uint8_t* o, uint64_t v, uint32_t nb) {
+  for (uint32_t j = 0; j < nb; j++) o[j] = (uint8_t)(v >> (8 * j));
+}
+__device__ __forceinline__ bool room(const Ctx& c, Sh& sh, uint64_t end) {
+  if (end > c.cap) {
+    set_err(sh, E_CAP);
+    return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// LDS hash table: word = count << 16 | (first row + 1); S slots (pow2)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t tab_slots(uint32_t n) {
+  uint32_t s = 64;
+  while (s < 2 * n) s <<= 1;
+  return s;
+}
+template <class KeyF>
+__device__ __forceinline__ uint32_t tab_insert(uint32_t* tab, uint32_t S, uint32_t r, uint64_t k, KeyF key) {
+  uint32_t h = (uint32_t)(mix64(k) >> 32) & (S - 1);
+  for (;;) {
+    uint32_t e = tab[h];
+    if (e == 0) {
+      const uint32_t prev = atomicCAS(&tab[h], 0u, (1u << 16) | (r + 1));
+      if (prev == 0) return h;
+      e = prev;
+    }
+    const uint32_t o = (e & 0xFFFFu) - 1;
+    if (key(o) == k) {
+      uint32_t old = atomicAdd(&tab[h], 1u << 16) + (1u << 16);
+      while ((old & 0xFFFFu) > r + 1) {  // keep the smallest row
+        const uint32_t prev = atomicCAS(&tab[h], old, (old & 0xFFFF0000u) | (r + 1));
+        if (prev == old) break;
+        old = prev;
+      }
+      return h;
+    }
+    h = (h + 1) & (S - 1);
+  }
+}
+template <class KeyF>
+__device__ __forceinline__ uint32_t tab_find(const uint32_t* tab, uint32_t S, uint64_t k, KeyF key) {
+  uint32_t h = (uint32_t)(mix64(k) >> 32) & (S - 1);
+  for (;;) {
+    const uint32_t e = tab[h];
+    if (e == 0 || key((e & 0xFFFFu) - 1) == k) return h;
+    h = (h + 1) & (S - 1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// gen_stats (integer/mod.rs:179-229, double/mod.rs:178-229)
+// ---------------------------------------------------------------------------
+template <int W, bool FLT, bool SGN>
+__device__ void gen_stats(Ctx& c, Sh& sh, const Av& a) {
+  const uint32_t tid = threadIdx.x, n = a.n;
+  // sortedness over valid rows against the previous valid value (T::default()
+  // before the first), min / max over every slot, null count: thread chunks
+  const uint32_t ch = (n + NT - 1) / NT;
+  const uint32_t r0 = min(n, tid * ch), r1 = min(n, r0 + ch);
+  uint32_t nulls = 0, lastv = 0, firstv = 0;  // rows + 1 (0 = none)
+  bool sorted = true;
+  uint64_t kmin = ~0ull, kmax = 0, prevk = 0;
+  bool have = false;
+  for (uint32_t r = r0; r < r1; r++) {
+    const uint64_t k = key_of<W, FLT, SGN>(ld<W>(a.p, r));
+    kmin = min(kmin, k);
+    kmax = max(kmax, k);
+    if (valid_at(a, r)) {
+      if (have && k < prevk) sorted = false;
+      if (!firstv) firstv = r + 1;
+      prevk = k;
+      have = true;
+      lastv = r + 1;
+    } else {
+      nulls++;
+    }
+  }
+  uint32_t tot;
+  const uint32_t prev_row = bexcl_max(sh, lastv, &tot);  // last valid row (+1) before this chunk
+  if (firstv) {
+    const uint64_t pk = prev_row ? key_of<W, FLT, SGN>(ld<W>(a.p, prev_row - 1)) : key_of<W, FLT, SGN>(0);
+    const uint64_t fk = key_of<W, FLT, SGN>(ld<W>(a.p, firstv - 1));
+    if (fk < pk) sorted = false;
+  }
+  const uint64_t s_nulls = bsum(sh, nulls);
+  const uint64_t s_unsorted = bsum(sh, sorted ? 0u : 1u);
+  const uint64_t s_kmin = bmin(sh, kmin), s_kmax = bmax(sh, kmax);
+  const uint64_t s_first = bmin(sh, firstv ? firstv : 0xFFFFFFFFu);
+  // distinct values over every slot (nulls included)
+  const uint32_t S = tab_slots(n);
+  uint32_t* tab = c.work;
+  for (uint32_t i = tid; i < S; i += NT) tab[i] = 0;
+  __syncthreads();
+  auto key = [&](uint32_t r) { return key_of<W, FLT, SGN>(ld<W>(a.p, r)); };
+  for (uint32_t r = tid; r < n; r += NT) tab_insert(tab, S, r, key(r), key);
+  __syncthreads();
+  uint32_t uniq = 0;
+  uint64_t best = 0;
+  for (uint32_t i = tid; i < S; i += NT) {
+    const uint32_t e = tab[i];
+    if (e) {
+      uniq++;
+      best = max(best, ((uint64_t)(e >> 16) << 32) | (0xFFFFFFFFu - ((e & 0xFFFFu) - 1)));
+    }
+  }
+  const uint64_t s_uniq = bsum(sh, uniq);
+  const uint64_t s_best = bmax(sh, best);
+  if (tid == 0) {
+    sh.nulls = (uint32_t)s_nulls;
+    sh.sorted = s_unsorted == 0;
+    sh.kmin = n ? s_kmin : key_of<W, FLT, SGN>(0);
+    sh.kmax = n ? s_kmax : key_of<W, FLT, SGN>(0);
+    sh.unique = (uint32_t)s_uniq;
+    sh.top_count = (uint32_t)(s_best >> 32);
+    sh.top_row = 0xFFFFFFFFu - (uint32_t)s_best;
+    sh.first_valid = (uint32_t)s_first;  // row + 1, or ~0u when every row is null
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// size-only and writing codec bodies
+// ---------------------------------------------------------------------------
+// RLE (rle.rs:64-104): runs start at row 0 and at every valid row whose key
+// differs from the previous valid row's; nulls extend the current run.
+// WRITE: run records at c.out + pos.  Returns the body size.
+template <int W, bool FLT, bool SGN, bool WRITE>
+__device__ uint32_t rle_body(Ctx& c, Sh& sh, const Av& a, uint32_t pos) {
+  const uint32_t tid = threadIdx.x, n = a.n;
+  if (n == 0) return 0;
+  uint32_t carry_last = 0, carry_runs = 0;  // last valid row + 1 so far, runs so far
+  uint32_t* rs = c.work;                    // run starts (WRITE)
+  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+    const uint32_t r = t0 + tid;
+    const bool in = r < n;
+    const bool v = in && valid_at(a, r);
+    uint32_t tmax;
+    uint32_t prev = bexcl_max(sh, v ? r + 1 : 0u, &tmax);  // previous valid row (+1) in the tile
+    prev = max(prev, carry_last);
+    bool start = in && r == 0;
+    if (v && prev) {
+      const uint64_t k = key_of<W, FLT, SGN>(ld<W>(a.p, r));
+      const uint64_t pk = key_of<W, FLT, SGN>(ld<W>(a.p, prev - 1));
+      start = k != pk;
+    }
+    uint32_t tot;
+    const uint32_t ex = bscan(sh, start ? 1u : 0u, &tot);
+    if (WRITE && start) rs[carry_runs + ex] = r;
+    carry_runs += tot;
+    carry_last = max(carry_last, tmax);
+  }
+  const uint32_t R = carry_runs;
+  const uint32_t rec = 4 + W;
+  if (WRITE) {
+    if (!room(c, sh, (uint64_t)pos + (uint64_t)R * rec)) return 0;
+    if (tid == 0) rs[R] = n;
+    __syncthreads();
+    const uint32_t fv = sh.first_valid;
+    for (uint32_t j = tid; j < R; j += NT) {
+      const uint32_t s = rs[j], e = rs[j + 1];
+      uint64_t val;
+      if (j == 0) val = fv != 0xFFFFFFFFu ? ld<W>(a.p, fv - 1) : 0;
+      else val = ld<W>(a.p, s);
+      uint8_t* o = c.out + pos + (uint64_t)j * rec;
+      put8(o, e - s, 4);
+      put8(o + 4, val, W);
+    }
+    __syncthreads();
+  }
+  return R * rec;
+}
+
+// first valid row (+1, ~0u if none) of an array (for views whose stats are not current)
+__device__ uint32_t first_valid_row(Sh& sh, const Av& a) {
+  uint32_t f = 0xFFFFFFFFu;
+  for (uint32_t r = threadIdx.x; r < a.n; r += NT)
+    if (valid_at(a, r)) {
+      f = r + 1;
+      break;
+    }
+  return (uint32_t)bmin(sh, f);
+}
+
+// BitPacker4x (bitpacking 0.8.0): value 4i + l of a block at bit i*b of lane
+// l's stream, lane word k at byte 16k + 4l; b = bits of the OR of the raw
+// values (also for the delta variant, delta_bp.rs:50).
+__device__ __forceinline__ uint32_t bp_val(const uint8_t* p, uint32_t base, uint32_t j, bool delta) {
+  const uint32_t x = (uint32_t)ld<4>(p, base + j);
+  if (!delta) return x;
+  const uint32_t prev = (base + j) ? (uint32_t)ld<4>(p, base + j - 1) : 0u;
+  return x - prev;
+}
+template <bool WRITE>
+__device__ uint32_t bp_body(Ctx& c, Sh& sh, const Av& a, uint32_t pos, bool delta) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t nblk = a.n / 128;
+  uint32_t* bw = c.work;          // [nblk] widths
+  uint32_t* boff = c.work + 256;  // [nblk + 1] block offsets (nblk <= 128)
+  for (uint32_t k = wv; k < nblk; k += NW) {
+    uint32_t acc = (uint32_t)ld<4>(a.p, 128 * k + lane) | (uint32_t)ld<4>(a.p, 128 * k + 64 + lane);
+#pragma unroll
+    for (int d = 32; d; d >>= 1) acc |= __shfl_xor(acc, d, 64);
+    if (lane == 0) bw[k] = acc ? 32 - __builtin_clz(acc) : 0;
+  }
+  __syncthreads();
+  uint32_t tot;
+  const uint32_t ex = bscan(sh, tid < nblk ? 1 + 16 * bw[tid] : 0u, &tot);
+  if (!WRITE) return tot;
+  if (!room(c, sh, (uint64_t)pos + tot)) return 0;
+  if (tid < nblk) boff[tid] = ex;
+  __syncthreads();
+  for (uint32_t s = tid; s < nblk * 128; s += NT) {
+    const uint32_t k = s >> 7, w = s & 127, b = bw[k];
+    uint8_t* o = c.out + pos + boff[k];
+    if (w == 0) o[0] = (uint8_t)b;
+    if (w < 4 * b) {
+      const uint32_t kk = w >> 2, l = w & 3;
+      const uint64_t mask = b == 32 ? 0xFFFFFFFFull : ((1ull << b) - 1);
+      const uint32_t i0 = (32 * kk) / b, i1 = min(31u, (32 * kk + 31) / b);
+      uint32_t word = 0;
+      for (uint32_t i = i0; i <= i1; i++) {
+        const uint64_t v = bp_val(a.p, 128 * k, 4 * i + l, delta) & mask;
+        const int32_t sft = (int32_t)(i * b) - (int32_t)(32 * kk);
+        word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
+      }
+      put8(o + 1 + 4 * w, word, 4);
+    }
+  }
+  __syncthreads();
+  return tot;
+}
+
+// Patas (double/patas.rs:37-105): reference = the nearest earlier equal value
+// within 127 rows, else row i-1 (row 0 while i < 128 and no earlier equal).
+// Returns the body size, or ~0u when an f32 value equals its reference (the
+// reference writes a page its decoder misreads; the caller falls back).
+template <int W, bool WRITE>
+__device__ uint32_t patas_body(Ctx& c, Sh& sh, const Av& a, uint32_t pos) {
+  const uint32_t tid = threadIdx.x, n = a.n;
+  constexpr uint32_t nb = 8 * W;
+  if (tid == 0) sh.pfail = 0;
+  __syncthreads();
+  uint32_t carry = W;
+  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+    const uint32_t i = t0 + tid;
+    uint32_t sz = 0, packed = 0;
+    uint64_t xs = 0;
+    if (i < n && i > 0) {
+      const uint64_t v = ld<W>(a.p, i);
+      uint32_t ref = i < 128 ? 0u : i - 1;
+      const uint32_t lo = i >= 127 ? i - 127 : 0u;
+      for (uint32_t j = i; j-- > lo;)
+        if (ld<W>(a.p, j) == v) {
+          ref = j;
+          break;
+        }
+      const uint32_t diff = i - ref;
+      const uint64_t x = v ^ ld<W>(a.p, ref);
+      uint32_t tz, lz;
+      if (x == 0) {
+        tz = nb;
+        lz = nb;
+      } else {
+        tz = (uint32_t)__builtin_ctzll(x);
+        lz = (uint32_t)__builtin_clzll(x) - (64 - nb);
+      }
+      const uint32_t eq = tz == nb;
+      if (eq && nb == 32) sh.pfail = 1;
+      const uint32_t sig = eq ? 0 : nb - tz - lz;
+      const uint32_t sb = (sig >> 3) + ((sig & 7) != 0);
+      const uint32_t sft = tz - eq;
+      packed = ((diff & 0xFF) << 9) | ((sb & 7) << 6) | (sft & 0xFF);
+      xs = sft >= 64 ? 0 : x >> sft;
+      sz = 2 + sb;
+    }
+    uint32_t tot;
+    const uint32_t ex = bscan(sh, sz, &tot);
+    if (WRITE && sz) {
+      if ((uint64_t)pos + carry + ex + sz <= c.cap) {
+        uint8_t* o = c.out + pos + carry + ex;
+        put8(o, packed, 2);
+        put8(o + 2, xs, sz - 2);
+      } else {
+        set_err(sh, E_CAP);
+      }
+    }
+    carry += tot;
+  }
+  __syncthreads();
+  if (sh.pfail) return ~0u;
+  if (WRITE && tid == 0 && n) {
+    if ((uint64_t)pos + W <= c.cap) put8(c.out + pos, ld<W>(a.p, 0), W);
+  }
+  __syncthreads();
+  return n ? carry : 0u;
+}
+
+// the 640-row sample of compress_sample_ratio (integer/mod.rs:310-347) in LDS
+template <int W>
+__device__ Av take_sample(Ctx& c, Sh& sh, const Av& a) {
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) {
+    const uint32_t sep = a.n / SC, rem = a.n % SC;
+    for (uint32_t k = 0; k < SC; k++) {
+      const uint32_t range_end = (k == SC - 1 ? sep + rem : sep) - SS;
+      sh.win[k] = k * sep + (uint32_t)(rng_next(sh.rng) % range_end);
+    }
+  }
+  uint8_t* vb = c.samp + kSample * 8;
+  for (uint32_t i = tid; i < kSample / 8; i += NT) vb[i] = 0;
+  __syncthreads();
+  for (uint32_t q = tid; q < kSample; q += NT) {
+    const uint32_t src = sh.win[q / SS] + q % SS;
+    const uint64_t v = ld<W>(a.p, src);
+    if constexpr (W == 8) ((uint64_t*)c.samp)[q] = v;
+    else if constexpr (W == 4) ((uint32_t*)c.samp)[q] = (uint32_t)v;
+    else if constexpr (W == 2) ((uint16_t*)c.samp)[q] = (uint16_t)v;
+    else c.samp[q] = (uint8_t)v;
+  }
+  if (a.vb) {
+    for (uint32_t q = tid; q < kSample; q += NT) {
+      const uint32_t src = sh.win[q / SS] + q % SS;
+      if (valid_at(a, src)) atomicOr((uint32_t*)vb + (q >> 5), 1u << (q & 31));
+    }
+  }
+  __syncthreads();
+  return Av{c.samp, a.vb ? vb : nullptr, 0, kSample};
+}
+
+// compress_sample_ratio for RLE / Bitpacking / Patas
+template <int W, bool FLT, bool SGN>
+__device__ double sample_ratio(Ctx& c, Sh& sh, const Av& a, int codec) {
+  Av s = a;
+  if (a.n / SC > SS) s = take_sample<W>(c, sh, a);
+  const uint64_t total = (uint64_t)s.n * W;
+  uint64_t sz;
+  if (codec == C_RLE) {
+    sz = rle_body<W, FLT, SGN, false>(c, sh, s, 0);
+  } else if (codec == C_BP) {
+    if constexpr (W == 4 && !FLT) sz = bp_body<false>(c, sh, s, 0, false);
+    else sz = total;
+  } else {
+    const uint32_t r = patas_body<W, false>(c, sh, s, 0);
+    sz = r == ~0u ? total : r;
+  }
+  return (double)total / (double)sz;
+}
+
+__device__ __forceinline__ uint32_t bits_needed(uint64_t x) { return x ? 64 - (uint32_t)__clzll(x) : 0; }
+
+// choose_compressor (integer/mod.rs:231-308; double/mod.rs:231-307)
+template <int W, bool FLT, bool SGN>
+__device__ int choose(Ctx& c, Sh& sh, const Av& a, uint32_t fm) {
+  const Opts& o = c.o;
+  const uint32_t n = a.n;
+  const bool bp_ok = !FLT && W == 4 && key_as_i64<W, FLT, SGN>(sh.kmin) >= 0 && n % 128 == 0;
+  if (o.forced >= 0 && !(fm & (1u << o.forced))) {
+    const int f = o.forced;
+    const bool ok = FLT ? (f == C_FREQ || f == C_DICT || f == C_RLE || f == C_PATAS)
+                        : (f == C_FREQ || f == C_DICT || f == C_RLE || (f == C_BP && bp_ok));
+    if (ok) return f;
+  }
+  int result = o.dflt;
+  if (!o.has_ratio) return result;
+  double maxr = o.ratio;
+  const int ic[6] = {C_ONE, C_FREQ, C_DICT, C_RLE, C_BP, C_DBP};
+  const int dc[5] = {C_ONE, C_FREQ, C_DICT, C_PATAS, C_RLE};
+  const int nc = FLT ? 5 : 6;
+  const uint32_t uniq = sh.unique, nulls = sh.nulls;
+  for (int k = 0; k < nc; k++) {
+    const int cd = FLT ? dc[k] : ic[k];
+    if (fm & (1u << cd)) continue;
+    double r = 0.0;
+    switch (cd) {
+      case C_ONE: r = uniq <= 1 ? (double)n : 0.0; break;
+      case C_FREQ:  // freq.rs:129-151
+        if (uniq > 1) {
+          if ((double)nulls / (double)n >= 0.9) r = (double)(n - 1);
+          else if ((double)sh.top_count / (double)n >= 0.9 && (FLT || key_as_i64<W, FLT, SGN>(sh.kmax) >= 256))
+            r = (double)(n - 1);
+        }
+        break;
+      case C_DICT:  // dict.rs:105-120 (integer division in bits / 8 and 2n / 128)
+        if ((uint64_t)uniq * 3 < n) {
+          uint64_t after = (uint64_t)uniq * W + (uint64_t)n * (bits_needed(uniq) / 8);
+          after += (uint64_t)n * 2 / 128;
+          r = (double)((uint64_t)n * W) / (double)after;
+        }
+        break;
+      case C_RLE:
+      case C_PATAS: r = sample_ratio<W, FLT, SGN>(c, sh, a, cd); break;
+      case C_BP: r = bp_ok ? sample_ratio<W, FLT, SGN>(c, sh, a, C_BP) : 0.0; break;
+      case C_DBP:  // delta_bp.rs:97-110
+        r = (bp_ok && sh.sorted && nulls == 0) ? sample_ratio<W, FLT, SGN>(c, sh, a, C_BP) * 1.5 : 0.0;
+        break;
+    }
+    if (r > maxr) {
+      maxr = r;
+      result = cd;
+      if (r == (double)n) break;
+    }
+  }
+  return result;
+}
+
+// Basic codecs: the raw bytes of the values, None / LZ4 / Snappy
+__device__ uint32_t basic_body(Ctx& c, Sh& sh, int codec, const uint8_t* src, uint32_t len, uint32_t pos) {
+  const uint32_t tid = threadIdx.x;
+  if (codec == C_NONE) {
+    if (!room(c, sh, (uint64_t)pos + len)) return 0;
+    for (uint32_t j = tid; j < len; j += NT) c.out[pos + j] = src[j];
+    __syncthreads();
+    return len;
+  }
+  if (codec == C_LZ4 || codec == C_SNAPPY) {
+    const uint64_t bound = codec == C_LZ4 ? sbc::lz4_bound(len) : (uint64_t)len + len / 20 + 32;
+    if (!room(c, sh, (uint64_t)pos + bound)) return 0;
+    if (codec == C_LZ4)
+      for (uint32_t i = tid; i < sbc::kLz4TableBytes / 4; i += NT) c.work[i] = 0;
+    __syncthreads();
+    if (tid == 0) {
+      sh.redu[0] = codec == C_LZ4 ? sbc::lz4_compress(src, len, c.out + pos, c.work)
+                                  : sbc::snappy_compress(src, len, c.out + pos, c.work);
+    }
+    __syncthreads();
+    const uint32_t r = sh.redu[0];
+    __syncthreads();
+    return r;
+  }
+  if (tid == 0) set_err(sh, E_NYI);  // Zstd: libzstd level 3 is not restated on the device
+  __syncthreads();
+  return 0;
+}
+
+__device__ __forceinline__ void write_hdr(Ctx& c, uint32_t pos, int codec, uint32_t csize, uint32_t usize) {
+  if (threadIdx.x == 0) {
+    c.out[pos] = (uint8_t)codec;
+    put8(c.out + pos + 1, csize, 4);
+    put8(c.out + pos + 5, usize, 4);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// compress_integer / compress_double: [codec u8][csize u32][usize u32][body]
+// at c.out + pos; returns the position after it.  D = cascade depth.
+// ---------------------------------------------------------------------------
+template <int W, bool FLT, bool SGN, int D>
+__device__ uint32_t enc_stream(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos);
+
+// Dict (dict.rs:34-73): ids by first occurrence over valid rows (a null row
+// repeats the previous row's id; a null row 0 is T::default()), the u32
+// index stream cascades with Dict forbidden, then u32 k + k raw values.
+template <int W, bool FLT, bool SGN, int D>
+__device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos) {
+  const uint32_t tid = threadIdx.x, n = a.n;
+  uint32_t* idx = (uint32_t*)(c.scratch + (uint64_t)D * c.nmax * 8);
+  uint32_t* row_of = idx + c.nmax;
+  const bool v0 = n && valid_at(a, 0);
+  auto dv = [&](uint32_t r) -> uint64_t { return (r == 0 && !v0) ? 0ull : ld<W>(a.p, r); };
+  auto ins = [&](uint32_t r) { return r == 0 || valid_at(a, r); };
+  const uint32_t S = tab_slots(n);
+  uint32_t* tab = c.work;
+  for (uint32_t i = tid; i < S; i += NT) tab[i] = 0;
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += NT)
+    if (ins(r)) idx[r] = tab_insert(tab, S, r, dv(r), dv);  // the slot, for now
+  __syncthreads();
+  // ids: first rows in row order
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+    const uint32_t r = t0 + tid;
+    bool f = false;
+    uint32_t slot = 0;
+    if (r < n && ins(r)) {
+      slot = idx[r];
+      f = (tab[slot] & 0xFFFFu) == r + 1;
+    }
+    uint32_t tot;
+    const uint32_t ex = bscan(sh, f ? 1u : 0u, &tot);
+    if (f) row_of[carry + ex] = r;
+    carry += tot;
+  }
+  const uint32_t k = carry;
+  __syncthreads();
+  for (uint32_t j = tid; j < k; j += NT) {
+    const uint32_t r = row_of[j];
+    const uint32_t slot = idx[r];
+    tab[slot] = (j << 16) | (r + 1);
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += NT)
+    if (ins(r)) idx[r] = tab[idx[r]] >> 16;
+  __syncthreads();
+  // null rows take the id of the last inserted row before them
+  uint32_t carry_last = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+    const uint32_t r = t0 + tid;
+    const bool in = r < n && ins(r);
+    uint32_t tmax;
+    const uint32_t incl = bscan_max(sh, in ? r + 1 : 0u, &tmax);
+    const uint32_t last = max(incl, carry_last);
+    if (r < n && !in) idx[r] = idx[last - 1];
+    carry_last = max(carry_last, tmax);
+    __syncthreads();
+  }
+  __syncthreads();
+  const Av ia{(const uint8_t*)idx, nullptr, 0, n};
+  const uint32_t p2 = enc_stream<4, false, false, D + 1>(c, sh, ia, fm | (1u << C_DICT), pos);
+  if (sh.err) return pos;
+  if (!room(c, sh, (uint64_t)p2 + 4 + (uint64_t)k * W)) return pos;
+  if (tid == 0) put8(c.out + p2, k, 4);
+  for (uint32_t j = tid; j < k; j += NT) put8(c.out + p2 + 4 + j * W, dv(row_of[j]), W);
+  __syncthreads();
+  return p2 + 4 + k * W;
+}
+
+// Freq (freq.rs:34-86): top value (the most frequent, first occurrence on
+// ties; T::default() when >= 90 % nulls), roaring bitmap of the valid rows
+// that differ from it, their values as a cascaded stream (Freq forbidden).
+template <int W, bool FLT, bool SGN, int D>
+__device__ uint32_t freq_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos) {
+  const uint32_t tid = threadIdx.x, n = a.n;
+  const bool top_null = (double)sh.nulls / (double)n >= 0.9;
+  const uint64_t top = top_null ? 0ull : ld<W>(a.p, sh.top_row);
+  const uint64_t tk = key_of<W, FLT, SGN>(top);
+  uint8_t* exc = c.scratch + (uint64_t)D * c.nmax * 8;
+  uint32_t* bm = c.work;  // bitmap container (1024 x u64) when card > 4096
+  for (uint32_t i = tid; i < 2048; i += NT) bm[i] = 0;
+  __syncthreads();
+  // exceptions in row order; positions written as an array container after the header
+  const uint32_t rpos = pos + W + 4;  // roaring start
+  const uint32_t data = rpos + 16;    // container data (one container: n <= 65536)
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+    const uint32_t r = t0 + tid;
+    bool e = false;
+    uint64_t v = 0;
+    if (r < n && valid_at(a, r)) {
+      v = ld<W>(a.p, r);
+      e = top_null || key_of<W, FLT, SGN>(v) != tk;
+    }
+    uint32_t tot;
+    const uint32_t ex = bscan(sh, e ? 1u : 0u, &tot);
+    if (e) {
+      const uint32_t j = carry + ex;
+      if constexpr (W == 8) ((uint64_t*)exc)[j] = v;
+      else if constexpr (W == 4) ((uint32_t*)exc)[j] = (uint32_t)v;
+      else if constexpr (W == 2) ((uint16_t*)exc)[j] = (uint16_t)v;
+      else exc[j] = (uint8_t)v;
+      atomicOr(&bm[r >> 5], 1u << (r & 31));
+      if ((uint64_t)data + 2ull * (j + 1) <= c.cap) put8(c.out + data + 2 * j, r & 0xFFFF, 2);
+    }
+    carry += tot;
+  }
+  const uint32_t e = carry;
+  __syncthreads();
+  const uint32_t bytes = e == 0 ? 8u : (e <= 4096 ? 16 + 2 * e : 16 + 8192u);
+  if (!room(c, sh, (uint64_t)rpos + bytes)) return pos;
+  if (tid == 0) {
+    put8(c.out + pos, top, W);
+    put8(c.out + pos + W, bytes, 4);
+    put8(c.out + rpos, 12346, 4);  // roaring 0.10.1 SERIAL_COOKIE_NO_RUNCONTAINER
+    put8(c.out + rpos + 4, e ? 1u : 0u, 4);
+    if (e) {
+      put8(c.out + rpos + 8, 0, 2);  // container key (high 16 bits)
+      put8(c.out + rpos + 10, e - 1, 2);
+      put8(c.out + rpos + 12, 16, 4);  // offset of the data
+    }
+  }
+  if (e > 4096)  // bitmap container: 1024 words
+    for (uint32_t i = tid; i < 2048; i += NT) put8(c.out + data + 4 * i, bm[i], 4);
+  __syncthreads();
+  const Av ea{exc, nullptr, 0, e};
+  return enc_stream<W, FLT, SGN, D + 1>(c, sh, ea, fm | (1u << C_FREQ), rpos + bytes);
+}
+
+template <int W, bool FLT, bool SGN, int D>
+__device__ uint32_t enc_stream(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos) {
+  const uint32_t tid = threadIdx.x, n = a.n;
+  if (!room(c, sh, (uint64_t)pos + 9)) return pos;
+  gen_stats<W, FLT, SGN>(c, sh, a);
+  int codec = choose<W, FLT, SGN>(c, sh, a, fm);
+  const uint32_t body = pos + 9;
+  uint32_t end = body;
+  switch (codec) {
+    case C_NONE:
+    case C_LZ4:
+    case C_ZSTD:
+    case C_SNAPPY: end = body + basic_body(c, sh, codec, a.p, n * W, body); break;
+    case C_RLE: end = body + rle_body<W, FLT, SGN, true>(c, sh, a, body); break;
+    case C_ONE: {  // one_value.rs:63-75: the first valid value, else default
+      if (!room(c, sh, (uint64_t)body + W)) break;
+      const uint32_t fv = sh.first_valid;
+      if (tid == 0) put8(c.out + body, fv != 0xFFFFFFFFu ? ld<W>(a.p, fv - 1) : 0, W);
+      __syncthreads();
+      end = body + W;
+      break;
+    }
+    case C_BP:
+    case C_DBP:
+      if constexpr (W == 4 && !FLT) end = body + bp_body<true>(c, sh, a, body, codec == C_DBP);
+      break;
+    case C_PATAS: {
+      const uint32_t r = patas_body<W, true>(c, sh, a, body);
+      if (r == ~0u) {  // f32 desync guard (sb_encode.cpp compress_stream): Basic instead
+        codec = c.o.dflt;
+        end = body + basic_body(c, sh, codec, a.p, n * W, body);
+      } else {
+        end = body + r;
+      }
+      break;
+    }
+    case C_DICT:
+      if constexpr (D < 2) end = dict_body<W, FLT, SGN, D>(c, sh, a, fm, body);
+      else set_err(sh, E_SPEC);
+      break;
+    case C_FREQ:
+      if constexpr (D < 2) end = freq_body<W, FLT, SGN, D>(c, sh, a, fm, body);
+      else set_err(sh, E_SPEC);
+      break;
+    default: set_err(sh, E_SPEC);
+  }
+  __syncthreads();
+  write_hdr(c, pos, codec, end - body, n * W);
+  __syncthreads();
+  return end;
+}
+
+// ---------------------------------------------------------------------------
+// page kernel, scan, compaction
+// ---------------------------------------------------------------------------
+struct AdArgs {
+  const uint8_t* values;
+  const uint8_t* validity;  // column bitmap or nullptr
+  uint64_t n_rows;
+  uint32_t P;
+  uint32_t page0;
+  uint32_t n_batch;
+  int nullable;
+  Opts o;
+  uint64_t seed;
+  uint8_t* slots;
+  uint64_t slot_bytes;
+  uint8_t* scratch;
+  uint64_t scratch_bytes;  // per page
+  uint32_t work_bytes;
+  uint64_t* sizes;         // [n_pages]
+  uint32_t* status;        // [n_pages]
+  uint64_t* offs;          // [n_pages + 1]: page offsets in the output; [n_pages] running total
+  uint8_t* out;
+  uint64_t out_cap;
+  uint32_t n_pages;
+};
+
+__device__ __forceinline__ uint64_t page_seed(uint64_t seed, uint64_t page) {  // sb_encode.cpp page_seed
+  uint64_t s = seed ^ (page * 0xD1B54A32D192ED03ull);
+  return rng_next(s);
+}
+
+__device__ __forceinline__ uint32_t uleb_len(uint64_t h) {
+  uint32_t l = 1;
+  while (h >= 0x80) {
+    h >>= 7;
+    l++;
+  }
+  return l;
+}
+
+template <int W, bool FLT, bool SGN>
+__global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
+  extern __shared__ uint32_t lds[];
+  __shared__ Sh sh;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t p = A.page0 + blockIdx.x;
+  const uint64_t r0 = (uint64_t)p * A.P;
+  const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
+  Ctx c;
+  c.work = lds;
+  c.work_bytes = A.work_bytes;
+  c.samp = (uint8_t*)lds + A.work_bytes;
+  c.scratch = A.scratch + (uint64_t)blockIdx.x * A.scratch_bytes;
+  c.nmax = A.P;
+  c.out = A.slots + (uint64_t)blockIdx.x * A.slot_bytes;
+  c.cap = (uint32_t)A.slot_bytes;
+  c.o = A.o;
+  if (tid == 0) {
+    sh.err = 0;
+    sh.rng = page_seed(A.seed, p);
+  }
+  __syncthreads();
+  uint32_t pos = 0;
+  const bool has_vb = A.nullable && A.validity;
+  if (A.nullable) {  // write_validity (serialize.rs:200-215): u32 def_len + ULEB128 bit-packed run + bitmap
+    const uint32_t nb = (n + 7) / 8;
+    uint64_t h = ((uint64_t)nb << 1) | 1;
+    const uint32_t hl = uleb_len(h);
+    if (tid == 0) {
+      put8(c.out, hl + nb, 4);
+      for (uint32_t j = 0; j < hl; j++, h >>= 7) c.out[4 + j] = (uint8_t)((h & 0x7F) | (j + 1 < hl ? 0x80 : 0));
+    }
+    for (uint32_t j = tid; j < nb; j += NT) {
+      uint32_t v = 0;
+      for (uint32_t b = 0; b < 8; b++) {
+        const uint32_t i = 8 * j + b;
+        const bool ok = i < n && (!has_vb || ((A.validity[(r0 + i) >> 3] >> ((r0 + i) & 7)) & 1));
+        v |= (ok ? 1u : 0u) << b;
+      }
+      c.out[4 + hl + j] = (uint8_t)v;
+    }
+    pos = 4 + hl + nb;
+  }
+  const Av a{A.values + r0 * W, has_vb ? A.validity : nullptr, r0, n};
+  __syncthreads();
+  pos = enc_stream<W, FLT, SGN, 0>(c, sh, a, A.o.forbidden, pos);
+  __syncthreads();
+  if (tid == 0) {
+    A.sizes[p] = sh.err ? 0 : pos;
+    A.status[p] = sh.err;
+  }
+}
+
+// page offsets of a batch: running total in offs[n_pages]
+__global__ __launch_bounds__(NT) void k_enc_offsets(AdArgs A) {
+  __shared__ Sh sh;
+  uint64_t carry = A.offs[A.n_pages];
+  for (uint32_t q0 = 0; q0 < A.n_batch; q0 += NT) {
+    const uint32_t q = q0 + threadIdx.x;
+    const uint64_t v = q < A.n_batch ? A.sizes[A.page0 + q] : 0;
+    // 64-bit exclusive scan
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t x = v;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) sh.red[wv] = x;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (int k = 0; k < NW; k++) {
+      pre += (uint32_t)k < wv ? sh.red[k] : 0;
+      tot += sh.red[k];
+    }
+    __syncthreads();
+    if (q < A.n_batch) A.offs[A.page0 + q] = carry + pre + x - v;
+    carry += tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) A.offs[A.n_pages] = carry;
+}
+
+// slot -> output, one workgroup per page
+__global__ __launch_bounds__(NT) void k_enc_compact(AdArgs A) {
+  const uint32_t p = A.page0 + blockIdx.x;
+  const uint64_t len = A.sizes[p], off = A.offs[p];
+  if (off + len > A.out_cap) {
+    if (threadIdx.x == 0) A.status[p] = E_CAP;
+    return;
+  }
+  const uint8_t* src = A.slots + (uint64_t)blockIdx.x * A.slot_bytes;  // 16-byte aligned
+  uint8_t* dst = A.out + off;
+  const uint32_t head = (uint32_t)min<uint64_t>(len, (16 - ((uintptr_t)dst & 15)) & 15);
+  for (uint32_t j = threadIdx.x; j < head; j += NT) dst[j] = src[j];
+  // dst + head is 16-aligned; src + head is not in general: assemble from aligned dwords
+  const uint64_t body = (len - head) / 16;
+  const uint32_t sh4 = (uint32_t)(head & 3);
+  const uint32_t* sw = (const uint32_t*)(src + (head & ~3u));
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  for (uint64_t i = threadIdx.x; i < body; i += NT) {
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) w[k] = sw[4 * i + k];
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh4);
+    v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh4);
+    v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh4);
+    v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh4);
+    *(u32x4*)(dst + head + 16 * i) = v;
+  }
+  for (uint64_t j = head + body * 16 + threadIdx.x; j < len; j += NT) dst[j] = src[j];
+}
+
+}  // namespace sba
+
+// ===========================================================================
+// host side
+// ===========================================================================
+namespace sb {
+
+static uint64_t stream_bound(uint64_t n, uint64_t w, int depth) {
+  // worst case of one headered stream of n values of w bytes (cascade depth left)
+  const uint64_t leaf = 9 + std::max({n * (4 + w), n * w + n * w / 255 + 32, (n / 128) * 513, w + n * (2 + w)});
+  if (depth == 0) return leaf;
+  const uint64_t dict = 9 + stream_bound(n, 4, depth - 1) + 4 + n * w;
+  const uint64_t freq = 9 + w + 4 + 16 + std::max<uint64_t>(2 * n, 8192) + stream_bound(n, w, depth - 1);
+  return std::max({leaf, dict, freq});
+}
+
+uint64_t adaptive_slot_bytes(uint64_t P, uint32_t w, int nullable) {
+  const uint64_t pre = nullable ? 4 + 10 + (P + 7) / 8 : 0;
+  return (pre + stream_bound(P, w, 2) + 64 + 15) & ~15ull;
+}
+
+uint32_t adaptive_work_bytes(uint64_t P) {
+  uint64_t s = 64;
+  while (s < 2 * P) s <<= 1;
+  return (uint32_t)std::max<uint64_t>({4 * s, sbc::kSnappyTableBytes, 8192});
+}
+
+template <int W, bool FLT, bool SGN>
+static void launch_t(const sba::AdArgs& a, uint32_t lds, hipStream_t st) {
+  ensure_lds_attr(sba::k_enc_adaptive<W, FLT, SGN>, (int)lds);
+  hipLaunchKernelGGL((sba::k_enc_adaptive<W, FLT, SGN>), dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+}
+
+// Encodes every page of a fixed-width column; returns SB status.
+int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_t* d_validity, uint64_t n_rows,
+                    int nullable, const sb_write_options* opts, uint64_t P, uint8_t* d_out, uint64_t out_cap,
+                    uint64_t* out_len, sb_page_meta* h_metas, uint64_t np) {
+  sba::Opts o{opts->default_codec, opts->has_ratio, opts->ratio, opts->forbidden_mask, opts->forced_codec};
+  uint32_t w = 0;
+  bool flt = false, sgn = false;
+  switch (phys) {
+    case SB_T_INT8: w = 1; sgn = true; break;
+    case SB_T_INT16: w = 2; sgn = true; break;
+    case SB_T_INT32: w = 4; sgn = true; break;
+    case SB_T_INT64: w = 8; sgn = true; break;
+    case SB_T_UINT8: w = 1; break;
+    case SB_T_UINT16: w = 2; break;
+    case SB_T_UINT32: w = 4; break;
+    case SB_T_UINT64: w = 8; break;
+    case SB_T_FLOAT32: w = 4; flt = true; break;
+    case SB_T_FLOAT64: w = 8; flt = true; break;
+    default: return SB_E_NYI;
+  }
+  if (P > sba::kMaxRows) return SB_E_NYI;
+  if (o.dflt == SB_CODEC_ZSTD) return SB_E_NYI;  // libzstd's compressor is not restated on the device
+  const uint64_t slot = adaptive_slot_bytes(P, w, nullable);
+  const uint64_t scr = (2 * P * 8 + 255) & ~255ull;
+  const uint32_t batch = (uint32_t)std::min<uint64_t>(np, 2048);
+  const uint32_t work = adaptive_work_bytes(P);
+  const uint32_t lds = work + sba::kSample * 8 + sba::kSample / 8 + 16;
+  uint8_t* slots = (uint8_t*)ctx_scratch(ctx, batch * slot + 256, 0);
+  uint8_t* scratch = (uint8_t*)ctx_scratch(ctx, batch * scr, 1);
+  uint64_t* meta = (uint64_t*)ctx_scratch(ctx, (2 * np + 2) * 8 + np * 4, 2);
+  if (!slots || !scratch || !meta) return SB_E_DEVICE;
+  hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
+  uint64_t* sizes = meta;
+  uint64_t* offs = meta + np;  // [np + 1]
+  uint32_t* status = (uint32_t*)(meta + 2 * np + 2);
+  if (hipMemsetAsync(offs + np, 0, 8, st) != hipSuccess) return SB_E_DEVICE;
+  for (uint64_t b0 = 0; b0 < np; b0 += batch) {
+    sba::AdArgs a{d_values, d_validity, n_rows, (uint32_t)P, (uint32_t)b0, (uint32_t)std::min<uint64_t>(batch, np - b0),
+                  nullable, o, opts->seed, slots, slot, scratch, scr, work, sizes, status, offs, d_out, out_cap,
+                  (uint32_t)np};
+    if (flt) {
+      if (w == 4) launch_t<4, true, false>(a, lds, st);
+      else launch_t<8, true, false>(a, lds, st);
+    } else if (sgn) {
+      if (w == 1) launch_t<1, false, true>(a, lds, st);
+      else if (w == 2) launch_t<2, false, true>(a, lds, st);
+      else if (w == 4) launch_t<4, false, true>(a, lds, st);
+      else launch_t<8, false, true>(a, lds, st);
+    } else {
+      if (w == 1) launch_t<1, false, false>(a, lds, st);
+      else if (w == 2) launch_t<2, false, false>(a, lds, st);
+      else if (w == 4) launch_t<4, false, false>(a, lds, st);
+      else launch_t<8, false, false>(a, lds, st);
+    }
+    hipLaunchKernelGGL(sba::k_enc_offsets, dim3(1), dim3(sba::NT), 0, st, a);
+    hipLaunchKernelGGL(sba::k_enc_compact, dim3(a.n_batch), dim3(sba::NT), 0, st, a);
+    if (hipGetLastError() != hipSuccess) return SB_E_DEVICE;
+  }
+  std::vector<uint64_t> sz(np + 1 + np);
+  std::vector<uint32_t> stv(np);
+  if (hipMemcpyAsync(sz.data(), sizes, (2 * np + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(stv.data(), status, np * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return SB_E_DEVICE;
+  for (uint64_t p = 0; p < np; p++) {
+    if (stv[p] == sba::E_NYI) return SB_E_NYI;
+    if (stv[p] == sba::E_CAP) return SB_E_ARG;
+    if (stv[p]) return SB_E_OUT_OF_SPEC;
+  }
+  *out_len = sz[np + np];
+  for (uint64_t p = 0; p < np; p++) h_metas[p] = sb_page_meta{sz[p], std::min<uint64_t>(P, n_rows - p * P)};
+  return SB_OK;
+}
+
+}  // namespace sb

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/strawboat_gpu.h"
+#include "sb_internal.h"
 
 namespace sbe {
 
@@ -248,13 +249,22 @@ static uint32_t type_width(int32_t t) {
   return 0;
 }
 
+namespace sb {
+uint64_t adaptive_slot_bytes(uint64_t P, uint32_t w, int nullable);
+int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_t* d_validity, uint64_t n_rows,
+                    int nullable, const sb_write_options* opts, uint64_t P, uint8_t* d_out, uint64_t out_cap,
+                    uint64_t* out_len, sb_page_meta* h_metas, uint64_t np);
+}  // namespace sb
+
 extern "C" uint64_t sb_encode_device_bound(int32_t physical_type, uint64_t n_rows, int32_t nullable,
                                            uint64_t max_page_rows) {
-  const uint64_t w = type_width(physical_type), P = max_page_rows ? max_page_rows : n_rows;
+  const uint64_t w = type_width(physical_type), P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
   if (!w || !P) return 0;
   const uint64_t pages = (n_rows + P - 1) / P;
   // per page: prefix (4 + <= 10 + P/8) + header 9 + max(raw, bitpacked at b = 32)
-  return pages * ((nullable ? 14 + (P + 7) / 8 : 0) + 9 + std::max(P * w, P / 128 * 513) + 16);
+  const uint64_t fast = (nullable ? 14 + (P + 7) / 8 : 0) + 9 + std::max(P * w, P / 128 * 513) + 16;
+  // the adaptive cascade's worst case (forced RLE, Dict / Freq cascades)
+  return pages * std::max(fast, sb::adaptive_slot_bytes(P, (uint32_t)w, nullable));
 }
 
 extern "C" sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type, const void* d_values,
@@ -264,19 +274,26 @@ extern "C" sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type,
                                              uint64_t metas_cap, uint64_t* n_pages) {
   if (!ctx || !opts || !out_len || !n_pages) return SB_E_ARG;
   const uint32_t w = type_width(physical_type);
-  const uint64_t P = max_page_rows ? max_page_rows : n_rows;
+  // page_size = max_page_size.unwrap_or(len).min(len) (write/common.rs:54-58)
+  const uint64_t P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
   if (!w || (nullable && !d_validity) || (n_rows && (!d_values || !d_out))) return SB_E_ARG;
-  // options whose codec choice needs no trial compression (choose_compressor, integer/mod.rs:231-240)
-  if (opts->has_ratio || opts->default_codec != SB_CODEC_NONE) return SB_E_NYI;
-  const bool forced_bp = opts->forced_codec == SB_CODEC_BITPACKING && !(opts->forbidden_mask & (1u << 14));
-  if (opts->forced_codec >= 0 && !forced_bp && !(opts->forbidden_mask & (1u << opts->forced_codec))) return SB_E_NYI;
-  if (P > sbe::kMaxPageRows || (P % 128 && P < n_rows) || 2 * P * w + 8192 > sbe::kLds) return SB_E_NYI;
   const uint64_t np = n_rows ? (n_rows + P - 1) / P : 0;
   *n_pages = np;
   if (np > metas_cap || (h_metas == nullptr && np)) return SB_E_ARG;
-  if (out_capacity < sb_encode_device_bound(physical_type, n_rows, nullable, P)) return SB_E_ARG;
   *out_len = 0;
   if (!np) return SB_OK;
+  if (hipSetDevice(sb_ctx_device(ctx)) != hipSuccess) return SB_E_DEVICE;
+  // Options whose codec choice needs no trial compression (ratio None, default
+  // None, forced codec none or Bitpacking: choose_compressor,
+  // integer/mod.rs:231-240) take the sizing + assembly fast path; every other
+  // option runs the adaptive cascade (sb_encode_adapt.hip).
+  const bool forced_bp = opts->forced_codec == SB_CODEC_BITPACKING && !(opts->forbidden_mask & (1u << 14));
+  const bool forced_other = opts->forced_codec >= 0 && !forced_bp && !(opts->forbidden_mask & (1u << opts->forced_codec));
+  if (opts->has_ratio || opts->default_codec != SB_CODEC_NONE || forced_other || P > sbe::kMaxPageRows ||
+      (P % 128 && P < n_rows) || 2 * P * w + 8192 > sbe::kLds)
+    return (sb_status)sb::encode_adaptive(ctx, physical_type, (const uint8_t*)d_values, d_validity, n_rows, nullable,
+                                          opts, P, d_out, out_capacity, out_len, h_metas, np);
+  if (out_capacity < sb_encode_device_bound(physical_type, n_rows, nullable, P)) return SB_E_ARG;
   hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
   const bool bp = forced_bp && (physical_type == SB_T_INT32 || physical_type == SB_T_UINT32);
   uint8_t* d_bw = nullptr;
@@ -289,11 +306,7 @@ extern "C" sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type,
   }
   sbe::EncArgs a{(const uint8_t*)d_values, d_validity, n_rows, (uint32_t)P, (uint32_t)np, w,
                  physical_type == SB_T_INT32, bp, nullable, d_bw, d_sz, d_sz + np, d_out};
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)sbe::k_enc_write, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sbe::kLds);
-    attr = true;
-  }
+  sb::ensure_lds_attr(sbe::k_enc_write, (int)sbe::kLds);
   const dim3 grid((uint32_t)std::min<uint64_t>(np, 65535));
   hipLaunchKernelGGL(sbe::k_enc_size, grid, dim3(sbe::NT), 0, st, a);
   hipLaunchKernelGGL(sbe::k_enc_scan, dim3(1), dim3(sbe::NT), 0, st, a);

@@ -1,8 +1,32 @@
 // sb_internal.h -- host/device shared layout of the MI355X strawboat engine.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
+struct sb_ctx;
+
 namespace sb {
+
+// Grow-only device scratch owned by a context (slot < 4), reused across calls
+// on its stream; nullptr if the allocation fails.
+void* ctx_scratch(sb_ctx* ctx, size_t bytes, int slot);
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: set it once
+// for each (kernel, current device) pair before the first launch there.
+template <class F>
+inline void ensure_lds_attr(F* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  if (done.insert({(const void*)fn, dev}).second)
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
 
 // One entry of the device page table.  Built on the host from
 // ColumnMeta.pages (src/lib.rs:40-80): byte_off is the running sum of

@@ -10,6 +10,7 @@
 
 #include "../../include/strawboat_gpu.h"
 #include "sb_encode.h"
+#include "sb_lz4c.h"
 
 using sb::enc::Opts;
 
@@ -36,6 +37,17 @@ extern "C" {
 void sb_free(void* p) { std::free(p); }
 
 uint64_t sb_page_seed(uint64_t seed, uint64_t page) { return sb::enc::page_seed(seed, page); }
+
+// The device encoder's block compressors (sb_lz4c.h), run on the host.
+uint64_t sb_lz4_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst) {
+  std::vector<uint8_t> table(sbc::kLz4TableBytes, 0);
+  return sbc::lz4_compress(src, (uint32_t)n, dst, table.data());
+}
+
+uint64_t sb_snappy_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst) {
+  std::vector<uint8_t> table(sbc::kSnappyTableBytes);
+  return sbc::snappy_compress(src, (uint32_t)n, dst, table.data());
+}
 
 sb_status sb_encode_page(int32_t phys, const void* h_values, const uint8_t* h_validity, uint64_t n, int32_t nullable,
                          const sb_write_options* opts, uint64_t seed, uint8_t** h_out, uint64_t* out_len) {

@@ -19,7 +19,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native as N
-from .read import Context, PageMeta, default_context, physical_type, _as_device_bytes
+from .read import Context, PageMeta, resolve_context, physical_type, _as_device_bytes
 
 
 class ListDescC(ctypes.Structure):
@@ -94,7 +94,7 @@ class ListColumnDecoder:
         import torch
 
         self._torch = torch
-        self.ctx = ctx or default_context()
+        self.ctx = resolve_context(ctx, chunk)
         self.dtype = np.dtype(dtype)
         self.list_nullable, self.item_nullable = bool(list_nullable), bool(item_nullable)
         self.offset_width = 8 if large else 4

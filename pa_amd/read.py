@@ -152,17 +152,40 @@ class Context:
 _default_ctx = {}
 
 
-def default_context(device: int = 0) -> Context:
+def default_context(device: Optional[int] = None) -> Context:
+    """The shared context of `device` (default: torch's current device)."""
+    if device is None:
+        import torch
+
+        device = torch.cuda.current_device()
     if device not in _default_ctx:
         _default_ctx[device] = Context(device)
     return _default_ctx[device]
+
+
+def resolve_context(ctx: Optional[Context], data=None) -> Context:
+    """ctx as given, else the default context of the device `data` (a tensor)
+    lives on, else of torch's current device.  A device tensor on another
+    device than ctx is an argument error: the kernels would read it through
+    a peer mapping and write their outputs on the wrong GPU."""
+    import torch
+
+    dev = data.device.index if isinstance(data, torch.Tensor) and data.is_cuda else None
+    if ctx is None:
+        return default_context(dev)
+    if dev is not None and dev != ctx.device:
+        raise N.StrawboatError(N.E_ARG, f"tensor on cuda:{dev} but context on cuda:{ctx.device}")
+    return ctx
 
 
 def _as_device_bytes(chunk, device):
     import torch
 
     if isinstance(chunk, torch.Tensor):
-        assert chunk.dtype == torch.uint8 and chunk.is_cuda
+        if chunk.dtype != torch.uint8 or not chunk.is_cuda:
+            raise N.StrawboatError(N.E_ARG, "column chunk must be a uint8 device tensor or host bytes")
+        if chunk.device.index != device:
+            raise N.StrawboatError(N.E_ARG, f"chunk on cuda:{chunk.device.index} but context on cuda:{device}")
         return chunk.contiguous()
     arr = np.frombuffer(bytes(chunk), dtype=np.uint8)
     return torch.from_numpy(arr.copy()).to(f"cuda:{device}")
@@ -178,7 +201,7 @@ class ColumnDecoder:
                  timing: bool = False):
         import torch
 
-        self.ctx = ctx or default_context()
+        self.ctx = resolve_context(ctx, chunk)
         self.dtype = np.dtype(dtype)
         self.nullable = bool(nullable)
         self.chunk = _as_device_bytes(chunk, self.ctx.device)

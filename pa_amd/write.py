@@ -94,10 +94,10 @@ def encode_column_device(values, validity=None, nullable: bool = False, options:
     encode_column with the same options."""
     import torch
 
-    from .read import default_context
+    from .read import resolve_context
 
     options = options or WriteOptions()
-    ctx = ctx or default_context()
+    ctx = resolve_context(ctx, values)
     tdt = {torch.int8: np.int8, torch.int16: np.int16, torch.int32: np.int32, torch.int64: np.int64,
            torch.uint8: np.uint8, torch.uint16: np.uint16, torch.uint32: np.uint32, torch.uint64: np.uint64,
            torch.float32: np.float32, torch.float64: np.float64}[values.dtype]
@@ -106,14 +106,17 @@ def encode_column_device(values, validity=None, nullable: bool = False, options:
     n = values.numel()
     vb = None
     if nullable:
-        v = validity.to(torch.bool).reshape(-1)
+        # a missing bitmap is all-valid (write_def_levels' (is_optional, None) case), as in encode_column
+        v = (validity.to(device=values.device, dtype=torch.bool).reshape(-1) if validity is not None
+             else torch.ones(n, dtype=torch.bool, device=values.device))
         pad = (-n) % 8
         if pad:
             v = torch.cat([v, torch.zeros(pad, dtype=torch.bool, device=v.device)])
         w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=v.device)
         vb = (v.view(-1, 8).to(torch.uint8) * w).sum(1, dtype=torch.uint8) if n else torch.zeros(1, dtype=torch.uint8,
                                                                                                  device=v.device)
-    P = options.max_page_size or n
+    # page_size = max_page_size.unwrap_or(len).min(len) (write/common.rs:54-58)
+    P = min(options.max_page_size or n, n)
     cap = N.lib().sb_encode_device_bound(phys, n, int(nullable), P)
     out = torch.empty(max(cap, 16), dtype=torch.uint8, device=values.device)
     npages = (n + P - 1) // P if n else 0

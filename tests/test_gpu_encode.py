@@ -97,11 +97,29 @@ def test_config1_int64_none(ctx):
 
 
 def test_unsupported_options_are_nyi(ctx):
+    """Zstd as the default codec (libzstd's compressor is not restated on the
+    device) and adaptive pages over 16384 rows report NotYetImplemented."""
     import pa_amd
 
-    tv = torch.arange(1024, dtype=torch.int32, device="cuda")
-    for opts in (pa_amd.WriteOptions(default_compress_ratio=1.2), pa_amd.WriteOptions(default_compression=1),
-                 pa_amd.WriteOptions(forced_codec=10)):
+    tv = torch.arange(40000, dtype=torch.int32, device="cuda")
+    for opts in (pa_amd.WriteOptions(default_compression=2), pa_amd.WriteOptions(default_compression=2,
+                                                                                  default_compress_ratio=1.2),
+                 pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=20000)):
         with pytest.raises(pa_amd.StrawboatError) as e:
             pa_amd.encode_column_device(tv, None, False, opts, ctx=ctx)
         assert e.value.status == 2
+
+
+def test_page_size_clamped_and_missing_validity(ctx):
+    """max_page_size larger than the column (or None) is clamped to the
+    column length (write/common.rs:54-58); nullable with no bitmap = all valid."""
+    import pa_amd
+
+    rng = np.random.default_rng(8)
+    v = rng.integers(0, 1000, 3000).astype(np.int32)
+    for mp in (None, 100000):
+        roundtrip(ctx, v, np.ones(len(v), bool), False, pa_amd.WriteOptions(max_page_size=mp, **BP))
+    host, hm = pa_amd.encode_column(v, None, True, pa_amd.WriteOptions(max_page_size=1024))
+    dev, dm = pa_amd.encode_column_device(torch.from_numpy(v).cuda(), None, True,
+                                          pa_amd.WriteOptions(max_page_size=1024), ctx=ctx)
+    assert dev.cpu().numpy().tobytes() == host
