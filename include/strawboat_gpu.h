@@ -273,21 +273,40 @@ uint64_t sb_page_seed(uint64_t seed, uint64_t page);
  * Return the compressed size. */
 uint64_t sb_lz4_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst);
 uint64_t sb_snappy_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst);
-/* encode_chunk on the device (HIP, gfx950) for the options whose codec choice
- * needs no trial compression: default_compress_ratio None (has_ratio = 0),
- * default codec None, forced codec none or Bitpacking.  Pages of Int32 /
- * UInt32 take Bitpacking when forced and eligible (all values >= 0, length a
- * multiple of 128: bp.rs:92-100), every other page Compression::None --
- * byte-identical to sb_encode_column with the same options.  d_values /
- * d_validity (column LSB bitmap) / d_out are device memory; d_out holds at
- * least sb_encode_device_bound() bytes; page p is rows [p*P, (p+1)*P), P =
- * max_page_rows <= 16384 and a multiple of 128 unless it covers every row.
- * Synchronizes the context's stream.  Other options: SB_E_NYI. */
+/* encode_chunk on the device (HIP, gfx950), byte-identical to
+ * sb_encode_column with the same options: the adaptive cascade
+ * (compress_integer / compress_double / compress_boolean with the seeded
+ * trial-window sampler, forced codecs, Dict / Freq cascades, Patas) and the
+ * Basic codecs None / LZ4 / Snappy run on the GPU; a Zstd default codec that a
+ * page needs reports SB_E_NYI (libzstd's compressor is not restated).
+ * Options with ratio None + default None (+ forced Bitpacking) take a
+ * dedicated sizing/assembly fast path.  d_values (Boolean: the column's LSB
+ * bitmap) / d_validity (column LSB bitmap) / d_out are device memory; d_out
+ * holds at least sb_encode_device_bound() bytes; page p is rows
+ * [p*P, (p+1)*P), P = min(max_page_rows or n_rows, n_rows) <= 16384.
+ * Synchronizes the context's stream. */
 uint64_t sb_encode_device_bound(int32_t physical_type, uint64_t n_rows, int32_t nullable, uint64_t max_page_rows);
 sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type, const void* d_values, const uint8_t* d_validity,
                                   uint64_t n_rows, int32_t nullable, const sb_write_options* opts,
                                   uint64_t max_page_rows, uint8_t* d_out, uint64_t out_capacity, uint64_t* out_len,
                                   sb_page_meta* h_metas, uint64_t metas_cap, uint64_t* n_pages);
+/* encode_chunk for one Binary / Utf8 leaf on the device: d_offsets holds
+ * n_rows + 1 absolute int64 positions into d_values (values_len bytes, the
+ * array's whole buffer, which the stats and the Extend header use, as
+ * sb_encode_binary_column); d_validity the column's LSB bitmap.  The writer's
+ * full option set runs on the device (compress_binary, binary/mod.rs:26-93:
+ * OneValue / Freq / Dict by ratio or forced, the Dict index stream through the
+ * integer cascade, Basic None / LZ4 / Snappy) except a Zstd default codec
+ * (SB_E_NYI); byte-identical to sb_encode_binary_column.  d_out holds at
+ * least sb_encode_binary_device_bound() bytes.  Synchronizes the stream. */
+uint64_t sb_encode_binary_device_bound(int32_t physical_type, uint64_t n_rows, uint64_t values_len, int32_t nullable,
+                                       uint64_t max_page_rows);
+sb_status sb_encode_binary_column_device(sb_ctx* ctx, int32_t physical_type, const uint8_t* d_values,
+                                         uint64_t values_len, const int64_t* d_offsets, const uint8_t* d_validity,
+                                         uint64_t n_rows, int32_t nullable, const sb_write_options* opts,
+                                         uint64_t max_page_rows, uint8_t* d_out, uint64_t out_capacity,
+                                         uint64_t* out_len, sb_page_meta* h_metas, uint64_t metas_cap,
+                                         uint64_t* n_pages);
 /* NativeWriter::finish (write/writer.rs:128-167) footer bytes. */
 sb_status sb_write_footer(const uint8_t* h_schema, uint64_t schema_len, const uint64_t* h_col_offsets,
                           const uint64_t* h_col_npages, uint64_t n_cols, const sb_page_meta* h_pages,

@@ -40,6 +40,12 @@ def _lib():
         L.sb_plan_values_bytes.restype = U64
         L.sb_decode_binary_planned.argtypes = [P, P, ctypes.POINTER(BinaryOutC)]
         L.sb_decode_binary_planned.restype = I32
+        L.sb_encode_binary_device_bound.argtypes = [I32, U64, U64, I32, U64]
+        L.sb_encode_binary_device_bound.restype = U64
+        L.sb_encode_binary_column_device.argtypes = [P, I32, P, U64, P, P, U64, I32, ctypes.POINTER(N.WriteOptionsC), U64,
+                                                     P, U64, ctypes.POINTER(U64), ctypes.POINTER(N.PageMetaC), U64,
+                                                     ctypes.POINTER(U64)]
+        L.sb_encode_binary_column_device.restype = I32
         L._bin_ready = True
     return L
 
@@ -73,6 +79,49 @@ def encode_binary_column(values: bytes, offsets: np.ndarray, validity=None, null
     pm = [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
     L.sb_free(metas)
     return _take(out, olen.value), pm
+
+
+def encode_binary_column_device(values, offsets, validity=None, nullable: bool = False, options=None,
+                                physical_type: int = UTF8, ctx: Optional[Context] = None):
+    """encode_chunk for one Binary / Utf8 leaf on the GPU
+    (sb_encode_binary_column_device): values = the array's whole values buffer
+    (device uint8 tensor), offsets = n + 1 absolute positions (device int64
+    tensor), validity an optional device bool tensor.  Returns (device uint8
+    chunk, page metas), byte-identical to encode_binary_column."""
+    import torch
+
+    from .write import WriteOptions
+
+    L = _lib()
+    options = options or WriteOptions()
+    ctx = resolve_context(ctx, values)
+    offsets = offsets.to(dtype=torch.int64).contiguous()
+    values = values.contiguous()
+    n = offsets.numel() - 1
+    vb = None
+    if nullable:
+        v = (validity.to(device=offsets.device, dtype=torch.bool).reshape(-1) if validity is not None
+             else torch.ones(n, dtype=torch.bool, device=offsets.device))
+        pad = (-n) % 8
+        if pad:
+            v = torch.cat([v, torch.zeros(pad, dtype=torch.bool, device=v.device)])
+        w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=v.device)
+        vb = (v.view(-1, 8).to(torch.uint8) * w).sum(1, dtype=torch.uint8) if n else torch.zeros(
+            1, dtype=torch.uint8, device=v.device)
+    P = min(options.max_page_size or n, n)
+    cap = L.sb_encode_binary_device_bound(physical_type, n, values.numel(), int(nullable), P)
+    out = torch.empty(max(cap, 16), dtype=torch.uint8, device=offsets.device)
+    npages = (n + P - 1) // P if n else 0
+    metas = (N.PageMetaC * max(npages, 1))()
+    olen, npg = ctypes.c_uint64(), ctypes.c_uint64()
+    opts = options.c()
+    st = L.sb_encode_binary_column_device(
+        ctx._h, physical_type, ctypes.c_void_p(values.data_ptr()), values.numel(), ctypes.c_void_p(offsets.data_ptr()),
+        None if vb is None else ctypes.c_void_p(vb.data_ptr()), n, int(nullable), ctypes.byref(opts), P,
+        ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(olen), metas, max(npages, 1), ctypes.byref(npg))
+    if st:
+        raise N.StrawboatError(st, "encode_binary_column_device: " + ctx.error())
+    return out[: olen.value], [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
 
 
 class BinaryColumnDecoder:

@@ -40,6 +40,17 @@ void* ctx_scratch(sb_ctx* c, size_t bytes, int slot) {
   }
   return c->scr[slot];
 }
+int ctx_fail(sb_ctx* c, int st, const char* what, int hip_error) {
+  if (c) {
+    c->err = what;
+    const hipError_t e = hip_error >= 0 ? (hipError_t)hip_error : hipGetLastError();
+    if (e != hipSuccess) {
+      c->err += ": ";
+      c->err += hipGetErrorString(e);
+    }
+  }
+  return st;
+}
 }  // namespace sb
 
 struct sb_plan {

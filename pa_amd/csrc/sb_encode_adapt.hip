@@ -287,9 +287,9 @@ __device__ __forceinline__ uint32_t tab_slots(uint32_t n) {
   while (s < 2 * n) s <<= 1;
   return s;
 }
-template <class KeyF>
-__device__ __forceinline__ uint32_t tab_insert(uint32_t* tab, uint32_t S, uint32_t r, uint64_t k, KeyF key) {
-  uint32_t h = (uint32_t)(mix64(k) >> 32) & (S - 1);
+template <class Same>
+__device__ __forceinline__ uint32_t tab_insert_h(uint32_t* tab, uint32_t S, uint32_t r, uint64_t hv, Same same) {
+  uint32_t h = (uint32_t)(hv >> 32) & (S - 1);
   for (;;) {
     uint32_t e = tab[h];
     if (e == 0) {
@@ -298,7 +298,7 @@ __device__ __forceinline__ uint32_t tab_insert(uint32_t* tab, uint32_t S, uint32
       e = prev;
     }
     const uint32_t o = (e & 0xFFFFu) - 1;
-    if (key(o) == k) {
+    if (same(o)) {
       uint32_t old = atomicAdd(&tab[h], 1u << 16) + (1u << 16);
       while ((old & 0xFFFFu) > r + 1) {  // keep the smallest row
         const uint32_t prev = atomicCAS(&tab[h], old, (old & 0xFFFF0000u) | (r + 1));
@@ -311,13 +311,8 @@ __device__ __forceinline__ uint32_t tab_insert(uint32_t* tab, uint32_t S, uint32
   }
 }
 template <class KeyF>
-__device__ __forceinline__ uint32_t tab_find(const uint32_t* tab, uint32_t S, uint64_t k, KeyF key) {
-  uint32_t h = (uint32_t)(mix64(k) >> 32) & (S - 1);
-  for (;;) {
-    const uint32_t e = tab[h];
-    if (e == 0 || key((e & 0xFFFFu) - 1) == k) return h;
-    h = (h + 1) & (S - 1);
-  }
+__device__ __forceinline__ uint32_t tab_insert(uint32_t* tab, uint32_t S, uint32_t r, uint64_t k, KeyF key) {
+  return tab_insert_h(tab, S, r, mix64(k), [&](uint32_t o) { return key(o) == k; });
 }
 
 // ---------------------------------------------------------------------------
@@ -923,7 +918,19 @@ struct AdArgs {
   uint8_t* out;
   uint64_t out_cap;
   uint32_t n_pages;
+  // Binary / Utf8 columns
+  const int64_t* offsets;   // n_rows + 1 absolute positions into values
+  uint64_t parent_len;      // the array's whole values length (stats and the Extend header)
+  int ow;                   // offset width 4 / 8
+  const uint64_t* slot_offs;  // per page of the batch: slot start (variable slots), [n_batch] = end
 };
+
+__device__ __forceinline__ uint8_t* slot_of(const AdArgs& A, uint32_t b) {
+  return A.slot_offs ? A.slots + A.slot_offs[b] : A.slots + (uint64_t)b * A.slot_bytes;
+}
+__device__ __forceinline__ uint64_t slot_cap(const AdArgs& A, uint32_t b) {
+  return A.slot_offs ? A.slot_offs[b + 1] - A.slot_offs[b] : A.slot_bytes;
+}
 
 __device__ __forceinline__ uint64_t page_seed(uint64_t seed, uint64_t page) {  // sb_encode.cpp page_seed
   uint64_t s = seed ^ (page * 0xD1B54A32D192ED03ull);
@@ -939,6 +946,137 @@ __device__ __forceinline__ uint32_t uleb_len(uint64_t h) {
   return l;
 }
 
+// write_validity (serialize.rs:200-215): u32 def_len + ULEB128 bit-packed run
+// header + the page's validity bitmap; returns its length (0 when not nullable).
+__device__ uint32_t write_prefix(Ctx& c, const AdArgs& A, uint64_t r0, uint32_t n) {
+  if (!A.nullable) return 0;
+  const uint32_t tid = threadIdx.x;
+  const bool has_vb = A.validity != nullptr;
+  const uint32_t nb = (n + 7) / 8;
+  uint64_t h = ((uint64_t)nb << 1) | 1;
+  const uint32_t hl = uleb_len(h);
+  if (tid == 0) {
+    put8(c.out, hl + nb, 4);
+    for (uint32_t j = 0; j < hl; j++, h >>= 7) c.out[4 + j] = (uint8_t)((h & 0x7F) | (j + 1 < hl ? 0x80 : 0));
+  }
+  for (uint32_t j = tid; j < nb; j += NT) {
+    uint32_t v = 0;
+    for (uint32_t b = 0; b < 8; b++) {
+      const uint32_t i = 8 * j + b;
+      const bool ok = i < n && (!has_vb || ((A.validity[(r0 + i) >> 3] >> ((r0 + i) & 7)) & 1));
+      v |= (ok ? 1u : 0u) << b;
+    }
+    c.out[4 + hl + j] = (uint8_t)v;
+  }
+  return 4 + hl + nb;
+}
+
+__device__ void ctx_init(Ctx& c, Sh& sh, const AdArgs& A, uint32_t p) {
+  c.work = nullptr;
+  c.work_bytes = A.work_bytes;
+  c.scratch = A.scratch + (uint64_t)blockIdx.x * A.scratch_bytes;
+  c.nmax = A.P;
+  c.out = slot_of(A, blockIdx.x);
+  c.cap = (uint32_t)min<uint64_t>(slot_cap(A, blockIdx.x), 0xFFFFFFFFull);
+  c.o = A.o;
+  if (threadIdx.x == 0) {
+    sh.err = 0;
+    sh.rng = page_seed(A.seed, p);
+  }
+  __syncthreads();
+}
+
+// Boolean pages: compress_boolean (compression/boolean/mod.rs:22-61) with
+// choose_compressor (:222-280) -- forced RLE, else OneValue / RLE by ratio,
+// the RLE ratio from compress_sample_ratio (:282-321: total bytes n / 8, or
+// 80 for the 640-row sample) -- RLE over the bits as u8 values
+// (boolean/rle.rs:31-39), OneValue (one_value.rs:44-52) or the Basic codecs
+// over the page's bitmap bytes (the parent's bytes when the page starts on a
+// byte, a rebuilt zero-padded bitmap otherwise).  The page's bits are staged
+// one byte per row so the integer RLE and sampler serve unchanged.
+__global__ __launch_bounds__(NT) void k_enc_bool(AdArgs A) {
+  extern __shared__ uint32_t lds[];
+  __shared__ Sh sh;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t p = A.page0 + blockIdx.x;
+  const uint64_t r0 = (uint64_t)p * A.P;
+  const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
+  Ctx c;
+  ctx_init(c, sh, A, p);
+  c.work = lds;
+  c.samp = (uint8_t*)lds + A.work_bytes;
+  uint8_t* vals = c.samp + kSample * 8 + kSample / 8 + 16;
+  uint8_t* rebuilt = vals + ((A.P + 15) & ~15u);
+  const uint32_t nb = (n + 7) / 8;
+  for (uint32_t i = tid; i < n; i += NT) vals[i] = (A.values[(r0 + i) >> 3] >> ((r0 + i) & 7)) & 1;
+  __syncthreads();
+  if (r0 & 7)
+    for (uint32_t j = tid; j < nb; j += NT) {
+      uint32_t v = 0;
+      for (uint32_t b = 0; b < 8 && 8 * j + b < n; b++) v |= (uint32_t)vals[8 * j + b] << b;
+      rebuilt[j] = (uint8_t)v;
+    }
+  const bool has_vb = A.nullable && A.validity;
+  uint32_t pos = write_prefix(c, A, r0, n);
+  const Av a{vals, has_vb ? A.validity : nullptr, r0, n};
+  uint32_t t = 0, f = 0;
+  for (uint32_t i = tid; i < n; i += NT)
+    if (valid_at(a, i)) (vals[i] ? t : f)++;
+  const uint32_t T = (uint32_t)bsum(sh, t), F = (uint32_t)bsum(sh, f);
+  const uint32_t fv = first_valid_row(sh, a);
+  if (tid == 0) sh.first_valid = fv;
+  __syncthreads();
+  int codec = A.o.dflt;
+  const uint32_t fm = A.o.forbidden;
+  if (A.o.forced == C_RLE && !(fm & (1u << C_RLE))) {
+    codec = C_RLE;  // check_rle_env
+  } else if (A.o.has_ratio) {
+    double maxr = A.o.ratio;
+    const int cands[2] = {C_ONE, C_RLE};
+    for (int k = 0; k < 2; k++) {
+      const int cd = cands[k];
+      if (fm & (1u << cd)) continue;
+      double r;
+      if (cd == C_ONE) {
+        r = (T == 0 || F == 0) ? (double)n : 0.0;
+      } else if (n / SC <= SS) {
+        r = (double)(n / 8) / (double)rle_body<1, false, false, false>(c, sh, a, 0);
+      } else {
+        const Av smp = take_sample<1>(c, sh, a);
+        r = 80.0 / (double)rle_body<1, false, false, false>(c, sh, smp, 0);
+      }
+      if (r > maxr) {
+        maxr = r;
+        codec = cd;
+        if (r == (double)n) break;
+      }
+    }
+  }
+  const uint32_t body = pos + 9;
+  uint32_t end = body;
+  if (!room(c, sh, (uint64_t)body)) {
+  } else if (codec == C_RLE) {
+    end = body + rle_body<1, false, false, true>(c, sh, a, body);
+  } else if (codec == C_ONE) {
+    if (room(c, sh, (uint64_t)body + 1)) {
+      if (tid == 0) c.out[body] = fv != 0xFFFFFFFFu ? vals[fv - 1] : 0;
+      end = body + 1;
+    }
+  } else if (codec <= C_SNAPPY) {
+    const uint8_t* src = (r0 & 7) ? rebuilt : A.values + r0 / 8;
+    end = body + basic_body(c, sh, codec, src, nb, body);
+  } else {
+    set_err(sh, E_SPEC);
+  }
+  __syncthreads();
+  write_hdr(c, pos, codec, end - body, n);
+  __syncthreads();
+  if (tid == 0) {
+    A.sizes[p] = sh.err ? 0 : end;
+    A.status[p] = sh.err;
+  }
+}
+
 template <int W, bool FLT, bool SGN>
 __global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
   extern __shared__ uint32_t lds[];
@@ -948,46 +1086,316 @@ __global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
   const uint64_t r0 = (uint64_t)p * A.P;
   const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
   Ctx c;
+  ctx_init(c, sh, A, p);
   c.work = lds;
-  c.work_bytes = A.work_bytes;
   c.samp = (uint8_t*)lds + A.work_bytes;
-  c.scratch = A.scratch + (uint64_t)blockIdx.x * A.scratch_bytes;
-  c.nmax = A.P;
-  c.out = A.slots + (uint64_t)blockIdx.x * A.slot_bytes;
-  c.cap = (uint32_t)A.slot_bytes;
-  c.o = A.o;
-  if (tid == 0) {
-    sh.err = 0;
-    sh.rng = page_seed(A.seed, p);
-  }
-  __syncthreads();
-  uint32_t pos = 0;
   const bool has_vb = A.nullable && A.validity;
-  if (A.nullable) {  // write_validity (serialize.rs:200-215): u32 def_len + ULEB128 bit-packed run + bitmap
-    const uint32_t nb = (n + 7) / 8;
-    uint64_t h = ((uint64_t)nb << 1) | 1;
-    const uint32_t hl = uleb_len(h);
-    if (tid == 0) {
-      put8(c.out, hl + nb, 4);
-      for (uint32_t j = 0; j < hl; j++, h >>= 7) c.out[4 + j] = (uint8_t)((h & 0x7F) | (j + 1 < hl ? 0x80 : 0));
-    }
-    for (uint32_t j = tid; j < nb; j += NT) {
-      uint32_t v = 0;
-      for (uint32_t b = 0; b < 8; b++) {
-        const uint32_t i = 8 * j + b;
-        const bool ok = i < n && (!has_vb || ((A.validity[(r0 + i) >> 3] >> ((r0 + i) & 7)) & 1));
-        v |= (ok ? 1u : 0u) << b;
-      }
-      c.out[4 + hl + j] = (uint8_t)v;
-    }
-    pos = 4 + hl + nb;
-  }
+  uint32_t pos = write_prefix(c, A, r0, n);
   const Av a{A.values + r0 * W, has_vb ? A.validity : nullptr, r0, n};
   __syncthreads();
   pos = enc_stream<W, FLT, SGN, 0>(c, sh, a, A.o.forbidden, pos);
   __syncthreads();
   if (tid == 0) {
     A.sizes[p] = sh.err ? 0 : pos;
+    A.status[p] = sh.err;
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Binary / Utf8 pages: compress_binary (compression/binary/mod.rs:26-93) --
+// gen_stats (:265-300: distinct strings over every slot, nulls, the bytes of
+// the distinct strings + 8 each, the most frequent string), choose_compressor
+// (:302-348: forced Freq / Dict, else OneValue / Freq / Dict by ratio), Dict
+// (dict.rs:55-93: ids by first occurrence over valid rows, row 0's raw bytes
+// when it is null; the u32 index stream cascades), Freq (freq.rs:44-100:
+// top string, roaring of the differing valid rows, u64 len + bytes records),
+// OneValue (one_value.rs:50-68), Basic (offsets rebased to 0 + values, two
+// headered streams).  Strings are compared by a per-row 64-bit hash, then
+// by length and bytes.
+// ---------------------------------------------------------------------------
+struct Strs {
+  const uint8_t* v;    // the column's values
+  const int64_t* off;  // the page's rows: absolute positions off[0..n]
+  const uint64_t* hsh;
+  __device__ __forceinline__ uint64_t at(uint32_t r) const { return (uint64_t)off[r]; }
+  __device__ __forceinline__ uint32_t len(uint32_t r) const { return (uint32_t)(off[r + 1] - off[r]); }
+  __device__ bool eq(uint32_t a, uint32_t b) const {
+    if (hsh[a] != hsh[b]) return false;
+    const uint32_t l = len(a);
+    if (l != len(b)) return false;
+    const uint8_t* x = v + at(a);
+    const uint8_t* y = v + at(b);
+    for (uint32_t i = 0; i < l; i++)
+      if (x[i] != y[i]) return false;
+    return true;
+  }
+};
+
+__device__ __forceinline__ uint64_t str_hash(const uint8_t* p, uint32_t n) {  // FNV-1a 64
+  uint64_t h = 1469598103934665603ull;
+  for (uint32_t i = 0; i < n; i++) {
+    h ^= p[i];
+    h *= 1099511628211ull;
+  }
+  return mix64(h ^ n);
+}
+
+// records of rows (u64 len + bytes) at out + pos in the given row order;
+// returns the bytes written
+template <class RowF>
+__device__ uint32_t put_records(Ctx& c, Sh& sh, const Strs& S, uint32_t cnt, RowF row, uint32_t pos) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < cnt; t0 += NT) {
+    const uint32_t j = t0 + tid;
+    const uint32_t r = j < cnt ? row(j) : 0u;
+    const uint32_t l = j < cnt ? S.len(r) : 0u;
+    uint32_t tot;
+    const uint32_t ex = bscan(sh, j < cnt ? 8 + l : 0u, &tot);
+    if (j < cnt) {
+      if ((uint64_t)pos + carry + ex + 8 + l <= c.cap) {
+        uint8_t* o = c.out + pos + carry + ex;
+        put8(o, l, 8);
+        const uint8_t* x = S.v + S.at(r);
+        for (uint32_t i = 0; i < l; i++) o[8 + i] = x[i];
+      } else {
+        set_err(sh, E_CAP);
+      }
+    }
+    carry += tot;
+  }
+  __syncthreads();
+  return carry;
+}
+
+template <int OW>
+__global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
+  extern __shared__ uint32_t lds[];
+  __shared__ Sh sh;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t p = A.page0 + blockIdx.x;
+  const uint64_t r0 = (uint64_t)p * A.P;
+  const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
+  Ctx c;
+  ctx_init(c, sh, A, p);
+  c.work = lds;
+  c.samp = (uint8_t*)lds + A.work_bytes;
+  uint32_t* idx = (uint32_t*)c.scratch;  // region 0: ids, then rows of ids
+  uint32_t* row_of = idx + A.P;
+  uint64_t* hsh = (uint64_t*)(c.scratch + (uint64_t)2 * A.P * 8);
+  uint8_t* obuf = c.scratch + (uint64_t)3 * A.P * 8;  // rebased offsets for a compressed Basic page
+  const int64_t base = A.offsets[r0];
+  auto slen = [&](uint32_t r) { return (uint32_t)(A.offsets[r0 + r + 1] - A.offsets[r0 + r]); };
+  auto sptr = [&](uint32_t r) { return A.values + A.offsets[r0 + r]; };
+  const bool has_vb = A.nullable && A.validity;
+  const Av va{nullptr, has_vb ? A.validity : nullptr, r0, n};
+  uint32_t pos = write_prefix(c, A, r0, n);
+  for (uint32_t r = tid; r < n; r += NT) hsh[r] = str_hash(sptr(r), slen(r));
+  __syncthreads();
+  auto same = [&](uint32_t a, uint32_t b) {
+    if (hsh[a] != hsh[b]) return false;
+    const uint32_t l = slen(a);
+    if (l != slen(b)) return false;
+    const uint8_t* x = sptr(a);
+    const uint8_t* y = sptr(b);
+    for (uint32_t i = 0; i < l; i++)
+      if (x[i] != y[i]) return false;
+    return true;
+  };
+  // stats over every row (nulls included)
+  const uint32_t Sl = tab_slots(n);
+  uint32_t* tab = c.work;
+  for (uint32_t i = tid; i < Sl; i += NT) tab[i] = 0;
+  __syncthreads();
+  uint32_t nulls = 0;
+  for (uint32_t r = tid; r < n; r += NT) {
+    tab_insert_h(tab, Sl, r, hsh[r], [&](uint32_t o) { return same(o, r); });
+    nulls += !valid_at(va, r);
+  }
+  __syncthreads();
+  uint32_t uniq = 0;
+  uint64_t best = 0, tu = 0;
+  for (uint32_t i = tid; i < Sl; i += NT) {
+    const uint32_t e = tab[i];
+    if (e) {
+      uniq++;
+      tu += slen((e & 0xFFFFu) - 1) + 8;
+      best = max(best, ((uint64_t)(e >> 16) << 32) | (0xFFFFFFFFu - ((e & 0xFFFFu) - 1)));
+    }
+  }
+  const uint32_t NU = (uint32_t)bsum(sh, nulls), U = (uint32_t)bsum(sh, uniq);
+  const uint64_t TU = bsum(sh, tu), BEST = bmax(sh, best);
+  const uint32_t maxc = (uint32_t)(BEST >> 32), top_row = 0xFFFFFFFFu - (uint32_t)BEST;
+  const uint64_t total_bytes = A.parent_len + (uint64_t)(n + 1) * OW;
+  int codec = A.o.dflt;
+  const uint32_t fm = A.o.forbidden;
+  if (A.o.forced == C_FREQ && !(fm & (1u << C_FREQ))) {
+    codec = C_FREQ;
+  } else if (A.o.forced == C_DICT && !(fm & (1u << C_DICT))) {
+    codec = C_DICT;
+  } else if (A.o.has_ratio) {
+    double maxr = A.o.ratio;
+    const int cands[3] = {C_ONE, C_FREQ, C_DICT};
+    for (int k = 0; k < 3; k++) {
+      const int cd = cands[k];
+      if (fm & (1u << cd)) continue;
+      double r = 0.0;
+      if (cd == C_ONE) {
+        r = U <= 1 ? (double)n : 0.0;
+      } else if (cd == C_FREQ) {
+        if (U > 1) {
+          if ((double)NU / (double)n >= 0.9) r = (double)(n - 1);
+          else if ((double)maxc / (double)n >= 0.9) r = (double)(n - 1);
+        }
+      } else if ((uint64_t)U * 3 < n) {
+        const uint64_t after = TU + (uint64_t)n * (bits_needed(U) / 8) + (uint64_t)n * 2 / 128;
+        r = (double)total_bytes / (double)after;
+      }
+      if (r > maxr) {
+        maxr = r;
+        codec = cd;
+        if (r == (double)n) break;
+      }
+    }
+  }
+  const uint32_t body = pos + 9;
+  uint32_t end = body;
+  uint32_t usize = (uint32_t)A.parent_len;
+  if (!room(c, sh, (uint64_t)body)) {
+  } else if (codec <= C_SNAPPY) {
+    // offsets rebased to the page's first value, then the values (two streams)
+    const uint32_t ob = (n + 1) * OW;
+    uint32_t cs;
+    if (codec == C_NONE) {
+      if (room(c, sh, (uint64_t)body + ob)) {
+        for (uint32_t i = tid; i <= n; i += NT) put8(c.out + body + i * OW, (uint64_t)(A.offsets[r0 + i] - base), OW);
+      }
+      cs = ob;
+    } else {
+      for (uint32_t i = tid; i <= n; i += NT) put8(obuf + i * OW, (uint64_t)(A.offsets[r0 + i] - base), OW);
+      __syncthreads();
+      cs = basic_body(c, sh, codec, obuf, ob, body);
+    }
+    __syncthreads();
+    write_hdr(c, pos, codec, cs, ob);
+    const uint32_t h2 = body + cs;
+    const uint32_t vl = (uint32_t)(A.offsets[r0 + n] - base);
+    if (room(c, sh, (uint64_t)h2 + 9)) {
+      const uint32_t cs2 = basic_body(c, sh, codec, A.values + base, vl, h2 + 9);
+      __syncthreads();
+      write_hdr(c, h2, codec, cs2, vl);
+      end = h2 + 9 + cs2;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      A.sizes[p] = sh.err ? 0 : end;
+      A.status[p] = sh.err;
+    }
+    return;
+  } else if (codec == C_ONE) {
+    const uint32_t fv = first_valid_row(sh, va);
+    const uint32_t l = fv != 0xFFFFFFFFu ? slen(fv - 1) : 0u;
+    if (room(c, sh, (uint64_t)body + 4 + l)) {
+      if (tid == 0) put8(c.out + body, l, 4);
+      for (uint32_t i = tid; i < l; i += NT) c.out[body + 4 + i] = sptr(fv - 1)[i];
+      end = body + 4 + l;
+    }
+  } else if (codec == C_DICT) {
+    auto ins = [&](uint32_t r) { return r == 0 || valid_at(va, r); };
+    for (uint32_t i = tid; i < Sl; i += NT) tab[i] = 0;
+    __syncthreads();
+    for (uint32_t r = tid; r < n; r += NT)
+      if (ins(r)) idx[r] = tab_insert_h(tab, Sl, r, hsh[r], [&](uint32_t o) { return same(o, r); });
+    __syncthreads();
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+      const uint32_t r = t0 + tid;
+      const bool f = r < n && ins(r) && (tab[idx[r]] & 0xFFFFu) == r + 1;
+      uint32_t tot;
+      const uint32_t ex = bscan(sh, f ? 1u : 0u, &tot);
+      if (f) row_of[carry + ex] = r;
+      carry += tot;
+    }
+    const uint32_t k = carry;
+    __syncthreads();
+    for (uint32_t j = tid; j < k; j += NT) tab[idx[row_of[j]]] = (j << 16) | (row_of[j] + 1);
+    __syncthreads();
+    for (uint32_t r = tid; r < n; r += NT)
+      if (ins(r)) idx[r] = tab[idx[r]] >> 16;
+    __syncthreads();
+    uint32_t carry_last = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+      const uint32_t r = t0 + tid;
+      const bool in = r < n && ins(r);
+      uint32_t tmax;
+      const uint32_t incl = bscan_max(sh, in ? r + 1 : 0u, &tmax);
+      const uint32_t last = max(incl, carry_last);
+      if (r < n && !in) idx[r] = idx[last - 1];
+      carry_last = max(carry_last, tmax);
+      __syncthreads();
+    }
+    // the index stream cascades (Dict forbidden) at depth 1 (its scratch: region 1)
+    const Av ia{(const uint8_t*)idx, nullptr, 0, n};
+    const uint32_t p2 = enc_stream<4, false, false, 1>(c, sh, ia, fm | (1u << C_DICT), body);
+    if (!sh.err && room(c, sh, (uint64_t)p2 + 4)) {
+      if (tid == 0) put8(c.out + p2, k, 4);
+      const Strs SS2{A.values, A.offsets + r0, hsh};
+      end = p2 + 4 + put_records(c, sh, SS2, k, [&](uint32_t j) { return row_of[j]; }, p2 + 4);
+    }
+  } else if (codec == C_FREQ) {
+    const bool top_null = (double)NU / (double)n >= 0.9;
+    const uint32_t tl = top_null ? 0u : slen(top_row);
+    uint32_t* bm = c.work;
+    __syncthreads();
+    for (uint32_t i = tid; i < 2048; i += NT) bm[i] = 0;
+    __syncthreads();
+    const uint32_t rpos = body + 8 + tl + 4;
+    const uint32_t data = rpos + 16;
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+      const uint32_t r = t0 + tid;
+      const bool e = r < n && valid_at(va, r) && (top_null || !same(r, top_row));
+      uint32_t tot;
+      const uint32_t ex = bscan(sh, e ? 1u : 0u, &tot);
+      if (e) {
+        const uint32_t j = carry + ex;
+        row_of[j] = r;
+        atomicOr(&bm[r >> 5], 1u << (r & 31));
+        if ((uint64_t)data + 2ull * (j + 1) <= c.cap) put8(c.out + data + 2 * j, r & 0xFFFF, 2);
+      }
+      carry += tot;
+    }
+    const uint32_t e = carry;
+    __syncthreads();
+    const uint32_t bytes = e == 0 ? 8u : (e <= 4096 ? 16 + 2 * e : 16 + 8192u);
+    if (room(c, sh, (uint64_t)rpos + bytes)) {
+      if (tid == 0) {
+        put8(c.out + body, tl, 8);
+        put8(c.out + body + 8 + tl, bytes, 4);
+        put8(c.out + rpos, 12346, 4);
+        put8(c.out + rpos + 4, e ? 1u : 0u, 4);
+        if (e) {
+          put8(c.out + rpos + 8, 0, 2);
+          put8(c.out + rpos + 10, e - 1, 2);
+          put8(c.out + rpos + 12, 16, 4);
+        }
+      }
+      for (uint32_t i = tid; i < tl; i += NT) c.out[body + 8 + i] = sptr(top_row)[i];
+      if (e > 4096)
+        for (uint32_t i = tid; i < 2048; i += NT) put8(c.out + data + 4 * i, bm[i], 4);
+      __syncthreads();
+      const Strs SS2{A.values, A.offsets + r0, hsh};
+      end = rpos + bytes + put_records(c, sh, SS2, e, [&](uint32_t j) { return row_of[j]; }, rpos + bytes);
+    }
+  } else {
+    set_err(sh, E_SPEC);
+  }
+  __syncthreads();
+  write_hdr(c, pos, codec, end - body, usize);
+  __syncthreads();
+  if (tid == 0) {
+    A.sizes[p] = sh.err ? 0 : end;
     A.status[p] = sh.err;
   }
 }
@@ -1029,7 +1437,7 @@ __global__ __launch_bounds__(NT) void k_enc_compact(AdArgs A) {
     if (threadIdx.x == 0) A.status[p] = E_CAP;
     return;
   }
-  const uint8_t* src = A.slots + (uint64_t)blockIdx.x * A.slot_bytes;  // 16-byte aligned
+  const uint8_t* src = slot_of(A, blockIdx.x);  // 16-byte aligned
   uint8_t* dst = A.out + off;
   const uint32_t head = (uint32_t)min<uint64_t>(len, (16 - ((uintptr_t)dst & 15)) & 15);
   for (uint32_t j = threadIdx.x; j < head; j += NT) dst[j] = src[j];
@@ -1103,29 +1511,34 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
     case SB_T_UINT64: w = 8; break;
     case SB_T_FLOAT32: w = 4; flt = true; break;
     case SB_T_FLOAT64: w = 8; flt = true; break;
+    case SB_T_BOOLEAN: w = 1; break;
     default: return SB_E_NYI;
   }
+  const bool is_bool = phys == SB_T_BOOLEAN;
   if (P > sba::kMaxRows) return SB_E_NYI;
-  if (o.dflt == SB_CODEC_ZSTD) return SB_E_NYI;  // libzstd's compressor is not restated on the device
   const uint64_t slot = adaptive_slot_bytes(P, w, nullable);
   const uint64_t scr = (2 * P * 8 + 255) & ~255ull;
   const uint32_t batch = (uint32_t)std::min<uint64_t>(np, 2048);
   const uint32_t work = adaptive_work_bytes(P);
-  const uint32_t lds = work + sba::kSample * 8 + sba::kSample / 8 + 16;
+  uint32_t lds = work + sba::kSample * 8 + sba::kSample / 8 + 16;
+  if (is_bool) lds += (uint32_t)(((P + 15) & ~15ull) + (P + 7) / 8 + 16);  // staged bits + rebuilt bitmap
   uint8_t* slots = (uint8_t*)ctx_scratch(ctx, batch * slot + 256, 0);
   uint8_t* scratch = (uint8_t*)ctx_scratch(ctx, batch * scr, 1);
   uint64_t* meta = (uint64_t*)ctx_scratch(ctx, (2 * np + 2) * 8 + np * 4, 2);
-  if (!slots || !scratch || !meta) return SB_E_DEVICE;
+  if (!slots || !scratch || !meta) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 1");
   hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
   uint64_t* sizes = meta;
   uint64_t* offs = meta + np;  // [np + 1]
   uint32_t* status = (uint32_t*)(meta + 2 * np + 2);
-  if (hipMemsetAsync(offs + np, 0, 8, st) != hipSuccess) return SB_E_DEVICE;
+  if (hipMemsetAsync(offs + np, 0, 8, st) != hipSuccess) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 2");
   for (uint64_t b0 = 0; b0 < np; b0 += batch) {
     sba::AdArgs a{d_values, d_validity, n_rows, (uint32_t)P, (uint32_t)b0, (uint32_t)std::min<uint64_t>(batch, np - b0),
                   nullable, o, opts->seed, slots, slot, scratch, scr, work, sizes, status, offs, d_out, out_cap,
-                  (uint32_t)np};
-    if (flt) {
+                  (uint32_t)np, nullptr, 0, 0, nullptr};
+    if (is_bool) {
+      ensure_lds_attr(sba::k_enc_bool, (int)lds);
+      hipLaunchKernelGGL(sba::k_enc_bool, dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+    } else if (flt) {
       if (w == 4) launch_t<4, true, false>(a, lds, st);
       else launch_t<8, true, false>(a, lds, st);
     } else if (sgn) {
@@ -1141,14 +1554,15 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
     }
     hipLaunchKernelGGL(sba::k_enc_offsets, dim3(1), dim3(sba::NT), 0, st, a);
     hipLaunchKernelGGL(sba::k_enc_compact, dim3(a.n_batch), dim3(sba::NT), 0, st, a);
-    if (hipGetLastError() != hipSuccess) return SB_E_DEVICE;
+    if (const hipError_t e = hipGetLastError(); e != hipSuccess)
+      return ctx_fail(ctx, SB_E_DEVICE, "device encode launch (step 3)", (int)e);
   }
   std::vector<uint64_t> sz(np + 1 + np);
   std::vector<uint32_t> stv(np);
   if (hipMemcpyAsync(sz.data(), sizes, (2 * np + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipMemcpyAsync(stv.data(), status, np * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
-    return SB_E_DEVICE;
+    return ctx_fail(ctx, SB_E_DEVICE, "device encode step 4");
   for (uint64_t p = 0; p < np; p++) {
     if (stv[p] == sba::E_NYI) return SB_E_NYI;
     if (stv[p] == sba::E_CAP) return SB_E_ARG;
@@ -1159,4 +1573,138 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
   return SB_OK;
 }
 
+
+__global__ void k_page_offsets(const int64_t* offs, uint64_t n_rows, uint64_t P, uint64_t np, int64_t* out) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p <= np) out[p] = offs[std::min<uint64_t>(p * P, n_rows)];
+}
+
+// per-page slot of a Binary / Utf8 page of n rows and vl value bytes
+static uint64_t binary_slot_bytes(uint64_t n, uint64_t vl, int ow, int nullable) {
+  const uint64_t pre = nullable ? 4 + 10 + (n + 7) / 8 : 0;
+  return (pre + 256 + 2 * (n + 1) * ow + 32 + stream_bound(n, 4, 1) + 10 * n + 8192 + 3 * vl + 15) & ~15ull;
+}
+
+uint64_t binary_device_bound(uint64_t n_rows, uint64_t values_len, int ow, int nullable, uint64_t P) {
+  if (!P) return 0;
+  const uint64_t pages = (n_rows + P - 1) / P;
+  return pages * binary_slot_bytes(P, 0, ow, nullable) + 3 * values_len + 64;
+}
+
+int encode_binary_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, uint64_t values_len,
+                           const int64_t* d_offsets, const uint8_t* d_validity, uint64_t n_rows, int nullable,
+                           const sb_write_options* opts, uint64_t P, uint8_t* d_out, uint64_t out_cap,
+                           uint64_t* out_len, sb_page_meta* h_metas, uint64_t np) {
+  const int ow = (phys == SB_T_BINARY || phys == SB_T_UTF8) ? 4 : (phys == SB_T_LARGE_BINARY || phys == SB_T_LARGE_UTF8) ? 8 : 0;
+  if (!ow) return SB_E_NYI;
+  if (P > sba::kMaxRows) return SB_E_NYI;
+  hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
+  // value bytes of every page from the offsets at the page boundaries
+  int64_t* d_po = (int64_t*)ctx_scratch(ctx, (np + 1) * 8, 3);
+  if (!d_po) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 5");
+  std::vector<int64_t> po(np + 1);
+  hipLaunchKernelGGL(k_page_offsets, dim3((uint32_t)((np + 256) / 256)), dim3(256), 0, st, d_offsets, n_rows, P, np, d_po);
+  if (hipMemcpyAsync(po.data(), d_po, (np + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return ctx_fail(ctx, SB_E_DEVICE, "device encode step 6");
+  // batches of pages whose slots fit ~1 GiB; slot offsets relative to the batch start
+  std::vector<uint64_t> soff;
+  std::vector<std::pair<uint64_t, uint64_t>> batches;  // (first page, index of its slot_offs)
+  uint64_t acc = 0;
+  for (uint64_t p = 0; p < np; p++) {
+    const uint64_t n = std::min<uint64_t>(P, n_rows - p * P);
+    if (po[p + 1] < po[p]) return SB_E_ARG;
+    const uint64_t sb = binary_slot_bytes(n, (uint64_t)(po[p + 1] - po[p]), ow, nullable);
+    if (batches.empty() || (acc + sb > (1ull << 30) && p > batches.back().first) || p - batches.back().first >= 2048) {
+      if (!batches.empty()) soff.push_back(acc);
+      batches.push_back({p, soff.size()});
+      acc = 0;
+    }
+    soff.push_back(acc);
+    acc += sb;
+  }
+  soff.push_back(acc);
+  uint64_t max_batch = 0;
+  for (size_t b = 0; b < batches.size(); b++) {
+    const uint64_t end = b + 1 < batches.size() ? soff[batches[b + 1].second - 1] : soff.back();
+    max_batch = std::max(max_batch, end);
+  }
+  const uint64_t scr = (32 * P + 64 + 255) & ~255ull;
+  const uint32_t work = adaptive_work_bytes(P);
+  const uint32_t lds = work + sba::kSample * 8 + sba::kSample / 8 + 16;
+  uint8_t* slots = (uint8_t*)ctx_scratch(ctx, max_batch + 256, 0);
+  const uint32_t maxn = (uint32_t)std::min<uint64_t>(np, 2048);
+  uint8_t* scratch = (uint8_t*)ctx_scratch(ctx, maxn * scr, 1);
+  uint64_t* meta = (uint64_t*)ctx_scratch(ctx, (2 * np + 2) * 8 + np * 4 + 8 + soff.size() * 8, 2);
+  if (!slots || !scratch || !meta) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 7");
+  uint64_t* sizes = meta;
+  uint64_t* offs = meta + np;
+  uint32_t* status = (uint32_t*)(meta + 2 * np + 2);
+  uint64_t* d_soff = (uint64_t*)((uint8_t*)meta + (2 * np + 2) * 8 + ((np * 4 + 7) & ~7ull));
+  if (hipMemcpyAsync(d_soff, soff.data(), soff.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemsetAsync(offs + np, 0, 8, st) != hipSuccess)
+    return ctx_fail(ctx, SB_E_DEVICE, "device encode step 8");
+  sba::Opts o{opts->default_codec, opts->has_ratio, opts->ratio, opts->forbidden_mask, opts->forced_codec};
+  for (size_t b = 0; b < batches.size(); b++) {
+    const uint64_t b0 = batches[b].first;
+    const uint64_t b1 = b + 1 < batches.size() ? batches[b + 1].first : np;
+    sba::AdArgs a{d_values, d_validity, n_rows, (uint32_t)P, (uint32_t)b0, (uint32_t)(b1 - b0), nullable, o,
+                  opts->seed, slots, 0, scratch, scr, work, sizes, status, offs, d_out, out_cap, (uint32_t)np,
+                  d_offsets, values_len, ow, d_soff + batches[b].second};
+    if (ow == 4) {
+      ensure_lds_attr(sba::k_enc_binary<4>, (int)lds);
+      hipLaunchKernelGGL(sba::k_enc_binary<4>, dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+    } else {
+      ensure_lds_attr(sba::k_enc_binary<8>, (int)lds);
+      hipLaunchKernelGGL(sba::k_enc_binary<8>, dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+    }
+    hipLaunchKernelGGL(sba::k_enc_offsets, dim3(1), dim3(sba::NT), 0, st, a);
+    hipLaunchKernelGGL(sba::k_enc_compact, dim3(a.n_batch), dim3(sba::NT), 0, st, a);
+    if (const hipError_t e = hipGetLastError(); e != hipSuccess)
+      return ctx_fail(ctx, SB_E_DEVICE, "device encode launch (step 9)", (int)e);
+  }
+  std::vector<uint64_t> sz(2 * np + 1);
+  std::vector<uint32_t> stv(np);
+  if (hipMemcpyAsync(sz.data(), sizes, (2 * np + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(stv.data(), status, np * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return ctx_fail(ctx, SB_E_DEVICE, "device encode step 10");
+  for (uint64_t p = 0; p < np; p++) {
+    if (stv[p] == sba::E_NYI) return SB_E_NYI;
+    if (stv[p] == sba::E_CAP) return SB_E_ARG;
+    if (stv[p]) return SB_E_OUT_OF_SPEC;
+  }
+  *out_len = sz[2 * np];
+  for (uint64_t p = 0; p < np; p++) h_metas[p] = sb_page_meta{sz[p], std::min<uint64_t>(P, n_rows - p * P)};
+  return SB_OK;
+}
+
 }  // namespace sb
+
+extern "C" uint64_t sb_encode_binary_device_bound(int32_t physical_type, uint64_t n_rows, uint64_t values_len,
+                                                  int32_t nullable, uint64_t max_page_rows) {
+  const int ow = (physical_type == SB_T_BINARY || physical_type == SB_T_UTF8) ? 4
+                 : (physical_type == SB_T_LARGE_BINARY || physical_type == SB_T_LARGE_UTF8) ? 8 : 0;
+  const uint64_t P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
+  if (!ow) return 0;
+  return sb::binary_device_bound(n_rows, values_len, ow, nullable, P);
+}
+
+extern "C" sb_status sb_encode_binary_column_device(sb_ctx* ctx, int32_t physical_type, const uint8_t* d_values,
+                                                    uint64_t values_len, const int64_t* d_offsets,
+                                                    const uint8_t* d_validity, uint64_t n_rows, int32_t nullable,
+                                                    const sb_write_options* opts, uint64_t max_page_rows,
+                                                    uint8_t* d_out, uint64_t out_capacity, uint64_t* out_len,
+                                                    sb_page_meta* h_metas, uint64_t metas_cap, uint64_t* n_pages) {
+  if (!ctx || !opts || !out_len || !n_pages || (n_rows && (!d_offsets || !d_out)) || (nullable && !d_validity))
+    return SB_E_ARG;
+  const uint64_t P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
+  const uint64_t np = n_rows ? (n_rows + P - 1) / P : 0;
+  *n_pages = np;
+  *out_len = 0;
+  if (np > metas_cap || (!h_metas && np)) return SB_E_ARG;
+  if (!np) return SB_OK;
+  if (hipSetDevice(sb_ctx_device(ctx)) != hipSuccess) return (sb_status)sb::ctx_fail(ctx, SB_E_DEVICE, "hipSetDevice");
+  return (sb_status)sb::encode_binary_adaptive(ctx, physical_type, d_values, values_len, d_offsets, d_validity, n_rows,
+                                               nullable, opts, P, d_out, out_capacity, out_len, h_metas, np);
+}

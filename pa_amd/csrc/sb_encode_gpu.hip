@@ -258,7 +258,8 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
 
 extern "C" uint64_t sb_encode_device_bound(int32_t physical_type, uint64_t n_rows, int32_t nullable,
                                            uint64_t max_page_rows) {
-  const uint64_t w = type_width(physical_type), P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
+  const uint64_t w = physical_type == SB_T_BOOLEAN ? 1 : type_width(physical_type);
+  const uint64_t P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
   if (!w || !P) return 0;
   const uint64_t pages = (n_rows + P - 1) / P;
   // per page: prefix (4 + <= 10 + P/8) + header 9 + max(raw, bitpacked at b = 32)
@@ -273,7 +274,8 @@ extern "C" sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type,
                                              uint64_t out_capacity, uint64_t* out_len, sb_page_meta* h_metas,
                                              uint64_t metas_cap, uint64_t* n_pages) {
   if (!ctx || !opts || !out_len || !n_pages) return SB_E_ARG;
-  const uint32_t w = type_width(physical_type);
+  const bool is_bool = physical_type == SB_T_BOOLEAN;  // d_values = the column's LSB bitmap
+  const uint32_t w = is_bool ? 1 : type_width(physical_type);
   // page_size = max_page_size.unwrap_or(len).min(len) (write/common.rs:54-58)
   const uint64_t P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
   if (!w || (nullable && !d_validity) || (n_rows && (!d_values || !d_out))) return SB_E_ARG;
@@ -289,7 +291,7 @@ extern "C" sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type,
   // option runs the adaptive cascade (sb_encode_adapt.hip).
   const bool forced_bp = opts->forced_codec == SB_CODEC_BITPACKING && !(opts->forbidden_mask & (1u << 14));
   const bool forced_other = opts->forced_codec >= 0 && !forced_bp && !(opts->forbidden_mask & (1u << opts->forced_codec));
-  if (opts->has_ratio || opts->default_codec != SB_CODEC_NONE || forced_other || P > sbe::kMaxPageRows ||
+  if (is_bool || opts->has_ratio || opts->default_codec != SB_CODEC_NONE || forced_other || P > sbe::kMaxPageRows ||
       (P % 128 && P < n_rows) || 2 * P * w + 8192 > sbe::kLds)
     return (sb_status)sb::encode_adaptive(ctx, physical_type, (const uint8_t*)d_values, d_validity, n_rows, nullable,
                                           opts, P, d_out, out_capacity, out_len, h_metas, np);

@@ -14,6 +14,8 @@ namespace sb {
 // Grow-only device scratch owned by a context (slot < 4), reused across calls
 // on its stream; nullptr if the allocation fails.
 void* ctx_scratch(sb_ctx* ctx, size_t bytes, int slot);
+// Records a failure message on the context (sb_last_error) and returns st.
+int ctx_fail(sb_ctx* ctx, int st, const char* what, int hip_error = -1);
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: set it once
 // for each (kernel, current device) pair before the first launch there.

@@ -86,35 +86,44 @@ def encode_column(values: np.ndarray, validity=None, nullable: bool = False,
 
 def encode_column_device(values, validity=None, nullable: bool = False, options: Optional[WriteOptions] = None,
                          ctx=None):
-    """encode_chunk on the GPU (sb_encode_column_device) for the options
-    whose codec choice needs no sampling (ratio None, default codec None,
-    forced codec none or Bitpacking): values is a device tensor of a fixed
-    width type, validity an optional device bool tensor.  Returns (device
-    uint8 tensor of the column chunk, page metas), byte-identical to
-    encode_column with the same options."""
+    """encode_chunk on the GPU (sb_encode_column_device): values is a device
+    tensor of a fixed-width type or bool, validity an optional device bool
+    tensor.  Every option of the reference's writer runs on the device --
+    the adaptive cascade with the seeded sampler, forced codecs, Basic None /
+    LZ4 / Snappy -- except a Zstd default codec (NotYetImplemented).
+    Returns (device uint8 tensor of the column chunk, page metas),
+    byte-identical to encode_column with the same options."""
     import torch
 
     from .read import resolve_context
 
     options = options or WriteOptions()
     ctx = resolve_context(ctx, values)
-    tdt = {torch.int8: np.int8, torch.int16: np.int16, torch.int32: np.int32, torch.int64: np.int64,
-           torch.uint8: np.uint8, torch.uint16: np.uint16, torch.uint32: np.uint32, torch.uint64: np.uint64,
-           torch.float32: np.float32, torch.float64: np.float64}[values.dtype]
-    phys = physical_type(np.dtype(tdt))
     values = values.contiguous()
     n = values.numel()
+
+    def pack(bits):  # bool device tensor -> LSB-first bitmap bytes (at least one byte)
+        pad = (-n) % 8
+        if pad:
+            bits = torch.cat([bits, torch.zeros(pad, dtype=torch.bool, device=bits.device)])
+        w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=bits.device)
+        if not n:
+            return torch.zeros(1, dtype=torch.uint8, device=bits.device)
+        return (bits.view(-1, 8).to(torch.uint8) * w).sum(1, dtype=torch.uint8)
+
+    if values.dtype == torch.bool:  # compress_boolean takes the column's bitmap; pages slice it
+        phys = N.BOOLEAN
+        values = pack(values.reshape(-1))
+    else:
+        tdt = {torch.int8: np.int8, torch.int16: np.int16, torch.int32: np.int32, torch.int64: np.int64,
+               torch.uint8: np.uint8, torch.uint16: np.uint16, torch.uint32: np.uint32, torch.uint64: np.uint64,
+               torch.float32: np.float32, torch.float64: np.float64}[values.dtype]
+        phys = physical_type(np.dtype(tdt))
     vb = None
     if nullable:
         # a missing bitmap is all-valid (write_def_levels' (is_optional, None) case), as in encode_column
-        v = (validity.to(device=values.device, dtype=torch.bool).reshape(-1) if validity is not None
-             else torch.ones(n, dtype=torch.bool, device=values.device))
-        pad = (-n) % 8
-        if pad:
-            v = torch.cat([v, torch.zeros(pad, dtype=torch.bool, device=v.device)])
-        w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=v.device)
-        vb = (v.view(-1, 8).to(torch.uint8) * w).sum(1, dtype=torch.uint8) if n else torch.zeros(1, dtype=torch.uint8,
-                                                                                                 device=v.device)
+        vb = pack(validity.to(device=values.device, dtype=torch.bool).reshape(-1) if validity is not None
+                  else torch.ones(n, dtype=torch.bool, device=values.device))
     # page_size = max_page_size.unwrap_or(len).min(len) (write/common.rs:54-58)
     P = min(options.max_page_size or n, n)
     cap = N.lib().sb_encode_device_bound(phys, n, int(nullable), P)
@@ -128,7 +137,7 @@ def encode_column_device(values, validity=None, nullable: bool = False, options:
         int(nullable), ctypes.byref(opts), P, ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(olen),
         metas, max(npages, 1), ctypes.byref(npg))
     if st:
-        raise N.StrawboatError(st, "encode_column_device")
+        raise N.StrawboatError(st, "encode_column_device: " + ctx.error())
     return out[: olen.value], [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
 
 
