@@ -4,11 +4,15 @@
 Workload (BASELINE.json configs[1]): a non-nullable
 Int32 column of 100M rows in 8192-row pages, written by the engine's writer
 with the reference's adaptive codec choice at default_compress_ratio 1.2
-(write/common.rs:49-119, compression/integer/mod.rs:231-308).  Page data
-is shaped as SURVEY.md §8(d) specifies, so the adaptive choice lands on the
-two codecs the config names: 80 % of pages uniform in [0, 2^b) with b
-cycling 1..24 (-> Bitpacking), 20 % runs of 64-512 copies of random values
-in [0, 2^31) (-> RLE).  The codec of every page is read back and reported.
+(write/common.rs:49-119, compression/integer/mod.rs:231-308).  Page data is
+shaped as SURVEY.md §8(d) specifies: 80 % of pages uniform in [0, 2^b) with
+b cycling 1..24, 20 % runs of 64-512 copies of random values.  The adaptive
+choice then lands on Bitpacking for the uniform pages and on Dict -- not
+RLE -- for the run pages and some low-width pages: with at most 128 distinct
+values Dict's size estimate drops the index bytes to zero (dict.rs:109-120,
+integer division) and its ratio beats RLE's sampled one.  The codec of every
+page is read back and reported (workload "c2_int32_adaptive_bitpack_dict");
+RLE throughput is measured by the c2_hard_mix variant (RLE runs of 2-3).
 
 A "step" = one batched decode of the whole column (compressed pages resident
 in HBM -> Arrow values buffer in HBM).  value = decoded bytes of all ranks /
@@ -16,10 +20,13 @@ max-over-ranks wall time of the timed steps.  Weak scaling: each rank owns a
 100M-row shard (its own page queue, no collectives on the data path).
 
 Also reported: the all-Bitpacking b=12 variant (the north star's >=60 %
-roofline target), a harder C2 mix (b 12..24, RLE runs of 2-3), configs 3-5
-(Float64 + Utf8 under LZ4; List<Int32>; the 64-column mixed table), the
-roofline of the decode kernel from HIP events on the launch stream, and the
-CPU restatement (oracle, 1 thread) on the same column.
+roofline target), the harder C2 mix, configs 3-5 (Float64 + Utf8 under LZ4;
+List<Int32>; the 64-column mixed table, encoded on the GPU and checked byte
+for byte against the host writer), device encode rates, and per config the
+CPU restatement of the reference's src/read decoder (oracle/, the
+reference's algorithms with system liblz4 / libzstd) timed on 1 host thread
+(the reference's shape) and on all the box's cores (pages sharded over
+threads), with the CPU model.
 """
 from __future__ import annotations
 
@@ -143,13 +150,16 @@ def timed(torch, dist, wl: Workload, steps: int, warmup: int):
 
 
 def encode_gpu(torch, pa, rows: int, device: int, threads: int, steps: int) -> dict:
-    """Device page encode (sb_encode_column_device) of the C2 "b12" column with
-    the forced Bitpacking codec and ratio None, and of configs[0]'s Int64 None
-    column: input GB/s per call (values resident in HBM; the call includes its
-    page-table scan and the metas read-back), checked byte for byte against
-    the host writer with the same options."""
+    """Device page encode (sb_encode_column_device): the headline C2 column
+    with the writer's adaptive choice at ratio 1.2 (stats, seeded sampler,
+    Bitpacking / Dict / RLE cascade on the GPU), the C2 "b12" column with the
+    forced Bitpacking codec and ratio None (the sizing + assembly fast path),
+    and configs[0]'s Int64 None column: input GB/s per call (values resident
+    in HBM; the call includes its page-table scan and the metas read-back),
+    checked byte for byte against the host writer with the same options."""
     out = {}
-    cases = [("c2_int32_forced_bitpacking", gen_c2(rows, 4242, "b12"), dict(forced_codec=14)),
+    cases = [("c2_int32_adaptive_ratio1.2", gen_c2(rows, 42, "mix"), dict(default_compress_ratio=1.2, seed=42)),
+             ("c2_int32_forced_bitpacking", gen_c2(rows, 4242, "b12"), dict(forced_codec=14)),
              ("c1_int64_none", np.random.default_rng(42).integers(-2**63, 2**63 - 1, 1_000_000, dtype=np.int64), {})]
     for name, v, kw in cases:
         opts = pa.WriteOptions(max_page_size=PAGE_ROWS, **kw)
@@ -194,26 +204,65 @@ def encode_gpu(torch, pa, rows: int, device: int, threads: int, steps: int) -> d
     return out
 
 
-def cpu_baseline(wl: Workload, budget_s: float = 10.0) -> dict:
+def cpu_info() -> dict:
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count()}
+
+
+def cpu_threads() -> int:
+    """The box's CPU share: OMP_NUM_THREADS when set (16 per GPU on the pool),
+    else all CPUs, at most 16."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return env if env > 0 else max(1, min(16, os.cpu_count() or 1))
+
+
+def time_legs(fn, out_bytes: int, budget_s: float = 4.0) -> dict:
+    """fn(threads) decodes the workload once; timed on 1 thread and on the
+    box's CPU share, repeated within budget_s per leg -> GB/s of each."""
+    res = {}
+    for name, th in (("one_thread", 1), ("all_cores", cpu_threads())):
+        t0 = time.perf_counter()
+        fn(th)
+        first = time.perf_counter() - t0
+        reps = max(1, min(20, int(budget_s / max(first, 1e-3))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn(th)
+        dt = (time.perf_counter() - t0) / reps
+        res[name] = {"GBps": round(out_bytes / dt / 1e9, 3), "threads": th, "s_per_pass": round(dt, 4)}
+    return res
+
+
+def cpu_baseline(wl: Workload) -> dict:
+    """The oracle's restatement of read_integer over the headline column:
+    compressed pages in host RAM -> values in host RAM, 1 thread and all cores."""
     from oracle import oracle as O
 
     metas = [(m.length, m.num_values) for m in wl.metas]
-    t0 = time.perf_counter()
-    out, _ = O.read_column(wl.chunk, metas, np.int32)
-    first = time.perf_counter() - t0
-    assert np.array_equal(out, wl.values), "oracle decode mismatch"
-    passes = max(1, min(50, int(math.ceil(budget_s / max(first, 1e-3))) - 1))
-    t0 = time.perf_counter()
-    for _ in range(passes):
-        O.read_column(wl.chunk, metas, np.int32)
-    dt = time.perf_counter() - t0
+    src = np.frombuffer(wl.chunk, np.uint8)
+    out = (np.empty(wl.rows, np.int32), np.zeros(wl.rows // 8 + 2, np.uint8))
+    v, _ = O.mt_read_column(src, metas, np.int32, False, cpu_threads(), out)
+    assert np.array_equal(v[: wl.rows], wl.values), "CPU decode mismatch"
+    legs = time_legs(lambda th: O.mt_read_column(src, metas, np.int32, False, th, out), wl.out_bytes)
+    allc = legs["all_cores"]
     return {
-        "value": round(wl.out_bytes * passes / dt / 1e9, 3),
+        "value": allc["GBps"],
         "unit": "GB/s",
-        "cores": 1,
+        "cores": allc["threads"],
         "kind": "port",
-        "sample": f"oracle/ C restatement of read_integer over the full {wl.rows}-row column, {passes} passes "
-                  f"({dt:.1f} s), 1 thread, compressed pages in host RAM -> values in host RAM",
+        "sample": f"oracle/ C restatement of read_integer over the full {wl.rows}-row column (compressed pages in "
+                  f"host RAM -> values in host RAM), pages sharded over {allc['threads']} threads; the 1-thread leg "
+                  f"is the reference's single-threaded shape",
+        "one_thread": legs["one_thread"],
+        **cpu_info(),
     }
 
 
@@ -297,6 +346,7 @@ class WorkloadC3:
         self.in_bytes = len(self.fchunk) + len(self.schunk)
         nb = (rows + 7) // 8
         self.out_bytes = rows * 8 + nb + 4 * (rows + 1) + len(svals) + nb
+        self.svals_len = len(svals)
         self.exp = (torch.from_numpy(f.view(np.int64)).to(dev), torch.from_numpy(np.packbits(fvalid, bitorder="little")).to(dev),
                     torch.from_numpy(soffs.astype(np.int32)).to(dev), torch.from_numpy(np.frombuffer(svals, np.uint8).copy()).to(dev),
                     torch.from_numpy(np.packbits(svalid, bitorder="little")).to(dev))
@@ -326,6 +376,37 @@ class WorkloadC3:
     @property
     def decs(self):
         return self.fdec + self.sdec
+
+    def cpu_baseline(self) -> dict:
+        """read_double + read_binary of both columns on the host (LZ4 through
+        the system liblz4, as basic.rs:87-91), 1 thread and all cores."""
+        from oracle import oracle as O
+
+        fm = [(m.length, m.num_values) for m in self.fmetas]
+        sm = [(m.length, m.num_values) for m in self.smetas]
+        fsrc, ssrc = np.frombuffer(self.fchunk, np.uint8), np.frombuffer(self.schunk, np.uint8)
+        n = self.rows
+        fo = (np.empty(n, np.float64), np.zeros(n // 8 + 2, np.uint8))
+        so = (np.empty(n + 1, np.int32), np.empty(self.svals_len + 16, np.uint8), np.zeros(n // 8 + 2, np.uint8))
+
+        def run(th):
+            O.mt_read_column(fsrc, fm, np.float64, True, th, fo)
+            O.mt_read_binary_column(ssrc, sm, True, 4, th, self.svals_len + 16, so)
+
+        run(cpu_threads())
+        # the GPU's Arrow buffers against the CPU decoder's, byte for byte (values under nulls included)
+        nb = (n + 7) // 8
+        fv, fm_ = self.fout[0]
+        go, gv, gm = self.sout[0]
+        ok = fv.cpu().numpy().view(np.float64)[:n].tobytes() == fo[0].tobytes()
+        ok &= fm_.cpu().numpy()[:nb].tobytes() == fo[1][:nb].tobytes()
+        ok &= go.cpu().numpy().tobytes() == so[0].tobytes()
+        ok &= gv.cpu().numpy()[: self.svals_len].tobytes() == so[1][: self.svals_len].tobytes()
+        ok &= gm.cpu().numpy()[:nb].tobytes() == so[2][:nb].tobytes()
+        legs = time_legs(run, self.out_bytes)
+        return {"value": legs["all_cores"]["GBps"], "unit": "GB/s", "cores": legs["all_cores"]["threads"],
+                "kind": "port", "one_thread": legs["one_thread"], "gpu_bit_exact_vs_cpu": bool(ok),
+                "sample": "oracle/ read_double + read_binary of both full columns, LZ4 via the system liblz4"}
 
 
 class WorkloadC4:
@@ -363,6 +444,30 @@ class WorkloadC4:
     def step(self, k):
         self.decs[k & 1].decode_async(*self.outs[k & 1])
 
+    def cpu_baseline(self) -> dict:
+        """read_validity_nested + create_list + read_integer over every page on
+        the host (the oracle), 1 thread and all cores."""
+        from oracle import oracle as O
+
+        m = [(x.length, x.num_values) for x in self.metas]
+        src = np.frombuffer(self.chunk, np.uint8)
+        lev = sum(x.num_values for x in self.metas)
+        out = (np.empty(lev + 2, np.int64), np.zeros(lev // 8 + 2, np.uint8), np.empty(lev + 1, np.int32),
+               np.zeros(lev // 8 + 2, np.uint8))
+        r = O.mt_read_list_column(src, m, np.int32, True, True, cpu_threads(), out)
+        # the GPU's buffers against the CPU decoder's, byte for byte (values under null items included)
+        o, lv, v, fv = self.outs[0]
+        R, V = self.rows, self.leaves
+        ok = r[4] == R and r[5] == V
+        ok &= np.array_equal(o.cpu().numpy().astype(np.int64), out[0][: R + 1])
+        ok &= lv.cpu().numpy()[: (R + 7) // 8].tobytes() == out[1][: (R + 7) // 8].tobytes()
+        ok &= v.cpu().numpy()[:V].tobytes() == out[2][:V].tobytes()
+        ok &= fv.cpu().numpy()[: (V + 7) // 8].tobytes() == out[3][: (V + 7) // 8].tobytes()
+        legs = time_legs(lambda th: O.mt_read_list_column(src, m, np.int32, True, True, th, out), self.out_bytes)
+        return {"value": legs["all_cores"]["GBps"], "unit": "GB/s", "cores": legs["all_cores"]["threads"],
+                "kind": "port", "one_thread": legs["one_thread"], "gpu_bit_exact_vs_cpu": bool(ok),
+                "sample": "oracle/ nested page reader over every page of the column"}
+
     def verify(self, torch) -> bool:
         ok = True
         for d, (o, lv, v, fv) in zip(self.decs, self.outs):
@@ -392,15 +497,17 @@ class WorkloadC5:
     -- in 8192-row pages at default_compress_ratio 2.0 (tests/it/io.rs:433),
     each column shaped for a codec of the adaptive cascade (the LZ4 / None
     columns written with that default codec and no ratio); every fourth
-    fixed-width or Boolean column nullable (10 % nulls).  Encoding is the
-    engine's host C++ writer on the host threads (timed and reported; it is
-    not on the GPU).  A step decodes all 64 columns back to back on one
-    stream; each column is checked against its source values."""
+    fixed-width or Boolean column nullable (10 % nulls).  Every column is
+    encoded on the GPU from values resident in HBM (sb_encode_column_device /
+    sb_encode_binary_column_device; timed) and checked byte for byte against
+    the host C++ writer's chunk (timed on the host threads for comparison).
+    A step decodes all 64 device-encoded columns over 4 streams; each column
+    is checked against its source values."""
 
     I32 = ["bp4", "bp8", "bp12", "bp16", "bp20", "runs", "runs", "one", "one", "freq", "freq", "dict", "dict",
            "sorted", "sorted", "sorted"]
     I64 = ["runs"] * 4 + ["dict"] * 4 + ["freq"] * 4 + ["none"] * 4
-    F64 = ["slow", "slow", "dict", "dict", "runs", "runs", "lz4", "lz4"]
+    F64 = ["slow", "patas", "patas", "dict", "runs", "runs", "lz4", "lz4"]
     STR = ["dict", "dict", "freq", "freq", "one", "one", "lz4", "lz4"]
     BOOL = ["runs", "runs", "runs", "one", "one", "none", "none", "none"]
     U32 = ["bp6", "bp10", "bp14", "bp18", "sorted", "sorted", "sorted", "sorted"]
@@ -421,10 +528,17 @@ class WorkloadC5:
             pool = rng.integers(0, 2**31, 500)
             v = pool[rng.integers(0, 500, n)]
             return (v.astype(np.float64) / 7.0).astype(dt) if dt == np.float64 else v.astype(dt)
-        if kind == "sorted":
-            return np.cumsum(rng.integers(0, 100, n)).astype(dt)
-        if kind == "slow":  # slowly varying with repeats (Patas / RLE friendly)
+        if kind == "sorted":  # sorted within each page (the stats are per page): DeltaBitpacking
+            inc = rng.integers(0, 100, n)
+            c = np.cumsum(inc)
+            start = np.repeat(c[::PAGE_ROWS] - inc[::PAGE_ROWS], PAGE_ROWS)[:n]
+            return (c - start).astype(dt)
+        if kind == "slow":  # slowly varying with repeats (Dict / RLE friendly)
             return (1000.0 + np.cumsum(rng.integers(-1, 2, n)) * 0.5).astype(dt)
+        if kind == "patas":  # each value thrice, a small random walk: too many distinct values for Dict,
+            # runs of 3 too short for RLE, equal / near neighbours for Patas (double/patas.rs:37-105)
+            walk = 1000.0 + np.cumsum(rng.integers(1, 64, n // 3 + 1)) * 2.0**-20
+            return np.repeat(walk, 3)[:n].astype(dt)
         if dt == np.bool_:  # "none"
             return rng.random(n) > 0.5
         if dt == np.float64:  # "lz4"
@@ -449,21 +563,21 @@ class WorkloadC5:
     def __init__(self, torch, pa, rows, seed, device, threads):
         rng = np.random.default_rng(seed)
         self.rows = rows
+        self.threads = threads
         dev = f"cuda:{device}"
         specs = ([(np.int32, k) for k in self.I32] + [(np.int64, k) for k in self.I64] +
                  [(np.float64, k) for k in self.F64] + [("utf8", k) for k in self.STR] +
                  [(np.bool_, k) for k in self.BOOL] + [(np.uint32, k) for k in self.U32])
         self.cols = []
+        self.host = []  # (dt, chunk, metas, nullable, values_len) for the CPU baseline
         self.encode_s = 0.0
         self.in_bytes = self.out_bytes = self.raw_bytes = 0
         self.mix = {}
         names = {0: "none", 1: "lz4", 2: "zstd", 3: "snappy", 10: "rle", 11: "dict", 12: "one_value", 13: "freq",
                  14: "bitpacking", 15: "delta_bitpacking", 16: "patas"}
         nb = (rows + 7) // 8
-        # columns spread over 4 streams (GPU_MAX_HW_QUEUES), the LZ4 ones first so each gets its own
         self.ss = StreamSet(torch, pa, device, 4)
-        order = sorted(range(len(specs)), key=lambda i: specs[i][1] != "lz4")
-        home = {ci: self.ss.ctxs[j % 4] for j, ci in enumerate(order)}
+        enc = []  # device encode inputs: (dt, opts, nullable, device tensors)
         for ci, (dt, kind) in enumerate(specs):
             nullable = dt != "utf8" and ci % 4 == 3
             valid = (rng.random(rows) >= 0.1) if nullable else None
@@ -476,33 +590,120 @@ class WorkloadC5:
                 chunk, metas = pa.encode_binary_column(svals, soffs, None, False, opts, physical_type=pa.UTF8,
                                                        n_threads=threads)
                 self.encode_s += time.perf_counter() - t0
-                h = torch.from_numpy(np.frombuffer(chunk, np.uint8).copy()).to(dev)
-                torch.cuda.synchronize()
-                dec = pa.BinaryColumnDecoder(h, metas, pa.UTF8, False, ctx=home[ci])
                 raw = len(svals) + 4 * (rows + 1)
                 exp = (torch.from_numpy(soffs.astype(np.int32)).to(dev),
                        torch.from_numpy(np.frombuffer(svals, np.uint8).copy()).to(dev))
+                enc.append((dt, opts, False, (exp[1], torch.from_numpy(soffs).to(dev), None)))
+                self.host.append((dt, chunk, metas, False, len(svals)))
             else:
                 v = self._values(dt, kind, rows, rng)
                 t0 = time.perf_counter()
                 chunk, metas = pa.encode_column(v, valid, nullable, opts, n_threads=threads)
                 self.encode_s += time.perf_counter() - t0
-                h = torch.from_numpy(np.frombuffer(chunk, np.uint8).copy()).to(dev)
-                torch.cuda.synchronize()
-                dec = pa.ColumnDecoder(h, metas, dt, nullable, ctx=home[ci])
                 raw = nb if dt == np.bool_ else v.nbytes
-                if dt == np.bool_:
-                    ev = torch.from_numpy(v).to(dev)
-                else:
-                    ev = torch.from_numpy(v.view(np.uint8).copy()).to(dev)
-                exp = (ev, None if valid is None else torch.from_numpy(valid).to(dev))
+                tv = torch.from_numpy(v).to(dev)
+                ev = tv if dt == np.bool_ else tv.view(torch.uint8)
+                tvalid = None if valid is None else torch.from_numpy(valid).to(dev)
+                exp = (ev, tvalid)
+                enc.append((dt, opts, nullable, (tv, tvalid)))
+                self.host.append((dt, chunk, metas, nullable, 0))
             for c, k in page_codecs(chunk, metas, nullable).items():
                 self.mix[names.get(c, str(c))] = self.mix.get(names.get(c, str(c)), 0) + k
             self.raw_bytes += raw
             self.out_bytes += raw + (nb if nullable else 0)
             self.in_bytes += len(chunk)
-            self.cols.append((dt, dec, dec.alloc_outputs(), exp))
+            self.cols.append([dt, None, None, exp, chunk, metas, nullable])
         torch.cuda.synchronize()
+        # device encode of every column (values in HBM): a warm-up pass (context
+        # scratch), then a timed pass; byte-identical to the host writer
+        self.encode_gpu_s, self.byte_identical = self._encode_device(torch, pa, enc, device)
+        # decoders over the device-encoded chunks, columns over 4 streams (LZ4 ones first)
+        order = sorted(range(len(specs)), key=lambda i: specs[i][1] != "lz4")
+        home = {ci: self.ss.ctxs[j % 4] for j, ci in enumerate(order)}
+        for ci, col in enumerate(self.cols):
+            dt, chunk_d, metas = col[0], self.dev_chunks[ci], col[5]
+            if dt == "utf8":
+                dec = pa.BinaryColumnDecoder(chunk_d, metas, pa.UTF8, False, ctx=home[ci])
+            else:
+                dec = pa.ColumnDecoder(chunk_d, metas, dt, col[6], ctx=home[ci])
+            col[1], col[2] = dec, dec.alloc_outputs()
+        del self.dev_chunks
+        torch.cuda.synchronize()
+
+    def _encode_device(self, torch, pa, enc, device):
+        ctx = pa.default_context(device)
+        same = True
+        best = None
+        for rep in range(3):
+            chunks = []
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for dt, opts, nullable, t in enc:
+                if dt == "utf8":
+                    c, m = pa.encode_binary_column_device(t[0], t[1], None, False, opts, pa.UTF8, ctx=ctx)
+                else:
+                    c, m = pa.encode_column_device(t[0], t[1], nullable, opts, ctx=ctx)
+                chunks.append((c, m))
+            torch.cuda.synchronize()
+            dt_s = time.perf_counter() - t0
+            if rep:
+                best = dt_s if best is None else min(best, dt_s)
+        for (c, m), col in zip(chunks, self.cols):
+            same &= c.cpu().numpy().tobytes() == col[4]
+            same &= [(x.length, x.num_values) for x in m] == [(x.length, x.num_values) for x in col[5]]
+        self.dev_chunks = [c for c, _ in chunks]
+        return best, bool(same)
+
+    def cpu_baseline(self) -> dict:
+        """Every column's reader on the host (read_integer / read_double /
+        read_boolean / read_binary restated by the oracle), 1 thread and all cores."""
+        from oracle import oracle as O
+
+        n = self.rows
+        jobs, cpu_outs = [], []
+        for dt, chunk, metas, nullable, vlen in self.host:
+            m = [(x.length, x.num_values) for x in metas]
+            src = np.frombuffer(chunk, np.uint8)
+            if dt == "utf8":
+                out = (np.empty(n + 1, np.int32), np.empty(vlen + 16, np.uint8), np.zeros(n // 8 + 2, np.uint8))
+                jobs.append(lambda th, src=src, m=m, out=out, vlen=vlen:
+                            O.mt_read_binary_column(src, m, False, 4, th, vlen + 16, out))
+            elif dt == np.bool_:
+                out = (np.zeros(n // 8 + 2, np.uint8), np.zeros(n // 8 + 2, np.uint8))
+                jobs.append(lambda th, src=src, m=m, out=out, nl=nullable: O.mt_read_bool_column(src, m, nl, th, out))
+            else:
+                out = (np.empty(n, dt), np.zeros(n // 8 + 2, np.uint8))
+                jobs.append(lambda th, src=src, m=m, out=out, nl=nullable, dt=dt:
+                            O.mt_read_column(src, m, dt, nl, th, out))
+            cpu_outs.append(out)
+
+        def run(th):
+            for j in jobs:
+                j(th)
+
+        run(cpu_threads())
+        # every column's GPU buffers against the CPU decoder's, byte for byte (values under nulls included)
+        ok = True
+        nb = (n + 7) // 8
+        for col, cpu, host in zip(self.cols, cpu_outs, self.host):
+            dt, outs = col[0], col[2]
+            if dt == "utf8":
+                vlen = host[4]
+                ok &= outs[0].cpu().numpy().tobytes() == cpu[0].tobytes()
+                ok &= outs[1].cpu().numpy()[:vlen].tobytes() == cpu[1][:vlen].tobytes()
+            elif dt == np.bool_:
+                ok &= outs[0].cpu().numpy()[:nb].tobytes() == cpu[0][:nb].tobytes()
+                if col[6]:
+                    ok &= outs[1].cpu().numpy()[:nb].tobytes() == cpu[1][:nb].tobytes()
+            else:
+                ok &= outs[0].cpu().numpy().view(np.uint8)[: n * np.dtype(dt).itemsize].tobytes() == cpu[0].tobytes()
+                if col[6]:
+                    ok &= outs[1].cpu().numpy()[:nb].tobytes() == cpu[1][:nb].tobytes()
+        legs = time_legs(run, self.out_bytes, budget_s=3.0)
+        return {"value": legs["all_cores"]["GBps"], "unit": "GB/s", "cores": legs["all_cores"]["threads"],
+                "kind": "port", "one_thread": legs["one_thread"], "gpu_bit_exact_vs_cpu": bool(ok),
+                "sample": "oracle/ readers over all 64 columns (compressed pages in host RAM -> Arrow buffers in host "
+                          "RAM), each column's pages sharded over the threads"}
 
     @property
     def decs(self):
@@ -510,14 +711,14 @@ class WorkloadC5:
 
     def step(self, k):
         self.ss.fork()
-        for _, dec, outs, _ in self.cols:
-            dec.decode_async(*outs)
+        for col in self.cols:
+            col[1].decode_async(*col[2])
         self.ss.join()
 
     def verify(self, torch) -> bool:
         ok = True
         n = self.rows
-        for dt, dec, outs, exp in self.cols:
+        for dt, dec, outs, exp, _, _, _ in self.cols:
             dec.check()
             if dt == "utf8":
                 o, v, _ = outs
@@ -587,6 +788,7 @@ def main():
         dist = tdist
     threads = max(1, min(16, (os.cpu_count() or 8) // max(world, 1)))
     pa_amd.default_context(local)
+    do_cpu = world == 1 and not args.no_cpu  # CPU baselines on rank 0 at N=1 only
 
     wl = Workload(torch, pa_amd, args.rows, 42 + rank, "mix", local, threads)
     wall, kern_ms, ok = timed(torch, dist, wl, args.steps, args.warmup)
@@ -643,8 +845,11 @@ def main():
             "compressed_bytes": wl3.in_bytes,
             "decoded_bytes": wl3.out_bytes,
             "bit_exact": bool(ok3),
-            "kernels": "k_decode_staged<8,true> + k_decode_deferred<8,true> (LZ4) + k_bin_decode<4>",
+            "kernels": "Float64: k_decode_staged<8,true> (validity + LZ4 job list) + k_inflate (values); "
+                       "Utf8: k_bin_size<4> + k_bin_scan + k_inflate (offsets + values) + k_bin_decode<4>",
         }
+        if do_cpu:
+            extra["c3_f64_utf8_lz4_nullable"]["cpu_baseline"] = wl3.cpu_baseline()
         del wl3
 
     if not args.no_c4:
@@ -668,8 +873,10 @@ def main():
             "decoded_bytes_per_gpu": wl4.out_bytes,
             "bit_exact": bool(ok4),
             "parallelism": f"page-shard x{world}",
-            "kernels": "k_list_size + k_list_scan + k_list_levels + k_decode_staged<4,false>",
+            "kernels": "k_list_bscan + k_list_levels + k_decode_staged<4,false>",
         }
+        if do_cpu:
+            extra["c4_list_int32_nested"]["cpu_baseline"] = wl4.cpu_baseline()
         del wl4
 
     if not args.no_c5:
@@ -690,11 +897,20 @@ def main():
             "compressed_bytes_per_gpu": wl5.in_bytes,
             "decoded_bytes_per_gpu": wl5.out_bytes,
             "codec_mix_pages": wl5.mix,
+            "encode_gpu_GBps": round(wl5.raw_bytes / wl5.encode_gpu_s / 1e9, 1),
+            "encode_gpu_ms": round(wl5.encode_gpu_s * 1e3, 2),
+            "encode_byte_identical": wl5.byte_identical,
             "encode_host_GBps": round(wl5.raw_bytes / wl5.encode_s / 1e9, 2),
-            "encode": f"host C++ writer, {threads} threads (adaptive ratio 2.0: the device encoder covers ratio-None options only)",
+            "encode": f"all 64 columns encoded on the GPU from values in HBM (adaptive cascade at ratio 2.0, "
+                      f"Basic LZ4 / None; one C-ABI call per column, synchronous); compared byte for byte with "
+                      f"the host C++ writer's chunks ({threads} host threads, encode_host_GBps); the decode "
+                      f"steps read the device-encoded chunks",
+            "raw_bytes": wl5.raw_bytes,
             "bit_exact": bool(ok5),
             "parallelism": f"page-shard x{world} (each rank its own table)",
         }
+        if do_cpu:
+            extra["c5_mixed_64col"]["cpu_baseline"] = wl5.cpu_baseline()
         del wl5
 
     if not args.no_encode:
@@ -715,7 +931,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic (seeded numpy; pages encoded by the engine's writer)",
             "config": {
-                "workload": "c2_int32_adaptive_bitpack_rle",
+                "workload": "c2_int32_adaptive_bitpack_dict",
                 "rows_per_gpu": args.rows,
                 "page_rows": PAGE_ROWS,
                 "pages_per_gpu": len(wl.metas),
@@ -732,14 +948,14 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": load_traffic("c2_int32_adaptive_bitpack_rle"),
+                "traffic": load_traffic("c2_int32_adaptive_bitpack_dict"),
                 "kernel": "k_decode_staged<4,false>",
                 "kernel_ms": round(kavg, 4),
                 "bytes_per_launch": wl.in_bytes + wl.out_bytes,
             },
         }
         line.update(extra)
-        if world == 1 and not args.no_cpu:
+        if do_cpu:
             line["cpu_baseline"] = cpu_baseline(wl)
         print(json.dumps(line), flush=True)
     if dist:

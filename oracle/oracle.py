@@ -483,3 +483,76 @@ def read_bool_column(chunk: bytes, metas, nullable=False):
            "read_bool_column")
     vals = np.unpackbits(vb, bitorder="little")[:n].astype(bool)
     return vals, (np.unpackbits(mb, bitorder="little")[:n].astype(bool) if nullable else None)
+
+
+# ---- multi-threaded CPU baseline (sb_cpu_mt.c) ------------------------------
+def _mt_lib():
+    L = lib()
+    if not getattr(L, "_mt_ready", False):
+        P, S, I, U64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+        L.orc_mt_read_column.argtypes = [P, P, S, I, I, I, P, P, I]
+        L.orc_mt_read_binary_column.argtypes = [P, P, S, I, I, P, P, U64, P, I, ctypes.POINTER(U64)]
+        L.orc_mt_read_list_column.argtypes = [P, P, S, I, I, I, I, P, P, P, P, I, ctypes.POINTER(U64),
+                                              ctypes.POINTER(U64)]
+        L.orc_mt_read_bool_column.argtypes = [P, P, S, I, P, P, I]
+        L._mt_ready = True
+    return L
+
+
+def _metas(metas):
+    return np.asarray([(int(l), int(nv)) for l, nv in metas], dtype=np.uint64).reshape(-1)
+
+
+def mt_read_column(chunk, metas, dtype, nullable, threads, out=None):
+    """read_integer / read_double with the pages sharded over `threads`
+    workers -> (values, validity bytes|None).  `out` = preallocated buffers."""
+    dtype = np.dtype(dtype)
+    n = sum(int(nv) for _, nv in metas)
+    src = chunk if isinstance(chunk, np.ndarray) else np.frombuffer(chunk, np.uint8)
+    vals, bits = out if out is not None else (np.empty(max(n, 1), dtype), np.zeros(n // 8 + 2, np.uint8))
+    m = _metas(metas)
+    _check(_mt_lib().orc_mt_read_column(_ptr(src), _ptr(m), len(metas), int(dtype.kind == "f"), dtype.itemsize,
+                                        int(nullable), _ptr(vals), _ptr(bits), threads), "mt_read_column")
+    return vals, (bits if nullable else None)
+
+
+def mt_read_binary_column(chunk, metas, nullable, ow, threads, values_cap, out=None):
+    """read_binary with pages sharded over workers -> (offsets, values, bits|None, values_len)."""
+    n = sum(int(nv) for _, nv in metas)
+    src = chunk if isinstance(chunk, np.ndarray) else np.frombuffer(chunk, np.uint8)
+    offs, vals, bits = out if out is not None else (np.empty(n + 1, np.int64 if ow == 8 else np.int32),
+                                                    np.empty(max(values_cap, 1), np.uint8),
+                                                    np.zeros(n // 8 + 2, np.uint8))
+    vl = ctypes.c_uint64()
+    m = _metas(metas)
+    _check(_mt_lib().orc_mt_read_binary_column(_ptr(src), _ptr(m), len(metas), int(nullable), ow, _ptr(offs),
+                                               _ptr(vals), len(vals), _ptr(bits), threads, ctypes.byref(vl)),
+           "mt_read_binary_column")
+    return offs, vals, (bits if nullable else None), vl.value
+
+
+def mt_read_list_column(chunk, metas, dtype, list_nullable, item_nullable, threads, out=None):
+    """List<T> batch read with pages sharded over workers ->
+    (offsets int64, list bits|None, values, leaf bits|None, rows, leaves)."""
+    dtype = np.dtype(dtype)
+    lev = sum(int(nv) for _, nv in metas)
+    src = chunk if isinstance(chunk, np.ndarray) else np.frombuffer(chunk, np.uint8)
+    offs, lb, vals, fb = out if out is not None else (np.empty(lev + 2, np.int64), np.zeros(lev // 8 + 2, np.uint8),
+                                                      np.empty(lev + 1, dtype), np.zeros(lev // 8 + 2, np.uint8))
+    r, v = ctypes.c_uint64(), ctypes.c_uint64()
+    m = _metas(metas)
+    _check(_mt_lib().orc_mt_read_list_column(_ptr(src), _ptr(m), len(metas), int(list_nullable), int(item_nullable),
+                                             int(dtype.kind == "f"), dtype.itemsize, _ptr(offs), _ptr(lb), _ptr(vals),
+                                             _ptr(fb), threads, ctypes.byref(r), ctypes.byref(v)),
+           "mt_read_list_column")
+    return offs, (lb if list_nullable else None), vals, (fb if item_nullable else None), r.value, v.value
+
+
+def mt_read_bool_column(chunk, metas, nullable, threads, out=None):
+    n = sum(int(nv) for _, nv in metas)
+    src = chunk if isinstance(chunk, np.ndarray) else np.frombuffer(chunk, np.uint8)
+    vb, mb = out if out is not None else (np.zeros(n // 8 + 2, np.uint8), np.zeros(n // 8 + 2, np.uint8))
+    m = _metas(metas)
+    _check(_mt_lib().orc_mt_read_bool_column(_ptr(src), _ptr(m), len(metas), int(nullable), _ptr(vb), _ptr(mb),
+                                             threads), "mt_read_bool_column")
+    return vb, (mb if nullable else None)

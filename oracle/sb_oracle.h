@@ -163,6 +163,20 @@ int orc_hybrid_decode(const uint8_t* buf, size_t len, uint32_t bit_width, size_t
 int orc_common_decompress(int codec, const uint8_t* in, size_t in_len, uint8_t* out, size_t out_len);
 int orc_common_compress(int codec, const uint8_t* in, size_t in_len, orc_buf* out);
 
+/* ---- multi-threaded CPU baseline (sb_cpu_mt.c): pages sharded over
+ * n_threads contiguous ranges, each decoded by the page readers above ---- */
+int orc_mt_read_column(const uint8_t* chunk, const uint64_t* metas, size_t n_pages, int kind, int width, int nullable,
+                       uint8_t* out_values, uint8_t* out_bits, int n_threads);
+int orc_mt_read_binary_column(const uint8_t* chunk, const uint64_t* metas, size_t n_pages, int nullable, int ow,
+                              uint8_t* out_offsets, uint8_t* out_values, uint64_t values_cap, uint8_t* out_bits,
+                              int n_threads, uint64_t* values_len);
+int orc_mt_read_list_column(const uint8_t* chunk, const uint64_t* metas, size_t n_pages, int list_nullable,
+                            int item_nullable, int kind, int width, int64_t* out_offsets, uint8_t* out_list_bits,
+                            uint8_t* out_values, uint8_t* out_leaf_bits, int n_threads, uint64_t* rows_out,
+                            uint64_t* leaves_out);
+int orc_mt_read_bool_column(const uint8_t* chunk, const uint64_t* metas, size_t n_pages, int nullable,
+                            uint8_t* out_bits, uint8_t* out_valid, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

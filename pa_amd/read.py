@@ -168,9 +168,7 @@ def resolve_context(ctx: Optional[Context], data=None) -> Context:
     lives on, else of torch's current device.  A device tensor on another
     device than ctx is an argument error: the kernels would read it through
     a peer mapping and write their outputs on the wrong GPU."""
-    import torch
-
-    dev = data.device.index if isinstance(data, torch.Tensor) and data.is_cuda else None
+    dev = data.device.index if getattr(data, "is_cuda", False) else None
     if ctx is None:
         return default_context(dev)
     if dev is not None and dev != ctx.device:

@@ -19,7 +19,7 @@ def main():
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     per = warm + steps
     out = {}
-    for i, name in enumerate(["c2_int32_adaptive_bitpack_rle", "c2_hard_mix", "bitpack_b12"]):
+    for i, name in enumerate(["c2_int32_adaptive_bitpack_dict", "c2_hard_mix", "bitpack_b12"]):
         seg = dur[i * per:(i + 1) * per][warm:]
         if seg:
             out[name] = {"kernel": rows[0]["Kernel_Name"], "timed_dispatches": len(seg),
