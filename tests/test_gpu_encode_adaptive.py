@@ -84,12 +84,12 @@ def check(ctx, values, validity, nullable, page_rows, o: dict, seed=42, forbidde
     import pa_amd
 
     opts = pa_opts(o, page_rows, seed, forbidden)
-    if o.get("default_codec") == O.ZSTD:
-        with pytest.raises(pa_amd.StrawboatError) as e:
-            device_encode(ctx, values, validity, nullable, opts)
-        assert e.value.status == 2
+    try:
+        got, metas = device_encode(ctx, values, validity, nullable, opts)
+    except pa_amd.StrawboatError as e:
+        # a page that needs the Zstd Basic codec: NotYetImplemented on the device
+        assert o.get("default_codec") == O.ZSTD and e.status == 2, e
         return set()
-    got, metas = device_encode(ctx, values, validity, nullable, opts)
     host, hmetas = pa_amd.encode_column(values, validity, nullable, opts)
     assert got == host
     assert [(m.length, m.num_values) for m in metas] == [(m.length, m.num_values) for m in hmetas]

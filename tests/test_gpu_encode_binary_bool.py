@@ -75,12 +75,11 @@ def check_binary(ctx, s, validity, nullable, page_rows, o, phys, seed=42):
     tv = torch.from_numpy(np.frombuffer(vals, np.uint8).copy()).cuda()
     to = torch.from_numpy(offs.copy()).cuda()
     tvalid = torch.from_numpy(validity.copy()).cuda() if validity is not None else None
-    if o.get("default_codec") == O.ZSTD:
-        with pytest.raises(pa_amd.StrawboatError) as e:
-            pa_amd.encode_binary_column_device(tv, to, tvalid, nullable, opts, phys, ctx=ctx)
-        assert e.value.status == 2
+    try:
+        dev, dm = pa_amd.encode_binary_column_device(tv, to, tvalid, nullable, opts, phys, ctx=ctx)
+    except pa_amd.StrawboatError as e:  # a page that needs Zstd: NotYetImplemented on the device
+        assert o.get("default_codec") == O.ZSTD and e.status == 2, e
         return
-    dev, dm = pa_amd.encode_binary_column_device(tv, to, tvalid, nullable, opts, phys, ctx=ctx)
     got = dev.cpu().numpy().tobytes()
     host, hm = pa_amd.encode_binary_column(vals, offs, validity, nullable, opts, phys)
     assert [(m.length, m.num_values) for m in dm] == [(m.length, m.num_values) for m in hm]
@@ -139,11 +138,11 @@ def check_bool(ctx, v, validity, nullable, page_rows, o, seed=42):
     opts = pa_opts(o, page_rows, seed)
     tv = torch.from_numpy(v.copy()).cuda()
     tvalid = torch.from_numpy(validity.copy()).cuda() if validity is not None else None
-    if o.get("default_codec") == O.ZSTD:
-        with pytest.raises(pa_amd.StrawboatError):
-            pa_amd.encode_column_device(tv, tvalid, nullable, opts, ctx=ctx)
+    try:
+        dev, dm = pa_amd.encode_column_device(tv, tvalid, nullable, opts, ctx=ctx)
+    except pa_amd.StrawboatError as e:  # a page that needs Zstd: NotYetImplemented on the device
+        assert o.get("default_codec") == O.ZSTD and e.status == 2, e
         return
-    dev, dm = pa_amd.encode_column_device(tv, tvalid, nullable, opts, ctx=ctx)
     got = dev.cpu().numpy().tobytes()
     host, hm = pa_amd.encode_column(v, validity, nullable, opts)
     n = len(v)
