@@ -931,6 +931,45 @@ __device__ uint32_t snappy_wave(WaveWin& w, uint32_t p, uint32_t pend, WaveOut<R
 //     source ends before the batch's first match byte are copied
 //     lane-parallel and the rest in sequence order, wave-wide.
 // The compressed stream is staged by LDS-DMA into a per-wave kIb ring.
+// ---------------------------------------------------------------------------
+// Record chains through a window, wave-parallel.  Variable-length records
+// whose size follows from their own header (Patas records, LZ4 sequences)
+// chain: the next record starts at x + d(x).  Every lane sizes the records
+// that WOULD start at 4 positions of a 255-position window (byte k of lane l
+// = position 4l + k); successor tables T1 = x -> x + d(x) (0xFF past the
+// window or after a record that stops the chain) are doubled by ds_bpermute
+// lookups (T2 = T1 o T1, ..., T32), and lane k composes them along the bits
+// of k: the k-th record's position.  26 permutes per window instead of a
+// scalar chase per record.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t tab_at(uint32_t table, uint32_t x) {  // byte x of the wave-wide table
+  const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x >> 2) << 2), (int)table);
+  return x == 0xFF ? 0xFFu : (w >> ((x & 3) * 8)) & 0xFFu;
+}
+// t1: the packed successor table; returns the k-th record's position in lane k (0xFF: none)
+__device__ __forceinline__ uint32_t wave_chain(uint32_t t1) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t T[6];
+  T[0] = t1;
+#pragma unroll
+  for (int j = 1; j < 6; j++) {
+    uint32_t nt = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t t = (T[j - 1] >> (8 * k)) & 0xFFu;
+      nt |= tab_at(T[j - 1], t) << (8 * k);
+    }
+    T[j] = nt;
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    const uint32_t y = tab_at(T[j], x);
+    if ((lane >> j) & 1) x = y;
+  }
+  return x;
+}
+
 constexpr uint32_t kIb = 4096, kScan = 256, kLitFast = 64, kMatchFast = 32;
 
 struct InRing {
@@ -1081,16 +1120,19 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
       Seq s;
       if (seq_at(in.ib, x, lim, pend, s) && s.next - x <= 255) packed |= (s.next - x) << (8 * k);
     }
-    // 2. chase from p
-    uint32_t q = p, j = 0, starts = 0;
-    while (j < 64 && q - p < kScan) {
-      const uint32_t r = q - p;
-      const uint32_t d = (__builtin_amdgcn_readlane(packed, r >> 2) >> ((r & 3) * 8)) & 0xFFu;
-      if (!d) break;
-      starts = lane == j ? q : starts;
-      q += d;
-      j++;
+    // 2. the chain of sequence starts from p, wave-parallel (wave_chain): a
+    //    candidate with distance 0 (serial path) ends it
+    uint32_t t1 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t r = 4 * lane + k, d = (packed >> (8 * k)) & 0xFFu;
+      t1 |= ((d && r + d < 255) ? r + d : 0xFFu) << (8 * k);
     }
+    const uint32_t cx = wave_chain(t1);
+    const uint32_t cd = tab_at(packed, cx);
+    const uint32_t j = (uint32_t)__popcll(__ballot(cx != 0xFF && cd != 0));
+    const uint32_t starts = p + cx;
+    const uint32_t q = j ? p + __builtin_amdgcn_readlane(cx, j - 1) + __builtin_amdgcn_readlane(cd, j - 1) : p;
     // 3. decode and place
     Seq s{0, 0, 0, 0, 0};
     const bool v0 = lane < j && seq_at(in.ib, starts, lim, pend, s);
@@ -1144,6 +1186,130 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
   return ST_OK;
 }
 
+// Patas leaf pages of a Float32 / Float64 column (double/patas.rs:107-132),
+// one wave per page, decoded straight into the column.  References reach at
+// most 127 rows back, so the wave keeps the last 256 values in an LDS ring.
+// Per block of 64 rows:
+//  1. the rows' record starts come from wave_chain over 255-byte windows
+//     (record size = 2 + sig bytes, from the header alone);
+//  2. each lane parses its record (v << tz, reference row - ref_diff); a
+//     reference before the block reads the ring, references inside it resolve
+//     by pointer jumping across lanes (6 rounds of ds_bpermute);
+//  3. the block's values go to the ring and, coalesced, to HBM.
+// The first bad record decides the status, as in the reference's loop.
+template <int W>
+__device__ uint32_t patas_wave(const uint8_t* src, uint32_t ilen, uint8_t* dst, uint32_t n, lds_u8* ring) {
+  using T = typename VT<W>::T;
+  const uint32_t lane = threadIdx.x & 63;
+  if (n == 0) return ST_OUT_OF_SPEC;  // `length - 1` underflows (patas.rs:117)
+  if (ilen < W) return ST_IO;
+  gmem_u32* g = (gmem_u32*)((uintptr_t)src & ~(uintptr_t)3);
+  const uint32_t sb0 = (uint32_t)((uintptr_t)src & 3);
+  const uint32_t nd = (sb0 + ilen + 3) >> 2;
+  auto dw = [&](uint32_t i) -> uint32_t { return g[min(i, nd - 1)]; };
+  auto bytes4 = [&](uint32_t pos) -> uint32_t {  // the 4 stream bytes at pos (clamped at the end)
+    const uint32_t a = sb0 + pos, i = a >> 2;
+    return __builtin_amdgcn_alignbyte(dw(i + 1), dw(i), a & 3);
+  };
+  typedef __attribute__((address_space(3))) uint32_t l32;
+  l32* rlo = (l32*)ring;
+  l32* rhi = rlo + 256;
+  const uint32_t f_lo = bytes4(0), f_hi = W == 8 ? bytes4(4) : 0u;
+  uint32_t q = W;  // the next record's stream position
+  for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+    const uint32_t r_end = min(b0 + 64, n);
+    uint32_t i = b0 ? b0 : 1, start = 0, cerr = 0;
+    while (i < r_end && !cerr) {  // record starts of rows [i, r_end), a window at a time
+      uint32_t t1 = 0, dr = 0, ec = 0;
+      {
+        const uint32_t w4 = bytes4(q + 4 * lane), w5 = bytes4(q + 4 * lane + 4);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+          const uint32_t r = 4 * lane + k, x = q + r;
+          uint32_t d = 0, e = 0;
+          if (x + 2 > ilen) {
+            e = ST_IO;  // header past the stream
+          } else {
+            const uint32_t h = __builtin_amdgcn_alignbyte(w5, w4, k) & 0xFFFFu;
+            uint32_t sb = (h >> 6) & 7;
+            if ((h & 0x3F) < 63 && sb == 0) sb = 8;
+            d = 2 + sb;
+            if (sb > (uint32_t)W) e = ST_OUT_OF_SPEC;  // the f32 desync (patas.rs:154-160)
+            else if (x + d > ilen) e = ST_IO;
+          }
+          t1 |= ((e || r + d >= 255) ? 0xFFu : r + d) << (8 * k);
+          dr |= d << (8 * k);
+          ec |= e << (8 * k);
+        }
+      }
+      const uint32_t x = wave_chain(t1);
+      const bool valid = x != 0xFF;
+      const uint32_t my_d = tab_at(dr, x), my_e = tab_at(ec, x);
+      const uint64_t vm = __ballot(valid), em = __ballot(valid && my_e != 0);
+      const uint32_t m = (uint32_t)__popcll(vm);
+      const uint32_t fe = em ? (uint32_t)__builtin_ctzll(em) : 64u;
+      const uint32_t take = min(min(m, fe), r_end - i);
+      // record k of the window is row i + k, dealt to lane (i + k) & 63
+      const uint32_t k = (lane - i) & 63;
+      const uint32_t pos = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(q + x));
+      if (k < take) start = pos;
+      if (fe < m && fe < r_end - i) cerr = __builtin_amdgcn_readlane(my_e, fe) & 0xFFu;
+      if (take) q += __builtin_amdgcn_readlane(x, take - 1) + __builtin_amdgcn_readlane(my_d, take - 1);
+      i += take;
+    }
+    const uint32_t rows_ok = i, row = b0 + lane;
+    uint32_t lo = 0, hi = 0, P = 0xFF;  // P: lane of the in-block reference, 0xFF = resolved
+    bool bad = false;
+    if (row == 0) {
+      lo = f_lo;
+      hi = f_hi;
+    } else if (row < rows_ok) {
+      const uint32_t w0 = bytes4(start), w1 = bytes4(start + 4), w2 = bytes4(start + 8);
+      const uint32_t h = w0 & 0xFFFFu;
+      const uint32_t rd = (h >> 9) & 0x7F, tz = h & 0x3F;
+      uint32_t sb = (h >> 6) & 7;
+      if (tz < 63 && sb == 0) sb = 8;
+      uint64_t v = ((uint64_t)(w0 >> 16) | ((uint64_t)w1 << 16) | ((uint64_t)w2 << 48));
+      v = sb >= 8 ? v : (v & ((1ull << (8 * sb)) - 1));
+      const uint64_t xv = tz >= 8 * W ? 0ull : (uint64_t)(T)((T)v << tz);
+      if (rd == 0 || rd > row) {
+        bad = true;
+      } else if (row - rd < b0) {
+        const uint32_t j = (row - rd) & 255;
+        lo = (uint32_t)xv ^ rlo[j];
+        hi = (uint32_t)(xv >> 32) ^ rhi[j];
+      } else {
+        lo = (uint32_t)xv;
+        hi = (uint32_t)(xv >> 32);
+        P = row - rd - b0;
+      }
+    }
+    if (__ballot(bad)) return ST_OUT_OF_SPEC;  // a reference before row 0 (rows before it are fine)
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+      const int src_lane = (int)(P == 0xFF ? lane : P) << 2;
+      const uint32_t nlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, (int)lo);
+      const uint32_t nhi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, (int)hi);
+      const uint32_t nP = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, (int)P);
+      if (P != 0xFF) {
+        lo ^= nlo;
+        hi ^= nhi;
+        P = nP;
+      }
+    }
+    if (row < rows_ok) {
+      rlo[row & 255] = lo;
+      rhi[row & 255] = hi;
+      if constexpr (W == 8) ((uint64_t*)dst)[row] = (uint64_t)lo | ((uint64_t)hi << 32);
+      else ((uint32_t*)dst)[row] = lo;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (cerr) return cerr;
+  }
+  return ST_OK;
+}
+
 #include "sb_zstd.h"
 
 // One wave expands the general-codec stream [src, src + csize) of `olen`
@@ -1164,35 +1330,122 @@ __device__ uint32_t expand_to_lds(uint32_t codec, const uint8_t* src, uint32_t c
 
 // Patas (double/patas.rs:107-132): first value raw, then per value a u16
 // (ref_diff 7b | sig_bytes 3b | tz 6b; sig 0 => 8 when tz < 63) and sig
-// bytes; value = (v << tz) ^ out[i - ref_diff].  Serial (lane 0).
+// bytes; value = (v << tz) ^ out[i - ref_diff].  All NT threads call it.
+//  1. record starts (wave 0): each lane sizes the records that would start at
+//     4 of the window's 256 byte positions (2 + sig bytes from the header
+//     alone); a scalar chase follows the true chain through the window and
+//     deals the starts to lanes, 64 per flush, into the output slots;
+//  2. values, 256 rows at a time: each thread parses its row's record, a
+//     reference before the block reads the final value, references inside
+//     the block resolve by pointer jumping (8 rounds of value ^= value[ref],
+//     ref = ref[ref] through LDS).
+// Errors keep the reference's order: the first bad record decides the code
+// (a short stream is Io, sig bytes > width is the f32 desync OutOfSpec,
+// patas.rs:154-160, a reference before row 0 OutOfSpec).
 template <int W>
-__device__ uint32_t patas_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, uint32_t n) {
+__device__ uint32_t patas_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, uint32_t n, Shared& sh) {
   using T = typename VT<W>::T;
-  if ((threadIdx.x & 63) != 0) return ST_OK;
+  // the RLE scratch of Shared is idle here (the expanded stream decodes as None):
+  // jump values (lo / hi words), jump targets, the first error
+  static_assert(kRleFastRows / 32 >= NT, "Patas jump arrays alias the RLE scratch");
+  uint32_t* pa_Alo = sh.rle_bits;
+  uint32_t* pa_Ahi = sh.rle_start;
+  uint16_t* pa_P = sh.rle_pref;
+  uint32_t& pa_err = sh.rle_flags;  // (record index << 3) | status of the first bad record, ~0u = none
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  typedef __attribute__((address_space(3))) T lT;
+  typedef __attribute__((address_space(3))) uint32_t l32;
+  lT* o = (lT*)out;
   if (n == 0) return ST_OUT_OF_SPEC;  // `length - 1` underflows (patas.rs:117)
   if (ilen < W) return ST_IO;
-  __attribute__((address_space(3))) T* o = (__attribute__((address_space(3))) T*)out;
-  T first = 0;
-  for (int b = 0; b < W; b++) first |= (T)in[b] << (8 * b);
-  o[0] = first;
-  uint32_t p = W;
-  for (uint32_t i = 1; i < n; i++) {
-    if (p + 2 > ilen) return ST_IO;
-    const uint32_t packed = in[p] | ((uint32_t)in[p + 1] << 8);
-    p += 2;
-    const uint32_t rd = (packed >> 9) & 0x7F, tz = packed & 0x3F;
-    uint32_t sb = (packed >> 6) & 7;
-    if (tz < 63 && sb == 0) sb = 8;
-    if (sb > (uint32_t)W) return ST_OUT_OF_SPEC;  // the f32 desync (patas.rs:154-160)
-    if (p + sb > ilen) return ST_IO;
-    uint64_t v = 0;
-    for (uint32_t b = 0; b < sb; b++) v |= (uint64_t)in[p + b] << (8 * b);
-    p += sb;
-    if (rd == 0 || rd > i) return ST_OUT_OF_SPEC;
-    const T sh = tz >= 8 * W ? (T)0 : (T)((T)v << tz);
-    o[i] = sh ^ o[i - rd];
+  if (tid == 0) pa_err = 0xFFFFFFFFu;
+  uint32_t found = 1;  // records whose start is known: rows [1, found)
+  if (tid < 64) {
+    uint32_t p = W, i = 1, starts = 0, err = 0;
+    while (i < n && !err) {
+      uint32_t packed = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t x = p + 4 * lane + k;
+        uint32_t d = 0xFF;  // header past the stream
+        if (x + 2 <= ilen) {
+          const uint32_t h = in[x] | ((uint32_t)in[x + 1] << 8);
+          uint32_t sb = (h >> 6) & 7;
+          if ((h & 0x3F) < 63 && sb == 0) sb = 8;
+          d = sb > (uint32_t)W ? 0xFE : 2 + sb;
+        }
+        packed |= d << (8 * k);
+      }
+      uint32_t q = p;
+      while (i < n && q - p < 256) {
+        const uint32_t r = q - p;
+        const uint32_t d = (__builtin_amdgcn_readlane(packed, r >> 2) >> ((r & 3) * 8)) & 0xFFu;
+        if (d == 0xFF || (d != 0xFE && q + d > ilen)) { err = ST_IO; break; }
+        if (d == 0xFE) { err = ST_OUT_OF_SPEC; break; }
+        starts = lane == (i & 63) ? q : starts;
+        if ((i & 63) == 63) ((l32*)(out + (uint64_t)(i - 63) * W))[lane * (W / 4)] = starts;
+        q += d;
+        i++;
+      }
+      p = q;
+    }
+    const uint32_t i0 = i & ~63u;  // the partial group of starts
+    if (lane < (i & 63)) ((l32*)(out + (uint64_t)i0 * W))[lane * (W / 4)] = starts;
+    if (tid == 0) {
+      sh.walk_off = i;
+      if (err) pa_err = (i << 3) | err;
+    }
   }
-  return ST_OK;
+  __syncthreads();
+  found = sh.walk_off;
+  if (tid == 0) {
+    T first = 0;
+    for (int b = 0; b < W; b++) first |= (T)in[b] << (8 * b);
+    o[0] = first;
+  }
+  __syncthreads();
+  const uint32_t nv = found;  // rows with a parsed record (row 0 is the first value)
+  for (uint32_t b0 = 0; b0 < nv; b0 += NT) {
+    const uint32_t i = b0 + tid;
+    uint64_t A = 0;
+    uint32_t P = 0xFFFF;  // 0xFFFF: resolved
+    if (i < nv && i > 0) {
+      const uint32_t q = ((const l32*)(out + (uint64_t)i * W))[0];
+      const uint32_t h = in[q] | ((uint32_t)in[q + 1] << 8);
+      const uint32_t rd = (h >> 9) & 0x7F, tz = h & 0x3F;
+      uint32_t sb = (h >> 6) & 7;
+      if (tz < 63 && sb == 0) sb = 8;
+      uint64_t v = 0;
+      for (uint32_t k = 0; k < sb; k++) v |= (uint64_t)in[q + 2 + k] << (8 * k);
+      A = tz >= 8 * W ? 0 : (uint64_t)(T)((T)v << tz);
+      if (rd == 0 || rd > i) {
+        atomicMin(&pa_err, (i << 3) | ST_OUT_OF_SPEC);
+      } else if (i - rd < b0) {
+        A ^= (uint64_t)o[i - rd];
+      } else {
+        P = i - rd - b0;
+      }
+    } else if (i == 0) {
+      A = (uint64_t)o[0];
+    }
+#pragma unroll 1
+    for (uint32_t r = 0; r < 8; r++) {
+      pa_Alo[tid] = (uint32_t)A;
+      pa_Ahi[tid] = (uint32_t)(A >> 32);
+      pa_P[tid] = (uint16_t)P;
+      __syncthreads();
+      if (P != 0xFFFF) {
+        A ^= (uint64_t)pa_Alo[P] | ((uint64_t)pa_Ahi[P] << 32);
+        P = pa_P[P];
+      }
+      __syncthreads();
+    }
+    if (i < nv) o[i] = (T)A;
+    __syncthreads();
+  }
+  const uint32_t e = pa_err;
+  __syncthreads();
+  return e == 0xFFFFFFFFu ? ST_OK : (e & 7);
 }
 
 // read_validity (read/read_basic.rs:36-63): [def_len u32][ULEB128 h, h&1 =
@@ -1284,13 +1537,13 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
       sh.defer = 0;
       if (inner.codec == 1 || inner.codec == 2 || inner.codec == 3 || inner.codec == 16) {
         if (MODE == 0) {
-          if (chain == CH_LEAF && (inner.codec == 1 || inner.codec == 3)) {
-            // plain values under LZ4 / Snappy: k_inflate writes them straight
-            // into the column (the decompressed bytes are the values)
+          if (chain == CH_LEAF && (inner.codec == 1 || inner.codec == 3 || (FLT && inner.codec == 16))) {
+            // plain values under LZ4 / Snappy, or a Patas stream: k_inflate
+            // writes them straight into the column, one wave per page
             sh.defer = 2;
             const uint32_t slot = atomicAdd(a.job_count + a.parity, 1u);
             a.jobs[slot] = InflateJob{pd.byte_off + inner.body, pd.row_off * W, inner.csize, inner.n * (uint32_t)W,
-                                      inner.codec, page};
+                                      inner.codec == 16 ? 16u | ((uint32_t)W << 8) : inner.codec, page};
           } else {
             sh.defer = 1;
             const uint32_t slot = atomicAdd(a.defer_count + a.parity, 1u);
@@ -1315,16 +1568,18 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
       const uint64_t zt = (bytes + 15) & ~15ull;  // Zstd: its tables after the expanded stream
       if ((lf.codec == 2 ? zt + kZTablesBytes : bytes) > xcap) {
         if (tid == 0) set_err(sh, ST_NYI);  // decompressed stream larger than the LDS budget
-      } else if (tid < 64) {
+      } else if (lf.codec == 16) {  // Patas: every thread of the workgroup
         const lds_u8* in = (const lds_u8*)((const uint8_t*)s.w + s.base + lf.body);
+        uint32_t st;
+        if (!FLT || idx_stream) st = ST_OUT_OF_SPEC;  // Patas only in decompress_double
+        else st = patas_expand<W>(in, lf.csize, (lds_u8*)xbuf, lf.n, sh);
+        if (st && tid == 0) set_err(sh, st);
+      } else if (tid < 64) {
         lds_u8* xo = (lds_u8*)xbuf;
         uint32_t st = ST_OK;
         if (lf.codec == 1 || lf.codec == 3)
           st = expand_to_lds(lf.codec, a.chunk + pd.byte_off + lf.body, lf.csize, xo, (uint32_t)bytes);
-        else if (lf.codec == 16) {
-          if (!FLT || idx_stream) st = ST_OUT_OF_SPEC;  // Patas only in decompress_double
-          else st = patas_expand<W>(in, lf.csize, xo, lf.n);
-        } else {
+        else {
           st = zs::zstd_to_lds(LdsSrc{s.w, s.base + lf.body}, lf.csize, xo, (uint32_t)bytes, xo + zt,
                                (uint32_t)(xcap - zt));
         }
@@ -1548,6 +1803,10 @@ __global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) 
       WaveWin w;
       w.init(src, jb.csize);
       st = snappy_wave<true>(w, p0, p0 + jb.csize, o);
+    } else if ((jb.codec & 0xFF) == 16) {  // Patas leaf: codec 16 | width << 8
+      const uint32_t W = jb.codec >> 8;
+      st = W == 8 ? patas_wave<8>(src, jb.csize, dst, jb.usize / 8, o.ring)
+                  : patas_wave<4>(src, jb.csize, dst, jb.usize / 4, o.ring);
     }
     if (st && lane == 0) a.status[jb.page] = st;
   }
@@ -2140,7 +2399,6 @@ __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
 // k_inflate) at their leaf bases.
 // ===========================================================================
 constexpr uint32_t kLvK = 32;                   // levels per thread per tile
-constexpr uint32_t kLvTile = NT * kLvK;         // 8192 levels per tile
 constexpr uint32_t kMaxRuns = 64;               // hybrid runs per level stream
 
 struct LvRuns {
