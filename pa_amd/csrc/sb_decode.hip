@@ -716,6 +716,8 @@ struct WaveOut {
   lds_u8* ring;   // RING: kRing bytes (16-byte aligned); FULL: olen bytes
   uint8_t* dst;   // RING: HBM destination of the whole stream
   __amdgpu_buffer_rsrc_t rs;  // RING: dst, olen bytes (far history reads)
+  __amdgpu_buffer_rsrc_t rsa;  // RING: the same bytes from dst rounded down to a dword (dword reads)
+  uint32_t dal;                // dst & 3
   uint32_t olen;
   uint32_t op;
 
@@ -724,6 +726,9 @@ struct WaveOut {
   // past op overwrite the ring slots of chunks k-4 and k-3, and the flushes of
   // chunks <= k-2 have completed (each flush first waits for the previous).
   __device__ __forceinline__ uint32_t far_limit() const {
+#ifdef SB_V_NOFAR
+    return 0u;
+#endif
     const uint32_t k = op / kChunk;
     return k >= 2 ? (k - 2) * kChunk : 0u;
   }
@@ -733,7 +738,9 @@ struct WaveOut {
   __device__ void flush(uint32_t c0, uint32_t len) {
     const uint32_t lane = threadIdx.x & 63;
     // the previous chunk's stores must complete before far reads may use them
+#ifndef SB_V_NOFLUSHWAIT
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     uint8_t* d = dst + c0;
     if (len == kChunk) {
       const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(ring + slot(c0 + 16 * lane));
@@ -1049,6 +1056,93 @@ __device__ __forceinline__ bool seq_at(const lds_u8* ib, uint32_t x, uint32_t li
   return true;
 }
 
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// *p = (*p & ~clear) | set, one LDS op (lanes sharing a word apply in turn)
+__device__ __forceinline__ void lds_mskor(lds_u32* p, uint32_t clear, uint32_t set) {
+  asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"((uint32_t)(uintptr_t)p), "v"(clear), "v"(set) : "memory");
+}
+// Bytes [0, n) of a source whose byte i is byte sh + i of the words w[0..NW)
+// (sh + n <= 4 NW), stored at ring position d: one masked store per
+// destination word, so lanes writing neighbouring ranges may share edge words.
+template <int NW>
+__device__ __forceinline__ void ring_put(lds_u8* ring, uint32_t d, uint32_t n, uint32_t sh, const uint32_t* w) {
+  lds_u32* r32 = (lds_u32*)ring;
+  const uint32_t dsh = d & 3, base = d - dsh, e = (sh - dsh) & 3;
+  const bool fwd = sh >= dsh;
+#pragma unroll
+  for (int t = 0; t <= NW; t++) {
+    const int rem = (int)n - (4 * t - (int)dsh);  // source bytes from this word on
+    if (!__ballot(rem > 0)) break;
+    if (rem > 0) {
+      const uint32_t z = t > 0 ? w[t - 1] : 0u, a = t < NW ? w[t] : 0u, b = t + 1 < NW ? w[t + 1] : 0u;
+      const uint32_t u = fwd ? __builtin_amdgcn_alignbyte(b, a, e) : __builtin_amdgcn_alignbyte(a, z, e);
+      uint32_t m = rem >= 4 ? ~0u : (1u << (8 * rem)) - 1u;
+      if (t == 0) m &= ~0u << (8 * dsh);
+      lds_mskor(r32 + (((base + 4 * t) & (kRing - 1)) >> 2), m, u & m);
+    }
+  }
+}
+// lane % o for lane < 64, 0 < o < 64, without an integer divide
+__device__ __forceinline__ uint32_t lane_mod(uint32_t lane, uint32_t o) {
+  const uint32_t q = (uint32_t)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)o));
+  return lane - q * o;
+}
+
+// Successor table of the 256 candidate starts p + r (r = 4 lane + k): byte k
+// = r + d for a sequence of d bytes that batch decoding takes (literal <=
+// kLitFast, each length with at most one extension byte, not the final
+// sequence, staged below lim), else 0xFF (the chain stops); byte k of *okt
+// is 1 for such a sequence (the chain's last one may end past the window).
+__device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uint32_t lim, uint32_t pend,
+                                               uint32_t* okt) {
+  typedef __attribute__((address_space(3))) uint32_t l32;
+  const l32* ib32 = (const l32*)ib;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t x0 = p + 4 * lane, a0 = x0 & ~3u, sh = x0 & 3;
+  const uint32_t w0 = ib32[(a0 & (kIb - 1)) >> 2], w1 = ib32[((a0 + 4) & (kIb - 1)) >> 2],
+                 w2 = ib32[((a0 + 8) & (kIb - 1)) >> 2];
+  const uint32_t tok = __builtin_amdgcn_alignbyte(w1, w0, sh);   // bytes x0 .. x0 + 3
+  const uint32_t nxt = __builtin_amdgcn_alignbyte(w2, w1, sh);   // bytes x0 + 4 .. x0 + 7
+  const uint32_t ext = __builtin_amdgcn_alignbyte(nxt, tok, 1);  // bytes x0 + 1 .. x0 + 4
+  uint32_t t1 = 0, ov = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint32_t x = x0 + k, t = (tok >> (8 * k)) & 0xFFu, e = (ext >> (8 * k)) & 0xFFu;
+    const uint32_t ln = t >> 4;
+    const bool lx = ln == 15;
+    const uint32_t lit = lx ? 15 + e : ln;
+    const uint32_t le = x + 1 + (uint32_t)lx + lit;  // the offset's position
+    bool ok = x + 1 + (uint32_t)lx <= lim && lit <= kLitFast && le + 2 <= lim && le < pend;
+    uint32_t y = le + 2;
+    if (ok && (t & 15) == 15) {
+      const uint32_t e2 = y < lim ? (uint32_t)ib[y & (kIb - 1)] : 255u;
+      ok = e2 != 255;
+      y++;
+    }
+    const uint32_t r = 4 * lane + k, nr = r + (y - x);
+    t1 |= (ok && nr < 255 ? nr : 0xFFu) << (8 * k);
+    ov |= (uint32_t)ok << (8 * k);
+  }
+  *okt = ov;
+  return t1;
+}
+
+// The sequence at x, which cand_steps accepted (no checks left to make).
+__device__ __forceinline__ void seq_parse(const lds_u8* ib, uint32_t x, Seq& s) {
+  const uint32_t t = ib[x & (kIb - 1)], ln = t >> 4;
+  uint32_t y = x + 1, lit = ln;
+  if (ln == 15) lit += ib[(y++) & (kIb - 1)];
+  const uint32_t le = y + lit;
+  s.lit_pos = y;
+  s.lit = lit;
+  s.off = ib[le & (kIb - 1)] | ((uint32_t)ib[(le + 1) & (kIb - 1)] << 8);
+  y = le + 2;
+  uint32_t ml = (t & 15) + 4;
+  if ((t & 15) == 15) ml += ib[(y++) & (kIb - 1)];
+  s.ml = ml;
+  s.next = y;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
@@ -1112,30 +1206,22 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
   while (p < pend && !ended) {
     in.slide(p);
     const uint32_t lim = min(in.base + 3072, pend);
-    // 1. successor distances of the candidate starts
-    uint32_t packed = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      const uint32_t x = p + 4 * lane + k;
-      Seq s;
-      if (seq_at(in.ib, x, lim, pend, s) && s.next - x <= 255) packed |= (s.next - x) << (8 * k);
-    }
+    // 1. successor distances of the candidate starts x = p + 4 lane + k, from
+    //    the token and at most one extension byte per length: the tokens are
+    //    one unaligned dword of the ring, the literal extensions the next
+    //    bytes; only a match-length extension needs its own byte read
+    uint32_t okt;
+    const uint32_t t1 = cand_steps(in.ib, p, lim, pend, &okt);
     // 2. the chain of sequence starts from p, wave-parallel (wave_chain): a
-    //    candidate with distance 0 (serial path) ends it
-    uint32_t t1 = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      const uint32_t r = 4 * lane + k, d = (packed >> (8 * k)) & 0xFFu;
-      t1 |= ((d && r + d < 255) ? r + d : 0xFFu) << (8 * k);
-    }
+    //    candidate that needs the serial path ends it
     const uint32_t cx = wave_chain(t1);
-    const uint32_t cd = tab_at(packed, cx);
-    const uint32_t j = (uint32_t)__popcll(__ballot(cx != 0xFF && cd != 0));
+    const uint32_t j = (uint32_t)__popcll(__ballot(cx != 0xFF && tab_at(okt, cx) == 1));
     const uint32_t starts = p + cx;
-    const uint32_t q = j ? p + __builtin_amdgcn_readlane(cx, j - 1) + __builtin_amdgcn_readlane(cd, j - 1) : p;
     // 3. decode and place
     Seq s{0, 0, 0, 0, 0};
-    const bool v0 = lane < j && seq_at(in.ib, starts, lim, pend, s);
+    const bool v0 = lane < j;
+    if (v0) seq_parse(in.ib, starts, s);
+    const uint32_t q = j ? __builtin_amdgcn_readlane(s.next, j - 1) : p;
     const uint32_t len = v0 ? s.lit + s.ml : 0u;
     const uint32_t incl = wave_incl_scan(len), excl = incl - len;
     const uint32_t cap = min(kChunk, olen - o.op);
@@ -1148,16 +1234,64 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
       if (st) return st;
       continue;
     }
+#ifdef SB_V_NOCOPY
+    const bool v = false;
+#else
     const bool v = lane < k;
-    for (uint32_t i = 0; __ballot(v && i < s.lit); i++)
-      if (v && i < s.lit) o.ring[(dl + i) & (kRing - 1)] = in.ib[(s.lit_pos + i) & (kIb - 1)];
+#endif
+    typedef __attribute__((address_space(3))) uint32_t l32;
+    const l32* ib32 = (const l32*)in.ib;
+    const l32* r32 = (const l32*)o.ring;
+#ifdef SB_V_NOLIT
+    if (v) s.lit = 0;
+#endif
+    // literals, 16 bytes per lane per step: source dwords from the input ring,
+    // one masked dword store per destination word
+    for (uint32_t c = 0; __ballot(v && c < s.lit); c += 16) {
+      if (v && c < s.lit) {
+        const uint32_t x = s.lit_pos + c, sh = x & 3, a0 = x - sh, n = min(16u, s.lit - c);
+        uint32_t w[5];
+#pragma unroll
+        for (uint32_t t = 0; t < 5; t++) w[t] = ib32[((a0 + 4 * t) & (kIb - 1)) >> 2];
+        ring_put<5>(o.ring, dl + c, n, sh, w);
+      }
+    }
     const uint32_t d_first = __builtin_amdgcn_readfirstlane(dm);
     const uint32_t src = dm - s.off;
+#ifdef SB_V_NOHAZ
+    const bool hazard = false;
+#else
     const bool hazard = v && (src + s.ml > d_first || s.ml > kMatchFast);
+#endif
+#ifdef SB_V_NOFREE
+    const bool freel = false;
+#else
     const bool freel = v && !hazard;
+#endif
     const uint32_t farlim = o.far_limit();
-    for (uint32_t i = 0; __ballot(freel && i < s.ml); i++) {
-      if (freel && i < s.ml) {
+    // A free match's source is final before the batch: its dwords come from
+    // HBM below farlim (an out-of-range buffer offset reads 0 for the other
+    // lanes) or from the ring, all loads before the stores; a source
+    // straddling farlim goes byte by byte.
+    const bool mfar = src + s.ml <= farlim, mnear = src >= farlim;
+    const bool fw = freel && (mfar || mnear);
+    if (__ballot(fw)) {
+      constexpr uint32_t NW = kMatchFast / 4 + 1;
+      const uint32_t a = mfar ? src + o.dal : src, sh = a & 3, a0 = a - sh, need = fw ? sh + s.ml : 0u;
+      uint32_t w[NW];
+#pragma unroll
+      for (uint32_t t = 0; t < NW; t++) {
+        w[t] = 0;
+        if (!__ballot(4 * t < need)) continue;
+        const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(o.rsa, mfar && 4 * t < need ? a0 + 4 * t : 0x80000000u, 0, 16);
+        const uint32_t r = r32[((a0 + 4 * t) & (kRing - 1)) >> 2];
+        w[t] = mfar ? g : r;
+      }
+      if (fw) ring_put<NW>(o.ring, dm, s.ml, sh, w);
+    }
+    const bool fmix = freel && !mfar && !mnear;
+    for (uint32_t i = 0; __ballot(fmix && i < s.ml); i++) {
+      if (fmix && i < s.ml) {
         const uint32_t qq = src + i;
         const uint32_t b = qq < farlim ? __builtin_amdgcn_raw_buffer_load_b8(o.rs, qq, 0, 16) : o.ring[qq & (kRing - 1)];
         o.ring[(dm + i) & (kRing - 1)] = (uint8_t)b;
@@ -1170,7 +1304,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
       for (uint32_t c = 0; c < M; c += 64) {
         if (lane < M - c) {
           const uint32_t x = D + c;
-          const uint32_t qq = x - O + (O >= 64 ? lane : lane % O);
+          const uint32_t qq = x - O + (O >= 64 ? lane : lane_mod(lane, O));
           const uint32_t b = qq < farlim ? __builtin_amdgcn_raw_buffer_load_b8(o.rs, qq, 0, 16) : o.ring[qq & (kRing - 1)];
           o.ring[(x + lane) & (kRing - 1)] = (uint8_t)b;
         }
@@ -1788,6 +1922,8 @@ __global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) 
     o.ring = (lds_u8*)&rings[wv][0];
     o.dst = dst;
     o.rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)jb.usize, 0x00020000);
+    o.dal = (uint32_t)((uintptr_t)dst & 3);
+    o.rsa = __builtin_amdgcn_make_buffer_rsrc(dst - o.dal, 0, (int)(jb.usize + o.dal), 0x00020000);
     o.olen = jb.usize;
     o.op = 0;
     const uint32_t p0 = (uint32_t)((uintptr_t)src & 3);

@@ -8,7 +8,7 @@ mkdir -p variants _build/variants
 build() {
   name=$1; shift
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" -x hip -c csrc/sb_decode.hip -o _build/variants/$name.o
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o variants/libsb_$name.so _build/variants/$name.o _build/sb_api.cpp.o _build/sb_encode.cpp.o _build/sb_write_api.cpp.o -l:liblz4.so.1 -l:libzstd.so.1 -lpthread
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o variants/libsb_$name.so _build/variants/$name.o $(ls _build/*.o | grep -v sb_decode) -l:liblz4.so.1 -l:libzstd.so.1 -lpthread
 }
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
