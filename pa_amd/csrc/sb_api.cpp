@@ -79,7 +79,8 @@ struct sb_plan {
   sb_plan* inner = nullptr;
   uint64_t n_leaves = 0;
   int offset_width = 0;
-  uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1 | LDS need 1]
+  uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1 | LDS need 1] then BinLaunch::cls (u32)
+  uint32_t bin_grid = 0;      // staged-pass workgroups: the plan pass's staged page count
   uint32_t bin_lds = 0;       // dynamic LDS of the binary kernels (the largest page need, from the plan pass)
   uint64_t values_bytes = 0;
   uint32_t n_staged = 0, n_global = 0;
@@ -285,7 +286,7 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     return fail(ctx, SB_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
   }
   if (p->binary && n_pages) {  // size every page's values once: they are fixed for the plan
-    e = hipMalloc(&p->d_bin, (2 * np + 2) * sizeof(uint64_t));
+    e = hipMalloc(&p->d_bin, (2 * np + 2) * sizeof(uint64_t) + (3 * np + 2) * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemsetAsync(p->d_bin + 2 * np + 1, 0, sizeof(uint64_t), ctx->stream);
     if (e != hipSuccess) {
       sb_plan_destroy(p);
@@ -293,7 +294,8 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     }
     sb::BinLaunch L{d_chunk, p->d_pages, (uint32_t)n_pages, desc->nullable, p->d_bin, p->d_bin + np,
                     p->d_bin + 2 * np, nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr,
-                    sb::kDeferredLds, (uint32_t*)(p->d_bin + 2 * np + 1)};
+                    sb::kDeferredLds, (uint32_t*)(p->d_bin + 2 * np + 1), (uint32_t*)(p->d_bin + 2 * np + 2),
+                    (uint32_t)std::min<size_t>(np, 65535)};
     if (sb::launch_binary(0, owidth, L, ctx->stream) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "binary sizing failed: %s", hipGetErrorString(hipGetLastError()));
@@ -305,6 +307,9 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     uint32_t need = sb::kDeferredLds;
     (void)hipMemcpy(&need, p->d_bin + 2 * np + 1, 4, hipMemcpyDeviceToHost);
     p->bin_lds = std::min<uint32_t>(std::max<uint32_t>((need + 1023) & ~1023u, 4096), sb::kDeferredLds);
+    uint32_t n_staged = 0;
+    (void)hipMemcpy(&n_staged, (uint32_t*)(p->d_bin + 2 * np + 2) + 3 * np, 4, hipMemcpyDeviceToHost);
+    p->bin_grid = std::max<uint32_t>(1, std::min<uint32_t>(n_staged, 65535));
     for (uint64_t i = 0; i < n_pages; i++) {
       if (st[i]) {
         sb_plan_destroy(p);
@@ -338,12 +343,14 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   // LZ4 / Snappy streams): the plan-time pass only sized the caller's buffers.
   HIP_TRY(ctx, hipMemsetAsync(p->d_defer + 2, 0, sizeof(uint32_t), ctx->stream));
   sb::BinLaunch S{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
-                  nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr, p->bin_lds, nullptr};
+                  nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr, p->bin_lds, nullptr,
+                  (uint32_t*)(p->d_bin + 2 * np + 2), p->bin_grid};
   if (sb::launch_binary(0, p->offset_width, S, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "binary sizing launch failed: %s", hipGetErrorString(hipGetLastError()));
   sb::BinLaunch L{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
                   (uint8_t*)out->d_offsets, out->d_values, out->values_capacity, (uint32_t*)out->d_validity,
-                  p->d_status, p->d_jobs, nullptr, p->d_scratch, p->bin_lds, nullptr};
+                  p->d_status, p->d_jobs, nullptr, p->d_scratch, p->bin_lds, nullptr, (uint32_t*)(p->d_bin + 2 * np + 2),
+                  p->bin_grid};
   if (p->n_bin_jobs) {  // Basic LZ4 / Snappy pages: streams expanded first, one wave each
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2, p->n_bin_jobs, out->d_values, p->d_scratch,
                         p->d_bin + np, p->d_status};

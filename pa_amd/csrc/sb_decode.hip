@@ -1975,6 +1975,7 @@ struct BinArgs {
   uint32_t* job_count;
   uint8_t* scratch;
   uint32_t* lds_need;
+  uint32_t* cls;  // staged list [n] | header-only list [n] | validity bitmap positions [n] | the 2 list lengths
 };
 
 enum : uint32_t { BIN_BASIC = 0, BIN_ONE = 12, BIN_DICT = 11, BIN_FREQ = 13 };
@@ -2177,6 +2178,111 @@ __device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, ui
   __syncthreads();
 }
 
+// Header-only pages: Basic pages under LZ4 / Snappy need no staging.  Their
+// two streams are expanded by k_inflate (offsets into scratch, values at the
+// page's base), so only the validity prefix and the two stream headers are
+// read here, by one thread per page straight from HBM, with the checks of
+// parse_validity and bin_parse; any other page (or any check failing) goes to
+// the staged passes, which report the error.
+struct LightPage {
+  uint32_t codec, ob, ocs, vb, vcs, S, vbpos;
+};
+
+__device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int nullable, LightPage& lp) {
+  uint32_t p = 0;
+  lp.vbpos = 0;
+  if (n == 0) return false;
+  if (nullable) {
+    if (len < 4) return false;
+    const uint32_t def_len = s.u32(0);
+    p = 4;
+    if (def_len == 0 || def_len > len - p) return false;
+    uint32_t q = p, h = 0, sft = 0;
+    for (;;) {
+      if (q >= p + def_len || sft > 28) return false;
+      const uint32_t c = s.u8(q++);
+      h |= (c & 0x7Fu) << sft;
+      if (!(c & 0x80)) break;
+      sft += 7;
+    }
+    if (!(h & 1)) return false;
+    if ((uint64_t)min(h >> 1, p + def_len - q) * 8 < n) return false;
+    lp.vbpos = q;  // >= 5: 0 means no bitmap
+    p += def_len;
+  }
+  if (p + 9 > len) return false;
+  lp.codec = s.u8(p);
+  if (lp.codec != 1 && lp.codec != 3) return false;
+  const uint32_t cs = s.u32(p + 1), body = p + 9;
+  if (cs > len - body) return false;
+  const uint32_t vh = body + cs;
+  if (vh + 9 > len) return false;
+  lp.vcs = s.u32(vh + 1);
+  lp.S = s.u32(vh + 5);
+  lp.vb = vh + 9;
+  if (lp.vcs > len - lp.vb) return false;
+  lp.ob = body;
+  lp.ocs = cs;
+  return true;
+}
+
+// Classifies every page (one thread each): header-only pages get their two
+// inflate jobs and size here; the rest are listed for k_bin_size.
+template <int OW>
+__global__ __launch_bounds__(NT) void k_bin_light(BinArgs a) {
+  const uint32_t np = a.n_pages;
+  uint32_t *staged = a.cls, *light = a.cls + np, *vbpos = a.cls + 2 * np, *cnt = a.cls + 3 * np;
+  for (uint32_t page = blockIdx.x * NT + threadIdx.x; page < np; page += gridDim.x * NT) {
+    const PageDesc pd = a.pages[page];
+    LightPage lp;
+    if (bin_light_parse(GlbSrc{a.chunk + pd.byte_off}, pd.byte_len, pd.num_values, a.nullable, lp)) {
+      const uint32_t slot = atomicAdd(a.job_count, 2u);
+      a.jobs[slot] = InflateJob{pd.byte_off + lp.ob, kDstScratch | ((pd.row_off + page) * OW), lp.ocs,
+                                (pd.num_values + 1) * (uint32_t)OW, lp.codec, page};
+      a.jobs[slot + 1] = InflateJob{pd.byte_off + lp.vb, kDstBinBase | page, lp.vcs, lp.S, lp.codec, page};
+      a.sizes[page] = lp.S;
+      a.status[page] = 0;
+      vbpos[page] = lp.vbpos;
+      light[atomicAdd(&cnt[1], 1u)] = page;
+    } else {
+      staged[atomicAdd(&cnt[0], 1u)] = page;
+    }
+  }
+}
+
+// Header-only pages after k_inflate: offsets rebased from scratch onto the
+// page's values base (mod.rs:136-144; p[0] must be 0 and p[n] the values
+// length), the validity bitmap copied from the page in HBM.
+template <int OW>
+__global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
+  __shared__ uint32_t bad;
+  const uint32_t np = a.n_pages, nl = a.cls[3 * np + 1], tid = threadIdx.x;
+  for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    const uint32_t page = a.cls[np + i];
+    const PageDesc pd = a.pages[page];
+    const uint32_t n = pd.num_values;
+    const uint64_t R = pd.row_off, V = a.bases[page], S = a.sizes[page];
+    if (a.status[page]) continue;  // an inflate error stands
+    const uint8_t* xo = a.scratch + (R + page) * OW;
+    auto po = [&](uint32_t k) -> uint64_t {
+      if constexpr (OW == 8) return ((const uint64_t*)xo)[k];
+      else return (uint64_t)(int64_t)((const int32_t*)xo)[k];
+    };
+    if (tid == 0) bad = (po(0) != 0 || po(n) != S || V + S > a.values_cap) ? ST_OUT_OF_SPEC : 0u;
+    __syncthreads();
+    const uint32_t e = bad;
+    __syncthreads();
+    if (e) {
+      if (tid == 0) a.status[page] = e;
+      continue;
+    }
+    if (R == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);
+    for (uint32_t k = tid + 1; k <= n; k += NT) bin_put_off(a.out_offsets, R + k, V + po(k), OW);
+    const uint32_t vb = a.cls[2 * np + page];
+    if (vb) write_validity(GlbSrc{a.chunk + pd.byte_off}, vb, n, R, a.out_validity);
+  }
+}
+
 template <int OW>
 __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
   extern __shared__ u32x4 stage[];
@@ -2184,7 +2290,9 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
   __shared__ BinInfo bi;
   __shared__ Stream idx;
   uint8_t* lds = (uint8_t*)stage;
-  for (uint32_t page = blockIdx.x; page < a.n_pages; page += gridDim.x) {
+  const uint32_t n_staged = a.cls[3 * a.n_pages];
+  for (uint32_t i = blockIdx.x; i < n_staged; i += gridDim.x) {
+    const uint32_t page = a.cls[i];
     const PageDesc pd = a.pages[page];
     if (threadIdx.x == 0) sh.err = 0;
     const uint32_t stage_end = ((pd.byte_len + 15 + kStagePad) + 15) & ~15u;
@@ -2291,7 +2399,9 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
   __shared__ Stream idx;
   uint8_t* lds = (uint8_t*)stage;
   const uint32_t tid = threadIdx.x;
-  for (uint32_t page = blockIdx.x; page < a.n_pages; page += gridDim.x) {
+  const uint32_t n_staged = a.cls[3 * a.n_pages];
+  for (uint32_t i = blockIdx.x; i < n_staged; i += gridDim.x) {
+    const uint32_t page = a.cls[i];
     const PageDesc pd = a.pages[page];
     const uint32_t n = pd.num_values;
     const uint64_t R = pd.row_off, V = a.bases[page];
@@ -3083,22 +3193,37 @@ namespace sb {
 int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream) {
   const uint32_t lds = L.lds_bytes ? std::min(L.lds_bytes, kDeferredLds) : kDeferredLds;
   sbk::BinArgs a{L.chunk, L.pages, L.n_pages, L.nullable, L.sizes, L.bases, L.total, L.out_offsets, L.out_values,
-                 L.values_cap, L.out_validity, L.status, lds, L.jobs, L.job_count, L.scratch, L.lds_need};
+                 L.values_cap, L.out_validity, L.status, lds, L.jobs, L.job_count, L.scratch, L.lds_need, L.cls};
   hipStream_t st = (hipStream_t)stream;
   const dim3 block(sbk::NT);
-  // one workgroup per page (grid-stride past 64 Ki pages): as many resident per CU as the LDS budget allows
-  const dim3 grid(std::min<uint32_t>(L.n_pages ? L.n_pages : 1, 65535u));
+  // staged passes: one workgroup per listed page (grid-stride), as many
+  // resident per CU as the LDS budget allows; header-only pages: one thread
+  // each to classify, one workgroup each to write offsets and validity
+  const dim3 grid(std::max<uint32_t>(1, L.staged_grid));
+  const dim3 cgrid((L.n_pages + sbk::NT - 1) / sbk::NT);
+  const dim3 lgrid(std::min<uint32_t>(L.n_pages, 65535u));
   ensure_lds_attr(sbk::k_bin_size<4>, (int)kDeferredLds);
   ensure_lds_attr(sbk::k_bin_size<8>, (int)kDeferredLds);
   ensure_lds_attr(sbk::k_bin_decode<4>, (int)kDeferredLds);
   ensure_lds_attr(sbk::k_bin_decode<8>, (int)kDeferredLds);
   if (stage == 0) {
-    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_size<8>, grid, block, lds, st, a);
-    else hipLaunchKernelGGL(sbk::k_bin_size<4>, grid, block, lds, st, a);
+    if (hipMemsetAsync(L.cls + 3 * (size_t)L.n_pages, 0, 2 * sizeof(uint32_t), st) != hipSuccess) return -1;
+    if (offset_width == 8) {
+      hipLaunchKernelGGL(sbk::k_bin_light<8>, cgrid, block, 0, st, a);
+      hipLaunchKernelGGL(sbk::k_bin_size<8>, grid, block, lds, st, a);
+    } else {
+      hipLaunchKernelGGL(sbk::k_bin_light<4>, cgrid, block, 0, st, a);
+      hipLaunchKernelGGL(sbk::k_bin_size<4>, grid, block, lds, st, a);
+    }
     hipLaunchKernelGGL(sbk::k_bin_scan, dim3(1), block, 0, st, a);
   } else {
-    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, lds, st, a);
-    else hipLaunchKernelGGL(sbk::k_bin_decode<4>, grid, block, lds, st, a);
+    if (offset_width == 8) {
+      hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, lds, st, a);
+      hipLaunchKernelGGL(sbk::k_bin_light_out<8>, lgrid, block, 0, st, a);
+    } else {
+      hipLaunchKernelGGL(sbk::k_bin_decode<4>, grid, block, lds, st, a);
+      hipLaunchKernelGGL(sbk::k_bin_light_out<4>, lgrid, block, 0, st, a);
+    }
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -134,6 +134,9 @@ struct BinLaunch {
   uint8_t* scratch;       // expanded offsets streams, (row_off + page) * offset width
   uint32_t lds_bytes;     // dynamic LDS per workgroup (0 = kDeferredLds)
   uint32_t* lds_need;     // sizing pass at plan time: max LDS bytes any page needs
+  uint32_t* cls;          // [3 n_pages + 2]: staged-page list | header-only page list | validity
+                          // bitmap positions | the two list lengths (reset by stage 0)
+  uint32_t staged_grid;   // workgroups of the staged passes (any >= 1 is correct)
 };
 int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
 
