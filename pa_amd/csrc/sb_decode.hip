@@ -977,12 +977,39 @@ __device__ __forceinline__ uint32_t wave_chain(uint32_t t1) {
   return x;
 }
 
+// wave_chain through LDS byte tables: T1..T32 at tab + 256 j (T1 byte 255
+// must be 0xFF, so every table maps 0xFF to itself and no lookup needs a
+// guard); one byte read per lookup instead of a permute and a byte extract.
+__device__ __forceinline__ uint32_t lds_chain(lds_u8* tab, uint32_t t1) {
+  typedef __attribute__((address_space(3))) uint32_t l32;
+  const uint32_t lane = threadIdx.x & 63;
+  ((l32*)tab)[lane] = t1;
+  uint32_t T = t1;
+#pragma unroll
+  for (int j = 1; j < 6; j++) {
+    const lds_u8* prev = tab + 256 * (j - 1);
+    uint32_t nt = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) nt |= (uint32_t)prev[(T >> (8 * k)) & 0xFFu] << (8 * k);
+    ((l32*)tab)[64 * j + lane] = nt;
+    T = nt;
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    const uint32_t y = tab[256 * j + x];
+    if ((lane >> j) & 1) x = y;
+  }
+  return x;
+}
+
 constexpr uint32_t kIb = 4096, kScan = 256, kLitFast = 64, kMatchFast = 32;
 
 struct InRing {
   gmem_u32* g;   // dword-aligned stream base
   uint32_t nd;   // stream dwords
   lds_u8* ib;    // kIb bytes: stream byte x at ib[x % kIb]
+  lds_u8* ct;    // 7 x 256 bytes: the chain tables T1..T32 and the candidates' accept table
   uint32_t base; // [base, base + 3 KiB) staged and complete; base % 1 KiB == 0
 
   __device__ __forceinline__ void dma(uint32_t b) {  // [b, b + 1 KiB) -> ib
@@ -1143,13 +1170,13 @@ __device__ __forceinline__ void seq_parse(const lds_u8* ib, uint32_t x, Seq& s) 
   s.next = y;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += y;
-  }
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {  // DPP: no LDS round trips
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31
   return v;
 }
 
@@ -1214,8 +1241,9 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     const uint32_t t1 = cand_steps(in.ib, p, lim, pend, &okt);
     // 2. the chain of sequence starts from p, wave-parallel (wave_chain): a
     //    candidate that needs the serial path ends it
-    const uint32_t cx = wave_chain(t1);
-    const uint32_t j = (uint32_t)__popcll(__ballot(cx != 0xFF && tab_at(okt, cx) == 1));
+    const uint32_t cx = lds_chain(in.ct, t1);
+    ((__attribute__((address_space(3))) uint32_t*)in.ct)[64 * 6 + lane] = okt;
+    const uint32_t j = (uint32_t)__popcll(__ballot(cx != 0xFF && in.ct[256 * 6 + cx] == 1));
     const uint32_t starts = p + cx;
     // 3. decode and place
     Seq s{0, 0, 0, 0, 0};
@@ -1910,6 +1938,7 @@ static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
 __global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) {
   __shared__ u32x4 rings[kInfWaves][kRing / 16];
   __shared__ u32x4 ibufs[kInfWaves][kIb / 16];
+  __shared__ u32x4 ctabs[kInfWaves][7 * 256 / 16];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = a.count ? *a.count : a.n_jobs;
@@ -1933,6 +1962,7 @@ __global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) 
       in.g = (gmem_u32*)((uintptr_t)src & ~(uintptr_t)3);
       in.nd = (p0 + jb.csize + 3) >> 2;
       in.ib = (lds_u8*)&ibufs[wv][0];
+      in.ct = (lds_u8*)&ctabs[wv][0];
       in.seek(p0);
       st = lz4_inflate(in, p0, p0 + jb.csize, o);
     } else if (jb.codec == 3) {
