@@ -1329,6 +1329,10 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
       const uint32_t l = (uint32_t)__builtin_ctzll(hm);
       const uint32_t D = __builtin_amdgcn_readlane(dm, l), O = __builtin_amdgcn_readlane(s.off, l),
                      M = __builtin_amdgcn_readlane(s.ml, l);
+      if (M <= 64 && O >= M && D - O >= farlim) {  // no self-overlap, source in the ring: one byte a lane
+        if (lane < M) o.ring[(D + lane) & (kRing - 1)] = o.ring[(D - O + lane) & (kRing - 1)];
+        continue;
+      }
       for (uint32_t c = 0; c < M; c += 64) {
         if (lane < M - c) {
           const uint32_t x = D + c;
