@@ -1132,6 +1132,22 @@ __device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uin
   const uint32_t nxt = __builtin_amdgcn_alignbyte(w2, w1, sh);   // bytes x0 + 4 .. x0 + 7
   const uint32_t ext = __builtin_amdgcn_alignbyte(nxt, tok, 1);  // bytes x0 + 1 .. x0 + 4
   uint32_t t1 = 0, ov = 0;
+  if (lim - p >= 325) {  // every candidate's bytes (<= p + 324) are staged: no bounds checks
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t x = x0 + k, t = (tok >> (8 * k)) & 0xFFu, e = (ext >> (8 * k)) & 0xFFu;
+      const uint32_t ln = t >> 4, lx = ln == 15;
+      const uint32_t lit = lx ? 15 + e : ln;
+      const uint32_t y = x + 3 + lx + lit;  // past the offset
+      const uint32_t e2 = ib[y & (kIb - 1)], mx = (t & 15) == 15;
+      const bool ok = lit <= kLitFast && !(mx && e2 == 255);
+      const uint32_t r = 4 * lane + k, nr = r + (y + mx - x);
+      t1 |= (ok && nr < 255 ? nr : 0xFFu) << (8 * k);
+      ov |= (uint32_t)ok << (8 * k);
+    }
+    *okt = ov;
+    return t1;
+  }
 #pragma unroll
   for (uint32_t k = 0; k < 4; k++) {
     const uint32_t x = x0 + k, t = (tok >> (8 * k)) & 0xFFu, e = (ext >> (8 * k)) & 0xFFu;
@@ -1156,18 +1172,16 @@ __device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uin
 
 // The sequence at x, which cand_steps accepted (no checks left to make).
 __device__ __forceinline__ void seq_parse(const lds_u8* ib, uint32_t x, Seq& s) {
-  const uint32_t t = ib[x & (kIb - 1)], ln = t >> 4;
-  uint32_t y = x + 1, lit = ln;
-  if (ln == 15) lit += ib[(y++) & (kIb - 1)];
-  const uint32_t le = y + lit;
-  s.lit_pos = y;
+  const uint32_t t = ib[x & (kIb - 1)], e = ib[(x + 1) & (kIb - 1)];
+  const uint32_t lx = (t >> 4) == 15, lit = lx ? 15 + e : t >> 4;
+  const uint32_t le = x + 1 + lx + lit;
+  const uint32_t o0 = ib[le & (kIb - 1)], o1 = ib[(le + 1) & (kIb - 1)], e2 = ib[(le + 2) & (kIb - 1)];
+  const uint32_t mx = (t & 15) == 15;
+  s.lit_pos = x + 1 + lx;
   s.lit = lit;
-  s.off = ib[le & (kIb - 1)] | ((uint32_t)ib[(le + 1) & (kIb - 1)] << 8);
-  y = le + 2;
-  uint32_t ml = (t & 15) + 4;
-  if ((t & 15) == 15) ml += ib[(y++) & (kIb - 1)];
-  s.ml = ml;
-  s.next = y;
+  s.off = o0 | (o1 << 8);
+  s.ml = (t & 15) + 4 + (mx ? e2 : 0u);
+  s.next = le + 2 + mx;
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {  // DPP: no LDS round trips
