@@ -14,7 +14,8 @@ from .read import (  # noqa: F401
     unpack_bitmap,
 )
 from .write import NativeWriter, WriteOptions, encode_column, encode_column_device, encode_page, page_seed  # noqa: F401,E402
-from .shard import Shard, shard_pages  # noqa: F401,E402
+from .shard import (Shard, exclusive_bases, gather_sizes, rebase_offsets, shard_base, shard_pages,  # noqa: F401,E402
+                    shard_slice)
 from .binary import (  # noqa: F401,E402
     BINARY, LARGE_BINARY, LARGE_UTF8, UTF8, BinaryColumnDecoder, batch_read_binary, encode_binary_column,
     encode_binary_column_device,

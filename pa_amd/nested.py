@@ -114,6 +114,18 @@ class ListColumnDecoder:
         self.num_rows = int(L.sb_plan_num_rows(h))
         self.num_leaves = int(L.sb_plan_num_leaves(h))
 
+    @classmethod
+    def for_shard(cls, chunk, page_metas, shard, dtype, list_nullable: bool, item_nullable: bool, ctx=None, large: bool = False, timing: bool = False):
+        """The decoder of one rank's page range (pa_amd.shard_pages): only the
+        shard's bytes are planned and decoded; rows start at shard.row_offset
+        of the whole column."""
+        from .shard import shard_slice
+
+        part, metas = shard_slice(chunk, page_metas, shard)
+        dec = cls(part, metas, dtype, list_nullable, item_nullable, ctx, large, timing)
+        dec.shard = shard
+        return dec
+
     def alloc_outputs(self):
         torch = self._torch
         dev = f"cuda:{self.ctx.device}"

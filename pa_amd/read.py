@@ -217,6 +217,18 @@ class ColumnDecoder:
         self.num_rows = int(N.lib().sb_plan_num_rows(h))
         self._torch = torch
 
+    @classmethod
+    def for_shard(cls, chunk, page_metas, shard, dtype, nullable: bool, ctx=None, timing: bool = False):
+        """The decoder of one rank's page range (pa_amd.shard_pages): only the
+        shard's bytes are planned and decoded; rows start at shard.row_offset
+        of the whole column."""
+        from .shard import shard_slice
+
+        part, metas = shard_slice(chunk, page_metas, shard)
+        dec = cls(part, metas, dtype, nullable, ctx, timing)
+        dec.shard = shard
+        return dec
+
     def alloc_outputs(self):
         torch = self._torch
         dev = f"cuda:{self.ctx.device}"

@@ -43,3 +43,45 @@ def shard_pages(metas: Sequence, world: int) -> List[Shard]:
         byte_off += blen
         row_off += rows
     return shards
+
+
+def shard_slice(chunk, metas: Sequence, shard: Shard):
+    """The shard's bytes of the column chunk (host bytes or a device tensor
+    view) and its page metas: a rank reads nothing outside its range."""
+    return chunk[shard.byte_offset:shard.byte_offset + shard.byte_len], list(metas[shard.page_begin:shard.page_end])
+
+
+def exclusive_bases(sizes: Sequence[int]) -> List[int]:
+    """Exclusive scan: where each shard's variable-size output (Utf8 value
+    bytes, List leaves) starts in the whole column."""
+    out, acc = [], 0
+    for s in sizes:
+        out.append(acc)
+        acc += int(s)
+    return out
+
+
+def gather_sizes(local: int, group=None) -> List[int]:
+    """All ranks' local sizes in rank order (one int64 all-gather; gloo on
+    CPU, RCCL when the process group is nccl and the tensor is on a GPU)."""
+    import torch
+    import torch.distributed as dist
+
+    dev = "cpu"
+    if dist.get_backend(group) == "nccl":
+        dev = f"cuda:{torch.cuda.current_device()}"
+    t = torch.tensor([int(local)], dtype=torch.int64, device=dev)
+    parts = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, t, group=group)
+    return [int(p.item()) for p in parts]
+
+
+def shard_base(local: int, rank: int, group=None) -> int:
+    """This rank's base in the whole column's variable-size output."""
+    return exclusive_bases(gather_sizes(local, group))[rank]
+
+
+def rebase_offsets(offsets, base: int):
+    """A shard's offsets (starting at 0) moved onto the whole column's values:
+    rows [row_offset, row_offset + rows] of the column's offsets."""
+    return offsets + base

@@ -1,8 +1,13 @@
-"""N>1 path on CPU: world_size 2 over gloo.  Each rank takes its page range
-of one column chunk (pa_amd.shard_pages), decodes it (the
-oracle stands in for the GPU here), and the shards gathered in rank order
-equal the whole-column decode; the bench's max-over-ranks timing reduction
-is exercised the same way."""
+"""N>1 path on CPU: world_size 2 over gloo.  Each rank
+takes its page range of a column chunk (pa_amd.shard_pages), decodes it --
+with pa_amd's decoders (ColumnDecoder / BinaryColumnDecoder /
+ListColumnDecoder .for_shard) when a GPU is present, else with the oracle
+standing in -- and places it in the whole column: flat rows at the shard's
+row_offset; Utf8 offsets rebased by the exclusive scan of the ranks' value
+bytes, List offsets by the scan of their leaf counts (pa_amd.gather_sizes /
+exclusive_bases, one all-gather).  The reassembled column must equal the
+whole-column decode of the oracle bit for bit; the bench's max-over-ranks
+timing reduction is exercised the same way."""
 import os
 import socket
 
@@ -19,6 +24,58 @@ def _free_port():
     return p
 
 
+def _columns():
+    import pa_amd
+
+    rng = np.random.default_rng(5)
+    v = rng.integers(0, 1 << 14, 50000).astype(np.int32)
+    opts = pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=4096)
+    ichunk, imetas = pa_amd.encode_column(v, None, False, opts)
+    strs = [str(x).encode() * int(rng.integers(0, 3)) for x in rng.integers(0, 10**6, 30000)]
+    svals, soffs = pa_amd.binary.strings_to_arrow(strs)
+    svalid = rng.random(len(strs)) > 0.1
+    schunk, smetas = pa_amd.encode_binary_column(svals, soffs, svalid, True,
+                                                 pa_amd.WriteOptions(default_compression=1, max_page_size=2048))
+    lens = rng.integers(0, 6, 20000)
+    loffs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    child = rng.integers(-1000, 1000, int(loffs[-1])).astype(np.int64)
+    lchunk, lmetas = pa_amd.encode_list_column(loffs, child, None, None, False, False,
+                                               pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=1500))
+    return (ichunk, imetas), (schunk, smetas), (lchunk, lmetas)
+
+
+def _decode(kind, chunk, metas, sh, gpu):
+    """(offsets|None, values, validity|None) of one shard, as numpy."""
+    import pa_amd
+    from oracle import oracle as O
+
+    if gpu:
+        import torch
+
+        d = torch.from_numpy(np.frombuffer(chunk, np.uint8).copy()).cuda()
+        if kind == "int":
+            dec = pa_amd.ColumnDecoder.for_shard(d, metas, sh, np.int32, False)
+            v, _ = dec.decode()
+            return None, v.cpu().numpy()[:dec.num_rows], None
+        if kind == "utf8":
+            dec = pa_amd.BinaryColumnDecoder.for_shard(d, metas, sh, pa_amd.UTF8, True)
+            o, v, m = dec.decode()
+            valid = pa_amd.read.unpack_bitmap(m, dec.num_rows).cpu().numpy()
+            return o.cpu().numpy().astype(np.int64), v[:dec.values_bytes].cpu().numpy().tobytes(), valid
+        dec = pa_amd.ListColumnDecoder.for_shard(d, metas, sh, np.int64, False, False)
+        o, _, v, _ = dec.decode()
+        return o.cpu().numpy().astype(np.int64), v.cpu().numpy()[:dec.num_leaves], None
+    part, pm = pa_amd.shard_slice(chunk, metas, sh)
+    pm = [(m.length, m.num_values) for m in pm]
+    if kind == "int":
+        v, _ = O.read_column(part, pm, np.int32)
+        return None, v, None
+    if kind == "utf8":
+        return O.read_binary_column(part, pm, True)
+    o, _, v, _ = O.read_list_column(part, pm, np.int64, False, False)
+    return o, v, None
+
+
 def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
@@ -28,23 +85,40 @@ def _worker(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    rng = np.random.default_rng(5)
-    v = rng.integers(0, 1 << 14, 50000).astype(np.int32)
-    chunk, metas = pa_amd.encode_column(v, None, False, pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=4096))
-    shards = pa_amd.shard_pages(metas, world)
-    me = shards[rank]
-    mine = chunk[me.byte_offset:me.byte_offset + me.byte_len]
-    out, _ = O.read_column(mine, [(m.length, m.num_values) for m in metas[me.page_begin:me.page_end]], np.int32)
-    assert len(out) == me.rows
-    sizes = [s.rows for s in shards]
-    buf = torch.zeros(max(sizes), dtype=torch.int32)
-    buf[: me.rows] = torch.from_numpy(out)
-    gathered = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(gathered, buf)
-    full = np.concatenate([g[:n].numpy() for g, n in zip(gathered, sizes)])
+    gpu = torch.cuda.is_available()
+    ok = {}
+    for kind, (chunk, metas) in zip(("int", "utf8", "list"), _columns()):
+        shards = pa_amd.shard_pages(metas, world)
+        me = shards[rank]
+        offs, vals, valid = _decode(kind, chunk, metas, me, gpu)
+        whole = [(m.length, m.num_values) for m in metas]
+        parts = [None] * world
+        if kind == "int":
+            assert len(vals) == me.rows
+            dist.all_gather_object(parts, (me.row_offset, vals))
+            full = np.concatenate([p[1] for p in sorted(parts, key=lambda p: p[0])])
+            ok[kind] = bool((full == O.read_column(chunk, whole, np.int32)[0]).all())
+            continue
+        # variable-size outputs: this rank's base from the scan of all ranks' sizes
+        nvals = len(vals)
+        base = pa_amd.shard_base(nvals, rank)
+        rows_base = pa_amd.shard_base(len(offs) - 1, rank)
+        g = pa_amd.rebase_offsets(offs, base)
+        dist.all_gather_object(parts, (rows_base, g, vals, valid))
+        parts.sort(key=lambda p: p[0])
+        go = np.concatenate([parts[0][1][:1]] + [p[1][1:] for p in parts])
+        if kind == "utf8":
+            eo, ev, em = O.read_binary_column(chunk, whole, True)
+            gv = b"".join(p[2] for p in parts)
+            gm = np.concatenate([p[3] for p in parts])
+            ok[kind] = bool((go == eo).all() and gv == ev and (gm == em).all())
+        else:
+            eo, _, ev, _ = O.read_list_column(chunk, whole, np.int64, False, False)
+            gv = np.concatenate([p[2] for p in parts])
+            ok[kind] = bool((go == eo).all() and (gv == ev).all())
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    q.put((rank, bool((full == v).all()), float(t[0])))
+    q.put((rank, ok, float(t[0])))
     dist.destroy_process_group()
 
 
@@ -56,12 +130,19 @@ def test_page_shards_reassemble(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in procs]
+    res = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert all(ok for _, ok, _ in res)
+    for _, ok, _ in res:
+        assert ok == {"int": True, "utf8": True, "list": True}, ok
     assert all(t == float(world) for _, _, t in res)
+
+
+def test_exclusive_bases():
+    import pa_amd
+
+    assert pa_amd.exclusive_bases([3, 0, 5, 2]) == [0, 3, 3, 8]
 
 
 def test_shard_pages_balanced():
