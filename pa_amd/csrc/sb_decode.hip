@@ -1963,6 +1963,12 @@ __global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) 
   for (uint32_t j = blockIdx.x * kInfWaves + wv; j < n; j += gridDim.x * kInfWaves) {
     const InflateJob jb = a.jobs[j];
     const uint64_t kind = jb.dst >> 62, off = jb.dst & kDstMask;
+#ifdef SB_V_SKIPSCRATCH
+    if (kind == 1) continue;
+#endif
+#ifdef SB_V_SKIPVALS
+    if (kind == 2) continue;
+#endif
     uint8_t* dst = kind == 1 ? a.scratch + off : a.out + (kind == 2 ? a.bases[off] : off);
     const uint8_t* src = a.chunk + jb.src;
     WaveOut<true> o;
@@ -2274,6 +2280,19 @@ __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int n
   return true;
 }
 
+// A slot of `per` entries for each active lane with `want`, from one atomic
+// on *ctr per wave (lanes in lane order).
+__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr, bool want, uint32_t per) {
+  const uint64_t m = __ballot(want);
+  if (!m) return 0;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  uint32_t base = 0;
+  if ((threadIdx.x & 63) == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m) * per);
+  base = (uint32_t)__shfl((int)base, (int)leader, 64);
+  return base + rank * per;
+}
+
 // Classifies every page (one thread each): header-only pages get their two
 // inflate jobs and size here; the rest are listed for k_bin_size.
 template <int OW>
@@ -2283,17 +2302,19 @@ __global__ __launch_bounds__(NT) void k_bin_light(BinArgs a) {
   for (uint32_t page = blockIdx.x * NT + threadIdx.x; page < np; page += gridDim.x * NT) {
     const PageDesc pd = a.pages[page];
     LightPage lp;
-    if (bin_light_parse(GlbSrc{a.chunk + pd.byte_off}, pd.byte_len, pd.num_values, a.nullable, lp)) {
-      const uint32_t slot = atomicAdd(a.job_count, 2u);
+    const bool lt = bin_light_parse(GlbSrc{a.chunk + pd.byte_off}, pd.byte_len, pd.num_values, a.nullable, lp);
+    // one atomic per wave and counter (12k contended atomics on one address cost ~100 us)
+    const uint32_t slot = wave_slot(a.job_count, lt, 2), li = wave_slot(&cnt[1], lt, 1), si = wave_slot(&cnt[0], !lt, 1);
+    if (lt) {
       a.jobs[slot] = InflateJob{pd.byte_off + lp.ob, kDstScratch | ((pd.row_off + page) * OW), lp.ocs,
                                 (pd.num_values + 1) * (uint32_t)OW, lp.codec, page};
       a.jobs[slot + 1] = InflateJob{pd.byte_off + lp.vb, kDstBinBase | page, lp.vcs, lp.S, lp.codec, page};
       a.sizes[page] = lp.S;
       a.status[page] = 0;
       vbpos[page] = lp.vbpos;
-      light[atomicAdd(&cnt[1], 1u)] = page;
+      light[li] = page;
     } else {
-      staged[atomicAdd(&cnt[0], 1u)] = page;
+      staged[si] = page;
     }
   }
 }
