@@ -63,6 +63,7 @@ struct sb_plan {
   sb::PageDesc* d_pages = nullptr;
   uint32_t* d_status = nullptr;
   uint32_t* d_lists = nullptr;  // [staged list | global list]
+  uint32_t* d_light = nullptr;  // fixed width: per-page header-only tags (k_fix_light)
   uint32_t* d_defer = nullptr;  // [defer count x2 | inflate job count x2 | work list...]
   sb::InflateJob* d_jobs = nullptr;  // fixed: one per page; binary: two per page
   uint8_t* d_scratch = nullptr;      // binary: expanded offsets streams
@@ -190,6 +191,7 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_pages) (void)hipFree(p->d_pages);
   if (p->d_status) (void)hipFree(p->d_status);
   if (p->d_lists) (void)hipFree(p->d_lists);
+  if (p->d_light) (void)hipFree(p->d_light);
   if (p->d_defer) (void)hipFree(p->d_defer);
   if (p->d_jobs) (void)hipFree(p->d_jobs);
   if (p->d_scratch) (void)hipFree(p->d_scratch);
@@ -267,6 +269,7 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
   if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&p->d_lists, np * sizeof(uint32_t));
+  if (e == hipSuccess && !owidth && !is_bool) e = hipMalloc(&p->d_light, np * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&p->d_defer, (np + 4) * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemsetAsync(p->d_defer, 0, 4 * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipMalloc(&p->d_jobs, (owidth ? 2 : 1) * np * sizeof(sb::InflateJob));
@@ -284,6 +287,32 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   if (e != hipSuccess) {
     sb_plan_destroy(p);
     return fail(ctx, SB_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
+  }
+  if (p->d_light && n_pages) {
+    // Classify once: the per-decode classify pass (one thread per page) runs
+    // only for chunks that hold header-only pages; the staged pass handles
+    // every page correctly either way.
+    sb::LaunchArgs c{};
+    c.chunk = d_chunk;
+    c.pages = p->d_pages;
+    c.nullable = desc->nullable;
+    c.status = p->d_status;
+    c.job_count = p->d_defer + 2;
+    c.jobs = p->d_jobs;
+    uint32_t n_light = 0;
+    e = sb::launch_fix_light(c, (uint32_t)n_pages, width, is_float, p->d_light, ctx->stream) ? hipErrorUnknown
+                                                                                              : hipSuccess;
+    if (e == hipSuccess) e = hipMemcpyAsync(&n_light, p->d_defer + 2, 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(p->d_defer, 0, 4 * sizeof(uint32_t), ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "plan classify: %s", hipGetErrorString(e));
+    }
+    if (!n_light) {
+      (void)hipFree(p->d_light);
+      p->d_light = nullptr;
+    }
   }
   if (p->binary && n_pages) {  // size every page's values once: they are fixed for the plan
     e = hipMalloc(&p->d_bin, (2 * np + 2) * sizeof(uint64_t) + (3 * np + 2) * sizeof(uint32_t));
@@ -401,6 +430,11 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
       p->timed = true;
     }
     return SB_OK;
+  }
+  if (p->d_light) {  // header-only pages: inflate jobs without staging
+    if (sb::launch_fix_light(a, (uint32_t)p->n_pages, p->width, p->is_float, p->d_light, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "page classify launch failed: %s", hipGetErrorString(hipGetLastError()));
+    a.light = p->d_light;
   }
   a.list = p->staged_identity ? nullptr : p->d_lists;
   a.n_list = p->n_staged;

@@ -788,8 +788,68 @@ struct WaveOut {
     if (RING && q < far_limit()) return __builtin_amdgcn_raw_buffer_load_b8(rs, q, 0, 16);
     return ring[slot(q)];
   }
-  // len literal bytes from HBM, up to a chunk per step (16 loads per lane in flight)
+  // n (a multiple of kChunk) stream bytes straight to d: 16 bytes a lane per
+  // KiB, two KiB per step, no waits between steps
+  __device__ void copy_direct(gmem_u8* src, uint8_t* d, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
+    gmem_u32* s32 = (gmem_u32*)((uintptr_t)src - sh);
+    const uint32_t dal = (uint32_t)((uintptr_t)d & 15);
+    for (uint32_t c = 0; c < n; c += 2 * kChunk) {
+      uint32_t w[2][5];
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t x = c + h * kChunk + 16 * lane, i = (sh + x) >> 2;
+        const bool on = c + h * kChunk < n;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) w[h][k] = on ? s32[i + k] : 0u;
+        w[h][4] = on && sh ? s32[i + 4] : 0u;  // the dword past byte x + 15 only when x is unaligned
+      }
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        if (c + h * kChunk >= n) break;
+        const uint32_t x = c + h * kChunk + 16 * lane;
+        u32x4 v;
+        v.x = __builtin_amdgcn_alignbyte(w[h][1], w[h][0], sh);
+        v.y = __builtin_amdgcn_alignbyte(w[h][2], w[h][1], sh);
+        v.z = __builtin_amdgcn_alignbyte(w[h][3], w[h][2], sh);
+        v.w = __builtin_amdgcn_alignbyte(w[h][4], w[h][3], sh);
+        if (dal == 0) {
+          *(u32x4*)(d + x) = v;
+        } else if ((dal & 3) == 0) {
+          uint32_t* q = (uint32_t*)(d + x);
+          q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
+        } else {
+#pragma unroll
+          for (uint32_t b = 0; b < 16; b++) d[x + b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
+        }
+      }
+    }
+  }
+  // len literal bytes from HBM.  Whole chunks more than three chunks before
+  // the literal's end go straight to the destination (they are history only
+  // far reads reach, and the three ring flushes after them wait for their
+  // stores); the rest goes through the ring, a chunk per step.
   __device__ void lit_global(gmem_u8* src, uint32_t len) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (RING && len > 5 * kChunk) {
+      const uint32_t h = (kChunk - (op & (kChunk - 1))) & (kChunk - 1);
+      if (h) {
+        lit_ring(src, h);
+        src += h;
+        len -= h;
+      }
+      const uint32_t direct = (len / kChunk - 3) * kChunk;
+      copy_direct(src, dst + op, direct);
+      op += direct;
+      src += direct;
+      len -= direct;
+    }
+    (void)lane;
+    lit_ring(src, len);
+  }
+  // len literal bytes from HBM through the ring, up to a chunk per step (16 loads per lane in flight)
+  __device__ void lit_ring(gmem_u8* src, uint32_t len) {
     const uint32_t lane = threadIdx.x & 63;
     while (len) {
       const uint32_t m = min(len, RING ? kChunk - (op & (kChunk - 1)) : kChunk);
@@ -1867,6 +1927,82 @@ __device__ __forceinline__ uint32_t stage_page(u32x4* stage, const uint8_t* pg, 
   return base;
 }
 
+// The validity prefix as parse_validity reads it (one thread, from HBM):
+// false for anything but a valid bit-packed prefix of a non-empty page.
+__device__ bool light_validity(const GlbSrc& s, uint32_t len, uint32_t n, int nullable, uint32_t* pp, uint32_t* vbpos) {
+  uint32_t p = 0;
+  *vbpos = 0;
+  if (n == 0) return false;
+  if (nullable) {
+    if (len < 4) return false;
+    const uint32_t def_len = s.u32(0);
+    p = 4;
+    if (def_len == 0 || def_len > len - p) return false;
+    uint32_t q = p, h = 0, sft = 0;
+    for (;;) {
+      if (q >= p + def_len || sft > 28) return false;
+      const uint32_t c = s.u8(q++);
+      h |= (c & 0x7Fu) << sft;
+      if (!(c & 0x80)) break;
+      sft += 7;
+    }
+    if (!(h & 1)) return false;
+    if ((uint64_t)min(h >> 1, p + def_len - q) * 8 < n) return false;
+    *vbpos = q;  // >= 5: 0 means no bitmap
+    p += def_len;
+  }
+  *pp = p;
+  return true;
+}
+
+// A slot of `per` entries for each active lane with `want`, from one atomic
+// on *ctr per wave (lanes in lane order).
+__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr, bool want, uint32_t per) {
+  const uint64_t m = __ballot(want);
+  if (!m) return 0;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  uint32_t base = 0;
+  if ((threadIdx.x & 63) == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m) * per);
+  base = (uint32_t)__shfl((int)base, (int)leader, 64);
+  return base + rank * per;
+}
+
+// Header-only fixed-width pages: the leaf is LZ4 / Snappy (or, for Float
+// columns, Patas) with no cascade, so the page needs no staging: one thread
+// reads the validity prefix and the stream header from HBM (the checks of
+// decode_page), appends the k_inflate job and tags the page; the staged /
+// global passes then only copy its validity bits.
+__global__ __launch_bounds__(NT) void k_fix_light(LaunchArgs a, uint32_t n_pages, uint32_t W, uint32_t flt,
+                                                   uint32_t* light) {
+  for (uint32_t page = blockIdx.x * NT + threadIdx.x; page < n_pages; page += gridDim.x * NT) {
+    const PageDesc pd = a.pages[page];
+    const GlbSrc s{a.chunk + pd.byte_off};
+    const uint32_t len = pd.byte_len, n = pd.num_values;
+    uint32_t p = 0, vb = 0, codec = 0, cs = 0;
+    bool lt = light_validity(s, len, n, a.nullable, &p, &vb) && p + 9 <= len;
+    if (lt) {
+      codec = s.u8(p);
+      cs = s.u32(p + 1);
+      lt = cs <= len - (p + 9) && (codec == 1 || codec == 3 || (flt && codec == 16));
+    }
+    const uint32_t slot = wave_slot(a.job_count + a.parity, lt, 1);
+    if (lt) {
+      a.jobs[slot] = InflateJob{pd.byte_off + p + 9, pd.row_off * W, cs, n * W, codec == 16 ? 16u | (W << 8) : codec, page};
+      a.status[page] = 0;
+    }
+    light[page] = lt ? 1 + vb : 0u;
+  }
+}
+
+// A header-only page in the staged / global passes: its validity bits only.
+__device__ __forceinline__ bool light_page(const LaunchArgs& a, const PageDesc& pd, uint32_t page) {
+  const uint32_t lt = a.light ? a.light[page] : 0u;
+  if (!lt) return false;
+  if (lt > 1) write_validity(GlbSrc{a.chunk + pd.byte_off}, lt - 1, pd.num_values, pd.row_off, a.out_validity);
+  return true;
+}
+
 template <int W, bool FLT>
 __global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
   extern __shared__ u32x4 stage[];
@@ -1880,6 +2016,7 @@ __global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
       a.job_count[a.parity ^ 1] = 0;
     }
   }
+  if (light_page(a, pd, page)) return;
   const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
   LdsSrc s{(const uint32_t*)stage, base};
   decode_page<W, FLT, 0>(s, sh, pd, a, page);
@@ -1898,6 +2035,7 @@ __global__ __launch_bounds__(NT) void k_decode_global(LaunchArgs a) {
     a.defer_count[a.parity ^ 1] = 0;
     a.job_count[a.parity ^ 1] = 0;
   }
+  if (light_page(a, pd, page)) return;
   GlbSrc s{a.chunk + pd.byte_off};
   decode_page<W, FLT, 0>(s, sh, pd, a, page);
   __syncthreads();
@@ -2243,27 +2381,8 @@ struct LightPage {
 };
 
 __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int nullable, LightPage& lp) {
-  uint32_t p = 0;
-  lp.vbpos = 0;
-  if (n == 0) return false;
-  if (nullable) {
-    if (len < 4) return false;
-    const uint32_t def_len = s.u32(0);
-    p = 4;
-    if (def_len == 0 || def_len > len - p) return false;
-    uint32_t q = p, h = 0, sft = 0;
-    for (;;) {
-      if (q >= p + def_len || sft > 28) return false;
-      const uint32_t c = s.u8(q++);
-      h |= (c & 0x7Fu) << sft;
-      if (!(c & 0x80)) break;
-      sft += 7;
-    }
-    if (!(h & 1)) return false;
-    if ((uint64_t)min(h >> 1, p + def_len - q) * 8 < n) return false;
-    lp.vbpos = q;  // >= 5: 0 means no bitmap
-    p += def_len;
-  }
+  uint32_t p;
+  if (!light_validity(s, len, n, nullable, &p, &lp.vbpos)) return false;
   if (p + 9 > len) return false;
   lp.codec = s.u8(p);
   if (lp.codec != 1 && lp.codec != 3) return false;
@@ -2278,19 +2397,6 @@ __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int n
   lp.ob = body;
   lp.ocs = cs;
   return true;
-}
-
-// A slot of `per` entries for each active lane with `want`, from one atomic
-// on *ctr per wave (lanes in lane order).
-__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr, bool want, uint32_t per) {
-  const uint64_t m = __ballot(want);
-  if (!m) return 0;
-  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-  uint32_t base = 0;
-  if ((threadIdx.x & 63) == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m) * per);
-  base = (uint32_t)__shfl((int)base, (int)leader, 64);
-  return base + rank * per;
 }
 
 // Classifies every page (one thread each): header-only pages get their two
@@ -3241,6 +3347,13 @@ __global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
 }  // namespace sbk
 
 namespace sb {
+int launch_fix_light(const LaunchArgs& a, uint32_t n_pages, int width, bool is_float, uint32_t* light, void* stream) {
+  if (!n_pages) return 0;
+  hipLaunchKernelGGL(sbk::k_fix_light, dim3((n_pages + sbk::NT - 1) / sbk::NT), dim3(sbk::NT), 0, (hipStream_t)stream,
+                     a, n_pages, (uint32_t)width, (uint32_t)is_float, light);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (is_float) {

@@ -99,10 +99,14 @@ struct LaunchArgs {
   uint32_t parity;
   uint32_t* job_count;    // [2]: inflate job counts, double-buffered like defer_count
   InflateJob* jobs;       // CH_LEAF LZ4 / Snappy pages, expanded by k_inflate
+  const uint32_t* light;  // per page: 0, or 1 + validity bitmap position of a header-only page (k_fix_light)
 };
 
 // kind: 0 = LDS-staged pages, 1 = pages read from HBM, 2 = deferred work list
 int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a, void* stream);
+// Header-only fixed-width pages (LZ4 / Snappy leaf, Float Patas leaf): their
+// inflate jobs and light[] tags, one thread per page, before the staged pass.
+int launch_fix_light(const LaunchArgs& a, uint32_t n_pages, int width, bool is_float, uint32_t* light, void* stream);
 
 // Boolean pages: one workgroup per page (grid-strided), page + expanded
 // bitmap in a.stage_bytes of dynamic LDS.
