@@ -362,6 +362,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   if (!out->d_offsets || (p->values_bytes && (!out->d_values || out->values_capacity < p->values_bytes)))
     return fail(ctx, SB_E_ARG, "binary output buffers too small");
   if (p->desc.nullable && p->n_rows && !out->d_validity) return fail(ctx, SB_E_ARG, "validity buffer is null");
+  if ((uintptr_t)out->d_offsets % p->offset_width) return fail(ctx, SB_E_ARG, "offsets buffer is not aligned");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   if (p->desc.nullable && p->validity_needs_zero)
     HIP_TRY(ctx, hipMemsetAsync(out->d_validity, 0, (p->n_rows + 31) / 32 * 4, ctx->stream));
@@ -382,7 +383,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
                   p->bin_grid};
   if (p->n_bin_jobs) {  // Basic LZ4 / Snappy pages: streams expanded first, one wave each
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2, p->n_bin_jobs, out->d_values, p->d_scratch,
-                        p->d_bin + np, p->d_status};
+                        p->d_bin + np, p->d_status, (uint8_t*)out->d_offsets};
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
   }

@@ -720,8 +720,23 @@ struct WaveOut {
   uint32_t dal;                // dst & 3
   uint32_t olen;
   uint32_t op;
+  // Rebased offsets stream (RING, dst dword-aligned): every stored word gets
+  // xadd; past the column's first page stream word 0 is not stored (the
+  // previous page's last offset owns that slot: decompress_binary drops p[0],
+  // binary/mod.rs:136-144) but kept in w0; far reads undo both.
+  bool xf, skip0;
+  uint32_t xadd, w0;
 
   __device__ __forceinline__ uint32_t slot(uint32_t q) const { return RING ? (q & (kRing - 1)) : q; }
+  __device__ __forceinline__ uint32_t far8(uint32_t q) const {  // stream byte q < far_limit(), from HBM
+    if (!xf) return __builtin_amdgcn_raw_buffer_load_b8(rs, q, 0, 16);  // sc1: device scope, misses L1
+    const uint32_t w = q < 4 ? w0 : __builtin_amdgcn_raw_buffer_load_b32(rsa, q & ~3u, 0, 16) - xadd;
+    return (w >> (8 * (q & 3))) & 0xFFu;
+  }
+  __device__ __forceinline__ uint32_t far32(uint32_t a, bool on) const {  // dword at dst-aligned byte a (0 if !on)
+    const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(rsa, on ? a : 0x80000000u, 0, 16);
+    return !xf ? g : a == 0 ? w0 : g - xadd;
+  }
   // History below this position is read from HBM: writes of up to one chunk
   // past op overwrite the ring slots of chunks k-4 and k-3, and the flushes of
   // chunks <= k-2 have completed (each flush first waits for the previous).
@@ -742,6 +757,14 @@ struct WaveOut {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     uint8_t* d = dst + c0;
+    if (RING && xf) {  // dst is dword-aligned; len is a multiple of 4
+      const __attribute__((address_space(3))) uint32_t* r32 = (const __attribute__((address_space(3))) uint32_t*)ring;
+      if (c0 == 0) w0 = r32[0];
+      uint32_t* d32 = (uint32_t*)d;
+      for (uint32_t w = lane; w < len / 4; w += 64)
+        if (!skip0 || (c0 | w)) d32[w] = r32[slot(c0 + 4 * w) >> 2] + xadd;
+      return;
+    }
     if (len == kChunk) {
       const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(ring + slot(c0 + 16 * lane));
       const uintptr_t al = (uintptr_t)d;
@@ -774,7 +797,7 @@ struct WaveOut {
       const uint32_t q = op - off + (off >= 64 ? lane : lane % off);
       uint32_t v;
       if (RING && q < far_limit())
-        v = __builtin_amdgcn_raw_buffer_load_b8(rs, q, 0, 16);  // sc1: device scope, misses L1
+        v = far8(q);
       else
         v = ring[slot(q)];
       ring[slot(op + lane)] = (uint8_t)v;
@@ -785,16 +808,17 @@ struct WaveOut {
     if (RING && (op & (kChunk - 1))) flush(op & ~(kChunk - 1), op & (kChunk - 1));
   }
   __device__ __forceinline__ uint32_t hist(uint32_t q) const {
-    if (RING && q < far_limit()) return __builtin_amdgcn_raw_buffer_load_b8(rs, q, 0, 16);
+    if (RING && q < far_limit()) return far8(q);
     return ring[slot(q)];
   }
   // n (a multiple of kChunk) stream bytes straight to d: 16 bytes a lane per
   // KiB, two KiB per step, no waits between steps
-  __device__ void copy_direct(gmem_u8* src, uint8_t* d, uint32_t n) {
+  __device__ void copy_direct(gmem_u8* src, uint8_t* d, uint32_t n, uint32_t pos) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
     gmem_u32* s32 = (gmem_u32*)((uintptr_t)src - sh);
     const uint32_t dal = (uint32_t)((uintptr_t)d & 15);
+    if (xf && pos == 0) w0 = __builtin_amdgcn_alignbyte(s32[1], s32[0], sh);
     for (uint32_t c = 0; c < n; c += 2 * kChunk) {
       uint32_t w[2][5];
 #pragma unroll
@@ -814,7 +838,11 @@ struct WaveOut {
         v.y = __builtin_amdgcn_alignbyte(w[h][2], w[h][1], sh);
         v.z = __builtin_amdgcn_alignbyte(w[h][3], w[h][2], sh);
         v.w = __builtin_amdgcn_alignbyte(w[h][4], w[h][3], sh);
-        if (dal == 0) {
+        if (xf) {
+          uint32_t* q = (uint32_t*)(d + x);
+          if (!skip0 || pos + x) q[0] = v.x + xadd;
+          q[1] = v.y + xadd; q[2] = v.z + xadd; q[3] = v.w + xadd;
+        } else if (dal == 0) {
           *(u32x4*)(d + x) = v;
         } else if ((dal & 3) == 0) {
           uint32_t* q = (uint32_t*)(d + x);
@@ -840,7 +868,7 @@ struct WaveOut {
         len -= h;
       }
       const uint32_t direct = (len / kChunk - 3) * kChunk;
-      copy_direct(src, dst + op, direct);
+      copy_direct(src, dst + op, direct, op);
       op += direct;
       src += direct;
       len -= direct;
@@ -1385,7 +1413,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
       for (uint32_t t = 0; t < NW; t++) {
         w[t] = 0;
         if (!__ballot(4 * t < need)) continue;
-        const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(o.rsa, mfar && 4 * t < need ? a0 + 4 * t : 0x80000000u, 0, 16);
+        const uint32_t g = o.far32(a0 + 4 * t, mfar && 4 * t < need);
         const uint32_t r = r32[((a0 + 4 * t) & (kRing - 1)) >> 2];
         w[t] = mfar ? g : r;
       }
@@ -1395,7 +1423,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     for (uint32_t i = 0; __ballot(fmix && i < s.ml); i++) {
       if (fmix && i < s.ml) {
         const uint32_t qq = src + i;
-        const uint32_t b = qq < farlim ? __builtin_amdgcn_raw_buffer_load_b8(o.rs, qq, 0, 16) : o.ring[qq & (kRing - 1)];
+        const uint32_t b = qq < farlim ? o.far8(qq) : o.ring[qq & (kRing - 1)];
         o.ring[(dm + i) & (kRing - 1)] = (uint8_t)b;
       }
     }
@@ -1411,7 +1439,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
         if (lane < M - c) {
           const uint32_t x = D + c;
           const uint32_t qq = x - O + (O >= 64 ? lane : lane_mod(lane, O));
-          const uint32_t b = qq < farlim ? __builtin_amdgcn_raw_buffer_load_b8(o.rs, qq, 0, 16) : o.ring[qq & (kRing - 1)];
+          const uint32_t b = qq < farlim ? o.far8(qq) : o.ring[qq & (kRing - 1)];
           o.ring[(x + lane) & (kRing - 1)] = (uint8_t)b;
         }
       }
@@ -2107,9 +2135,13 @@ __global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) 
 #ifdef SB_V_SKIPVALS
     if (kind == 2) continue;
 #endif
-    uint8_t* dst = kind == 1 ? a.scratch + off : a.out + (kind == 2 ? a.bases[off] : off);
+    uint8_t* dst = kind == 1 ? a.scratch + off : kind == 3 ? a.offs + off : a.out + (kind == 2 ? a.bases[off] : off);
     const uint8_t* src = a.chunk + jb.src;
     WaveOut<true> o;
+    o.xf = kind == 3;  // Utf8 offsets rebased onto the page's values base
+    o.xadd = kind == 3 ? (uint32_t)a.bases[jb.page] : 0u;
+    o.skip0 = kind == 3 && jb.page != 0;
+    o.w0 = 0;
     o.ring = (lds_u8*)&rings[wv][0];
     o.dst = dst;
     o.rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)jb.usize, 0x00020000);
@@ -2412,8 +2444,11 @@ __global__ __launch_bounds__(NT) void k_bin_light(BinArgs a) {
     // one atomic per wave and counter (12k contended atomics on one address cost ~100 us)
     const uint32_t slot = wave_slot(a.job_count, lt, 2), li = wave_slot(&cnt[1], lt, 1), si = wave_slot(&cnt[0], !lt, 1);
     if (lt) {
-      a.jobs[slot] = InflateJob{pd.byte_off + lp.ob, kDstScratch | ((pd.row_off + page) * OW), lp.ocs,
-                                (pd.num_values + 1) * (uint32_t)OW, lp.codec, page};
+      // Utf8 (32-bit) offsets are expanded straight into the column, rebased
+      // (k_inflate xf); LargeUtf8 offsets go through scratch
+      a.jobs[slot] = InflateJob{pd.byte_off + lp.ob,
+                                OW == 4 ? kDstBinOffs | (pd.row_off * 4) : kDstScratch | ((pd.row_off + page) * OW),
+                                lp.ocs, (pd.num_values + 1) * (uint32_t)OW, lp.codec, page};
       a.jobs[slot + 1] = InflateJob{pd.byte_off + lp.vb, kDstBinBase | page, lp.vcs, lp.S, lp.codec, page};
       a.sizes[page] = lp.S;
       a.status[page] = 0;
@@ -2443,7 +2478,15 @@ __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
       if constexpr (OW == 8) return ((const uint64_t*)xo)[k];
       else return (uint64_t)(int64_t)((const int32_t*)xo)[k];
     };
-    if (tid == 0) bad = (po(0) != 0 || po(n) != S || V + S > a.values_cap) ? ST_OUT_OF_SPEC : 0u;
+    // p[n] must be the values stream's length (DEVIATION: the reference only
+    // fails once the column's last offset passes its values, at try_new)
+    if (tid == 0) {
+      if constexpr (OW == 4)  // rebased in place by k_inflate
+        bad = ((uint32_t)((const uint32_t*)a.out_offsets)[R + n] != (uint32_t)(V + S) || V + S > a.values_cap) ? ST_OUT_OF_SPEC
+                                                                                        : 0u;
+      else
+        bad = (po(n) != S || V + S > a.values_cap) ? ST_OUT_OF_SPEC : 0u;
+    }
     __syncthreads();
     const uint32_t e = bad;
     __syncthreads();
@@ -2451,8 +2494,10 @@ __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
       if (tid == 0) a.status[page] = e;
       continue;
     }
-    if (R == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);
-    for (uint32_t k = tid + 1; k <= n; k += NT) bin_put_off(a.out_offsets, R + k, V + po(k), OW);
+    if constexpr (OW == 8) {
+      if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, po(0), OW);  // the first page keeps its p[0]
+      for (uint32_t k = tid + 1; k <= n; k += NT) bin_put_off(a.out_offsets, R + k, V + po(k), OW);
+    }
     const uint32_t vb = a.cls[2 * np + page];
     if (vb) write_validity(GlbSrc{a.chunk + pd.byte_off}, vb, n, R, a.out_validity);
   }
@@ -2596,7 +2641,7 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
     __syncthreads();
     if (!sh.err) {
       if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
-      if (R == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);
+      if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);  // Extend codecs push 0 first
       if (bi.codec == 2) {  // Zstd: wave 0 decodes both streams into LDS; they then read as a None page
         if (tid < 64) {
           const uint32_t tcap = a.lds_bytes - bi.ztab - kStagePad;
@@ -2628,19 +2673,22 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
             if constexpr (OW == 8) return ((const uint64_t*)xo)[i];
             else return (uint64_t)(int64_t)((const int32_t*)xo)[i];
           };
-          if (tid == 0 && (po(0) != 0 || po(n) != bi.S)) set_err(sh, ST_OUT_OF_SPEC);
+          if (tid == 0 && po(n) != bi.S) set_err(sh, ST_OUT_OF_SPEC);  // DEVIATION, as in k_bin_light_out
           __syncthreads();
-          if (!sh.err)
+          if (!sh.err) {
+            if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, po(0), OW);  // the first page keeps p[0]
             for (uint32_t i = tid + 1; i <= n; i += NT) bin_put_off(a.out_offsets, R + i, V + po(i), OW);
+          }
         } else {
           const uint32_t opos = bi.ob;  // stream position of p[0]
           if (tid == 0 && (bi.ocs != (n + 1) * OW || bi.vcs != bi.S)) set_err(sh, ST_OUT_OF_SPEC);  // copy_from_slice
           __syncthreads();
           if (!sh.err && tid == 0) {
-            if (ldo<OW>(s, opos) != 0 || ldo<OW>(s, opos + n * OW) != bi.S) set_err(sh, ST_OUT_OF_SPEC);
+            if (ldo<OW>(s, opos + n * OW) != bi.S) set_err(sh, ST_OUT_OF_SPEC);  // DEVIATION, as above
           }
           __syncthreads();
           if (!sh.err) {
+            if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, ldo<OW>(s, opos), OW);
             for (uint32_t i = tid + 1; i <= n; i += NT) bin_put_off(a.out_offsets, R + i, V + ldo<OW>(s, opos + i * OW), OW);
             copy_lds_to_global(lds, base + bi.vb, a.out_values + V, bi.S);
           }

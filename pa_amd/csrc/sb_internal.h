@@ -68,7 +68,8 @@ struct InflateJob {
   uint32_t codec, page;
 };
 static_assert(sizeof(InflateJob) == 32, "inflate job is 32 bytes");
-constexpr uint64_t kDstScratch = 1ull << 62, kDstBinBase = 2ull << 62, kDstMask = (1ull << 62) - 1;
+constexpr uint64_t kDstScratch = 1ull << 62, kDstBinBase = 2ull << 62, kDstBinOffs = 3ull << 62,
+                   kDstMask = (1ull << 62) - 1;
 
 struct InflateLaunch {
   const uint8_t* chunk;
@@ -79,6 +80,7 @@ struct InflateLaunch {
   uint8_t* scratch;
   const uint64_t* bases;
   uint32_t* status;
+  uint8_t* offs;  // kDstBinOffs jobs: the column's 32-bit offsets (dword-aligned)
 };
 int launch_inflate(const InflateLaunch& a, void* stream);
 constexpr uint32_t kInflateGrid = 2048;  // 4-wave workgroups: 8 waves per SIMD on 256 CUs
