@@ -1,0 +1,150 @@
+"""The nested-level oracle against pyarrow (arrow2/parquet2
+row).  pyarrow.parquet writes List<Int32> columns as Data Page V2 pages (rep
+and def levels as RLE / bit-packed hybrid streams with explicit lengths --
+the same streams a strawboat nested page carries, read_basic.rs:65-99).  Each
+page's level bytes are cut out of the file (a minimal Thrift compact reader
+for PageHeader), wrapped into a strawboat nested page ([rows][rep_len]
+[def_len][rep][def][values], values = every leaf slot), and read back by the
+oracle (orc_hybrid_decode + the read_validity_nested / create_list
+restatement); offsets, list validity, values and leaf validity must equal
+pyarrow's ListArray.  Runs on CPU; covers list/item nullability, empty and
+null lists, several pages per column."""
+import io
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pa = pytest.importorskip("pyarrow")
+pq = pytest.importorskip("pyarrow.parquet")
+
+
+class Compact:
+    """Just enough of Thrift's compact protocol to walk a PageHeader."""
+
+    def __init__(self, b, p):
+        self.b, self.p = b, p
+
+    def varint(self):
+        v = s = 0
+        while True:
+            c = self.b[self.p]
+            self.p += 1
+            v |= (c & 0x7F) << s
+            if not c & 0x80:
+                return v
+            s += 7
+
+    def zz(self):
+        v = self.varint()
+        return (v >> 1) ^ -(v & 1)
+
+    def value(self, t):
+        if t in (1, 2):
+            return t == 1
+        if t == 3:
+            self.p += 1
+            return self.b[self.p - 1]
+        if t in (4, 5, 6):
+            return self.zz()
+        if t == 7:
+            self.p += 8
+            return None
+        if t == 8:
+            n = self.varint()
+            self.p += n
+            return None
+        if t in (9, 10):
+            h = self.b[self.p]
+            self.p += 1
+            n, et = h >> 4, h & 15
+            if n == 15:
+                n = self.varint()
+            return [self.value(et) for _ in range(n)]
+        if t == 12:
+            return self.struct()
+        raise ValueError(f"thrift type {t}")
+
+    def struct(self):
+        out, fid = {}, 0
+        while True:
+            h = self.b[self.p]
+            self.p += 1
+            if h == 0:
+                return out
+            d, t = h >> 4, h & 15
+            fid = fid + d if d else self.zz()
+            out[fid] = self.value(t)
+
+
+def data_pages_v2(path):
+    """(rows, levels, rep bytes, def bytes, values bytes) of each data page of column 0."""
+    f = pq.ParquetFile(path)
+    cm = f.metadata.row_group(0).column(0)
+    raw = open(path, "rb").read()
+    p, end = cm.data_page_offset, cm.data_page_offset + cm.total_compressed_size
+    pages = []
+    while p < end:
+        c = Compact(raw, p)
+        h = c.struct()
+        body = raw[c.p:c.p + h[3]]
+        p = c.p + h[3]
+        if h[1] != 3:  # DATA_PAGE_V2 only (no dictionary pages are written)
+            continue
+        v2 = h[8]
+        dl, rl = v2[5], v2[6]
+        pages.append((v2[3], v2[1], body[:rl], body[rl:rl + dl], body[rl + dl:]))
+    return pages
+
+
+def list_column(rng, rows, list_nullable, item_nullable):
+    vals = []
+    for _ in range(rows):
+        r = rng.random()
+        if list_nullable and r < 0.1:
+            vals.append(None)
+        elif r < 0.2:
+            vals.append([])
+        else:
+            vals.append([None if item_nullable and rng.random() < 0.15 else int(x)
+                         for x in rng.integers(-1000, 1000, int(rng.integers(1, 7)))])
+    field = pa.field("c", pa.list_(pa.field("item", pa.int32(), nullable=item_nullable)), nullable=list_nullable)
+    return pa.table({"c": pa.array(vals, type=field.type)}, schema=pa.schema([field]))
+
+
+@pytest.mark.parametrize("list_nullable", [False, True], ids=["list_req", "list_null"])
+@pytest.mark.parametrize("item_nullable", [False, True], ids=["item_req", "item_null"])
+def test_levels_match_pyarrow(tmp_path, list_nullable, item_nullable):
+    rng = np.random.default_rng(7 + 2 * list_nullable + item_nullable)
+    t = list_column(rng, 20000, list_nullable, item_nullable)
+    path = str(tmp_path / "l.parquet")
+    pq.write_table(t, path, data_page_version="2.0", compression="NONE", use_dictionary=False,
+                   data_page_size=8192, write_statistics=False)
+    pages = data_pages_v2(path)
+    assert len(pages) > 3
+    max_def = int(list_nullable) + 1 + int(item_nullable)
+    bw = max_def.bit_length()
+    chunk, metas = b"", []
+    for rows, nlev, rep, dfb, plain in pages:
+        d = O.hybrid_decode(dfb, bw, nlev) if dfb else np.full(nlev, max_def, np.uint32)
+        # every leaf slot (def >= the leaf level) carries a value: the page's
+        # PLAIN values at the non-null slots, 0 at the null ones
+        slot_def = d[d >= int(list_nullable) + 1]
+        page_vals = np.zeros(len(slot_def), np.int32)
+        nn = slot_def == max_def
+        page_vals[nn] = np.frombuffer(plain, np.int32, int(nn.sum()))
+        stream = O.compress(page_vals, None, O.WriteOptions.make())
+        body = rows.to_bytes(4, "little") + len(rep).to_bytes(4, "little") + len(dfb).to_bytes(4, "little")
+        chunk += body + rep + dfb + stream
+        metas.append((len(body) + len(rep) + len(dfb) + len(stream), nlev))
+    offs, lv, vals, fv = O.read_list_column(chunk, metas, np.int32, list_nullable, item_nullable)
+    arr = t.column("c").combine_chunks()
+    assert (offs == arr.offsets.to_numpy()).all()
+    if list_nullable:
+        assert (lv == arr.is_valid().to_numpy(zero_copy_only=False)).all()
+    assert len(vals) == len(arr.values)
+    present = arr.values.is_valid().to_numpy(zero_copy_only=False)
+    assert (vals[present] == arr.values.to_numpy(zero_copy_only=False)[present]).all()
+    if item_nullable:
+        assert (fv == arr.values.is_valid().to_numpy(zero_copy_only=False)).all()
