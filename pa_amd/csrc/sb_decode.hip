@@ -1025,7 +1025,8 @@ __device__ uint32_t snappy_wave(WaveWin& w, uint32_t p, uint32_t pend, WaveOut<R
 //     chunk per batch), literals are copied lane-parallel, then matches whose
 //     source ends before the batch's first match byte are copied
 //     lane-parallel and the rest in sequence order, wave-wide.
-// The compressed stream is staged by LDS-DMA into a per-wave kIb ring.
+// The compressed stream is staged into a per-wave kIb ring (LDS-DMA at a
+// seek, then a KiB at a time from registers loaded a KiB ahead).
 // ---------------------------------------------------------------------------
 // Record chains through a window, wave-parallel.  Variable-length records
 // whose size follows from their own header (Patas records, LZ4 sequences)
@@ -1091,14 +1092,16 @@ __device__ __forceinline__ uint32_t lds_chain(lds_u8* tab, uint32_t t1) {
   return x;
 }
 
-constexpr uint32_t kIb = 4096, kScan = 256, kLitFast = 64, kMatchFast = 32;
+constexpr uint32_t kIb = 2048, kScan = 256, kLitFast = 64, kMatchFast = 32;
 
 struct InRing {
   gmem_u32* g;   // dword-aligned stream base
   uint32_t nd;   // stream dwords
-  lds_u8* ib;    // kIb bytes: stream byte x at ib[x % kIb]
+  lds_u8* ib;    // kIb (2 KiB) bytes: stream byte x at ib[x % kIb]
   lds_u8* ct;    // 7 x 256 bytes: the chain tables T1..T32 and the candidates' accept table
-  uint32_t base; // [base, base + 3 KiB) staged and complete; base % 1 KiB == 0
+  uint32_t base; // [base, base + 2 KiB) staged and complete; base % 1 KiB == 0
+  u32x4 pf;      // [base + 2 KiB, base + 3 KiB), 16 bytes a lane, loaded ahead in registers
+  // (a 2 KiB ring keeps the wave at 7.75 KiB of LDS: five waves per SIMD)
 
   __device__ __forceinline__ void dma(uint32_t b) {  // [b, b + 1 KiB) -> ib
     const uint32_t lane = threadIdx.x & 63;
@@ -1110,22 +1113,30 @@ struct InRing {
                                        0, 0);
     }
   }
+  __device__ __forceinline__ void prefetch(uint32_t b) {  // [b, b + 1 KiB) -> pf
+    const uint32_t i = (b >> 2) + 4 * (threadIdx.x & 63);
+    pf.x = g[min(i, nd - 1)];
+    pf.y = g[min(i + 1, nd - 1)];
+    pf.z = g[min(i + 2, nd - 1)];
+    pf.w = g[min(i + 3, nd - 1)];
+  }
   __device__ void seek(uint32_t x) {
     base = x & ~1023u;
-    for (uint32_t k = 0; k < 4; k++) dma(base + 1024 * k);
+    dma(base);
+    dma(base + 1024);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    prefetch(base + 2048);
   }
   __device__ __forceinline__ void slide(uint32_t p) {
     if (p - base < 1024) return;
-    if (p - base >= 3072) { seek(p); return; }
-    do {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the in-flight KiB is complete
-      dma(base + 4096);                                    // into the slot of base
-      base += 1024;
-    } while (p - base >= 1024);
+    if (p - base >= 2048) { seek(p); return; }
+    // the prefetched KiB into the slot of base, then the next one
+    *(__attribute__((address_space(3))) u32x4*)(ib + (base & (kIb - 1)) + 16 * (threadIdx.x & 63)) = pf;
+    base += 1024;
+    prefetch(base + 2048);
   }
   __device__ __forceinline__ uint32_t ubyte(uint32_t x) const {  // uniform
-    if (x - base < 3072) return ib[x & (kIb - 1)];
+    if (x - base < 2048) return ib[x & (kIb - 1)];
     return ((gmem_u8*)g)[x];
   }
 };
@@ -1334,7 +1345,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
   bool ended = false;
   while (p < pend && !ended) {
     in.slide(p);
-    const uint32_t lim = min(in.base + 3072, pend);
+    const uint32_t lim = min(in.base + 2048, pend);
     // 1. successor distances of the candidate starts x = p + 4 lane + k, from
     //    the token and at most one extension byte per length: the tokens are
     //    one unaligned dword of the ring, the literal extensions the next
@@ -2119,7 +2130,10 @@ static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
 // wave with its own kRing-byte LDS history ring: 4 waves x 4 KiB per
 // workgroup, so 8 waves per SIMD can be resident and the serial token streams
 // of many pages overlap.
-__global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) {
+#ifndef SB_INF_BLOCKS
+#define SB_INF_BLOCKS 5  // 4-wave workgroups: 5 waves per SIMD (7.75 KiB of LDS and <= 96 VGPRs a wave)
+#endif
+__global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(InflateLaunch a) {
   __shared__ u32x4 rings[kInfWaves][kRing / 16];
   __shared__ u32x4 ibufs[kInfWaves][kIb / 16];
   __shared__ u32x4 ctabs[kInfWaves][7 * 256 / 16];
@@ -2159,7 +2173,9 @@ __global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) 
       in.ct = (lds_u8*)&ctabs[wv][0];
       in.seek(p0);
       st = lz4_inflate(in, p0, p0 + jb.csize, o);
-    } else if (jb.codec == 3) {
+    }
+#ifndef SB_V_LZ4ONLY
+    else if (jb.codec == 3) {
       WaveWin w;
       w.init(src, jb.csize);
       st = snappy_wave<true>(w, p0, p0 + jb.csize, o);
@@ -2168,6 +2184,7 @@ __global__ __launch_bounds__(64 * kInfWaves, 8) void k_inflate(InflateLaunch a) 
       st = W == 8 ? patas_wave<8>(src, jb.csize, dst, jb.usize / 8, o.ring)
                   : patas_wave<4>(src, jb.csize, dst, jb.usize / 4, o.ring);
     }
+#endif
     if (st && lane == 0) a.status[jb.page] = st;
   }
 }
