@@ -3154,92 +3154,123 @@ __device__ __forceinline__ uint32_t compress32(uint32_t x, uint32_t m) {
   return x;
 }
 
-// One wave walks its page's levels 2048 at a time.  WRITE = false: consumed
-// counts.  WRITE = true: offsets and bitmaps at (rbase, lbase).
+// One step of kLvStep levels [t0, t0 + kLvStep) of a page, one wave, rows
+// and leaves before it = (carry_r, carry_l).  *step_r / *step_l: the step's
+// row starts and leaves (all levels); the return value: leaves consumed
+// (levels whose inclusive row count stays <= rows, read_basic.rs:158-162).
+// WRITE: offsets and bitmaps at (rbase, lbase).
+template <bool WRITE, class Src>
+__device__ uint32_t lv_step(const Src& s, ListWave& w, const ListShared& ls, const ListArgs& a, uint32_t t0, uint32_t L,
+                            uint64_t rbase, uint64_t lbase, uint32_t carry_r, uint32_t carry_l, uint32_t* step_r,
+                            uint32_t* step_l) {
+  const uint32_t lane = threadIdx.x & 63, rows = ls.rows, cs1 = a.nl + 1;
+  const LvMasks m = level_masks(s, ls, t0 + lane * kLvK, L, cs1);
+  if (t0 == 0 && lane == 0 && !(m.rsm & 1)) put_err(&w.err, ST_OUT_OF_SPEC);  // level 0 starts no row
+  const uint32_t pk = ((uint32_t)__popc(m.rsm) << 16) | (uint32_t)__popc(m.lfm);
+  const uint32_t incl = wave_incl_scan(pk), tot = __builtin_amdgcn_readlane(incl, 63), ex = incl - pk;
+  const uint32_t rb = carry_r + (ex >> 16), lb = carry_l + (ex & 0xFFFFu);
+  uint32_t cm = m.vm;
+  if (rb + __popc(m.rsm) > rows) {
+    if (rb >= rows + 1) cm = 0;
+    else {  // cut at the (rows - rb + 1)-th row start
+      uint32_t x = m.rsm;
+      for (uint32_t k = rows - rb; k; k--) x &= x - 1;
+      cm = (x & (0u - x)) - 1;
+    }
+  }
+  const uint32_t rsm = m.rsm & cm, lfm = m.lfm & cm;
+  if constexpr (WRITE) {
+    const uint32_t s_r0 = carry_r, s_l0 = carry_l;
+    const uint64_t g0 = rbase + s_r0, v0 = lbase + s_l0;
+    const uint32_t al = a.ow == 4 ? (uint32_t)(g0 & 3) : (uint32_t)(g0 & 1);  // obuf index of row 0
+    for (uint32_t i = lane; i < kLvStep / 32 + 4; i += 64) w.lbits[i] = w.fbits[i] = 0;
+    wave_sync();
+    const uint32_t nr = __popc(rsm), nf = __popc(lfm);
+    uint16_t* ob = w.obuf + al + (rb - s_r0);
+    const uint32_t lrel = lb - s_l0;
+    uint32_t j = 0;
+#ifndef SB_V_LV_NOOB
+    for (uint32_t x = rsm; x; x &= x - 1, j++) ob[j] = (uint16_t)(lrel + __popc(m.lfm & ((x & (0u - x)) - 1)));
+#endif
+    if (a.nl) lds_or_bits(w.lbits + 1, rb - s_r0, compress32(m.lvm, rsm), nr);
+    if (a.ni) lds_or_bits(w.fbits + 1, lrel, compress32(m.fvm, lfm), nf);
+    const uint32_t cpk = (nr << 16) | nf;
+    const uint32_t ctot = __builtin_amdgcn_readlane(wave_incl_scan(cpk), 63);
+    const uint32_t tr = ctot >> 16, tl = ctot & 0xFFFFu;
+    wave_sync();
+#ifdef SB_V_LV_NOOFF
+    constexpr bool wr_off = false;
+#else
+    constexpr bool wr_off = true;
+#endif
+    if (!wr_off) {
+    } else if (a.ow == 4) {  // quads of rows on 16-byte boundaries: obuf[4q .. 4q + 3] -> o[4q - al ..]
+      uint32_t* o = (uint32_t*)a.out_offsets + (g0 - al);
+      const uint32_t v32 = (uint32_t)v0, nq = (al + tr + 3) >> 2;
+      for (uint32_t q = lane; q < nq; q += 64) {
+        const uint32_t* pr = (const uint32_t*)(w.obuf + 4 * q);
+        const uint32_t px = pr[0], py = pr[1];
+        const uint32_t e0 = v32 + (px & 0xFFFFu), e1 = v32 + (px >> 16), e2 = v32 + (py & 0xFFFFu), e3 = v32 + (py >> 16);
+        const uint32_t j0 = 4 * q;
+        if (j0 >= al && j0 + 4 <= al + tr) {
+          st_out((u32x4*)(o + j0), u32x4{e0, e1, e2, e3});
+        } else {
+          const uint32_t e[4] = {e0, e1, e2, e3};
+#pragma unroll
+          for (uint32_t k = 0; k < 4; k++)
+            if (j0 + k >= al && j0 + k < al + tr) o[j0 + k] = e[k];
+        }
+      }
+    } else {
+      uint64_t* o = (uint64_t*)a.out_offsets + (g0 - al);
+      const uint32_t nq = (al + tr + 1) >> 1;
+      for (uint32_t q = lane; q < nq; q += 64) {
+        const uint32_t j0 = 2 * q;
+        const uint64_t x0 = v0 + w.obuf[j0], x1 = v0 + w.obuf[j0 + 1];
+        if (j0 >= al && j0 + 2 <= al + tr) {
+          st_out((u32x4*)(o + j0), u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)});
+        } else {
+          if (j0 >= al && j0 < al + tr) o[j0] = x0;
+          if (j0 + 1 >= al && j0 + 1 < al + tr) o[j0 + 1] = x1;
+        }
+      }
+    }
+#ifndef SB_V_LV_NOBITS
+    if (a.nl) wave_put_bits(w.lbits + 1, tr, g0, a.out_list_validity);
+    if (a.ni) wave_put_bits(w.fbits + 1, tl, v0, a.out_leaf_validity);
+#endif
+    wave_sync();
+  }
+  *step_r = tot >> 16;
+  *step_l = tot & 0xFFFFu;
+  return (uint32_t)wave_sum64(__popc(lfm));
+}
+
+// One wave walks its page's levels a step at a time (the sizing pass).
 template <bool WRITE, class Src>
 __device__ void wave_levels(const Src& s, ListWave& w, const ListArgs& a, uint32_t L, uint64_t rbase, uint64_t lbase,
                             uint32_t* rows_c, uint32_t* leaves_c) {
-  const uint32_t lane = threadIdx.x & 63, rows = w.ls.rows, cs1 = a.nl + 1;
-  uint32_t carry_r = 0, carry_l = 0, my_leaves = 0;
+  const uint32_t lane = threadIdx.x & 63, rows = w.ls.rows;
+  uint32_t carry_r = 0, carry_l = 0, leaves = 0;
   for (uint32_t t0 = 0; t0 < L; t0 += kLvStep) {
-    const LvMasks m = level_masks(s, w.ls, t0 + lane * kLvK, L, cs1);
-    if (t0 == 0 && lane == 0 && !(m.rsm & 1)) put_err(&w.err, ST_OUT_OF_SPEC);  // level 0 starts no row
-    const uint32_t pk = ((uint32_t)__popc(m.rsm) << 16) | (uint32_t)__popc(m.lfm);
-    const uint32_t incl = wave_incl_scan(pk), tot = __builtin_amdgcn_readlane(incl, 63), ex = incl - pk;
-    const uint32_t rb = carry_r + (ex >> 16), lb = carry_l + (ex & 0xFFFFu);
-    // consumed: levels whose inclusive row count stays <= rows (read_basic.rs:158-162)
-    uint32_t cm = m.vm;
-    if (rb + __popc(m.rsm) > rows) {
-      if (rb >= rows + 1) cm = 0;
-      else {  // cut at the (rows - rb + 1)-th row start
-        uint32_t x = m.rsm;
-        for (uint32_t k = rows - rb; k; k--) x &= x - 1;
-        cm = (x & (0u - x)) - 1;
-      }
-    }
-    const uint32_t rsm = m.rsm & cm, lfm = m.lfm & cm;
-    my_leaves += __popc(lfm);
-    if constexpr (WRITE) {
-      const uint32_t s_r0 = carry_r, s_l0 = carry_l;
-      const uint64_t g0 = rbase + s_r0, v0 = lbase + s_l0;
-      const uint32_t al = a.ow == 4 ? (uint32_t)(g0 & 3) : (uint32_t)(g0 & 1);  // obuf index of row 0
-      for (uint32_t i = lane; i < kLvStep / 32 + 4; i += 64) w.lbits[i] = w.fbits[i] = 0;
-      wave_sync();
-      const uint32_t nr = __popc(rsm), nf = __popc(lfm);
-      uint16_t* ob = w.obuf + al + (rb - s_r0);
-      const uint32_t lrel = lb - s_l0;
-      uint32_t j = 0;
-      for (uint32_t x = rsm; x; x &= x - 1, j++) ob[j] = (uint16_t)(lrel + __popc(m.lfm & ((x & (0u - x)) - 1)));
-      if (a.nl) lds_or_bits(w.lbits + 1, rb - s_r0, compress32(m.lvm, rsm), nr);
-      if (a.ni) lds_or_bits(w.fbits + 1, lrel, compress32(m.fvm, lfm), nf);
-      const uint32_t cpk = (nr << 16) | nf;
-      const uint32_t ctot = __builtin_amdgcn_readlane(wave_incl_scan(cpk), 63);
-      const uint32_t tr = ctot >> 16, tl = ctot & 0xFFFFu;
-      wave_sync();
-      if (a.ow == 4) {  // quads of rows on 16-byte boundaries: obuf[4q .. 4q + 3] -> o[4q - al ..]
-        uint32_t* o = (uint32_t*)a.out_offsets + (g0 - al);
-        const uint32_t v32 = (uint32_t)v0, nq = (al + tr + 3) >> 2;
-        for (uint32_t q = lane; q < nq; q += 64) {
-          const uint32_t* pr = (const uint32_t*)(w.obuf + 4 * q);
-          const uint32_t px = pr[0], py = pr[1];
-          const uint32_t e0 = v32 + (px & 0xFFFFu), e1 = v32 + (px >> 16), e2 = v32 + (py & 0xFFFFu), e3 = v32 + (py >> 16);
-          const uint32_t j0 = 4 * q;
-          if (j0 >= al && j0 + 4 <= al + tr) {
-            st_out((u32x4*)(o + j0), u32x4{e0, e1, e2, e3});
-          } else {
-            const uint32_t e[4] = {e0, e1, e2, e3};
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++)
-              if (j0 + k >= al && j0 + k < al + tr) o[j0 + k] = e[k];
-          }
-        }
-      } else {
-        uint64_t* o = (uint64_t*)a.out_offsets + (g0 - al);
-        const uint32_t nq = (al + tr + 1) >> 1;
-        for (uint32_t q = lane; q < nq; q += 64) {
-          const uint32_t j0 = 2 * q;
-          const uint64_t x0 = v0 + w.obuf[j0], x1 = v0 + w.obuf[j0 + 1];
-          if (j0 >= al && j0 + 2 <= al + tr) {
-            st_out((u32x4*)(o + j0), u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)});
-          } else {
-            if (j0 >= al && j0 < al + tr) o[j0] = x0;
-            if (j0 + 1 >= al && j0 + 1 < al + tr) o[j0 + 1] = x1;
-          }
-        }
-      }
-      if (a.nl) wave_put_bits(w.lbits + 1, tr, g0, a.out_list_validity);
-      if (a.ni) wave_put_bits(w.fbits + 1, tl, v0, a.out_leaf_validity);
-      wave_sync();
-    }
-    carry_r += tot >> 16;
-    carry_l += tot & 0xFFFFu;
+    uint32_t sr, sl;
+    leaves += lv_step<WRITE>(s, w, w.ls, a, t0, L, rbase, lbase, carry_r, carry_l, &sr, &sl);
+    carry_r += sr;
+    carry_l += sl;
     if (carry_r > rows) break;  // uniform: every later level is past the last row
   }
-  const uint32_t lsum = (uint32_t)wave_sum64(my_leaves);
   const uint32_t rc = min(carry_r, rows);
   if (lane == 0 && rc != rows) put_err(&w.err, ST_OUT_OF_SPEC);  // levels ended before `rows` rows
   *rows_c = rc;
-  *leaves_c = lsum;
+  *leaves_c = leaves;
+}
+
+// Row starts and leaves of the step at t0 (all its levels), one wave.
+template <class Src>
+__device__ __forceinline__ uint32_t lv_count(const Src& s, const ListShared& ls, uint32_t t0, uint32_t L, uint32_t cs1) {
+  const LvMasks m = level_masks(s, ls, t0 + (threadIdx.x & 63) * kLvK, L, cs1);
+  const uint32_t pk = ((uint32_t)__popc(m.rsm) << 16) | (uint32_t)__popc(m.lfm);
+  return (uint32_t)wave_sum64(pk);  // rows < 2^16 per 2048-level step
 }
 
 // Per page setup of one wave: the page's first kLvStage bytes staged in LDS
@@ -3351,61 +3382,6 @@ __global__ __launch_bounds__(NT) void k_list_bscan(ListArgs a) {
   if (threadIdx.x == 0) {
     a.blk[2 * blockIdx.x] = tr;
     a.blk[2 * blockIdx.x + 1] = tl;
-  }
-}
-
-// Levels pass: one wave per page.  Bases = the page's in-block bases + the
-// totals of the blocks before it (summed by the wave, 64 blocks per probe).
-// Writes offsets and both bitmaps, the page's values-stream descriptor, its
-// status; the last page also the totals and the final offset.
-__global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
-  __shared__ ListWave waves[NW];
-  __shared__ uint32_t stages[NW][kLvStage / 4 + 16];  // the page's first bytes at byte `mis` (+ pad)
-  const uint32_t lane = threadIdx.x & 63;
-  ListWave& w = waves[threadIdx.x >> 6];
-  uint32_t* stage = stages[threadIdx.x >> 6];
-  for (uint32_t page = blockIdx.x * NW + (threadIdx.x >> 6); page < a.n_pages; page += gridDim.x * NW) {
-    const PageDesc pd = a.pages[page];
-    const uint32_t nb = page / NT;
-    uint64_t br = 0, bl = 0;
-    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
-      const uint32_t b = b0 + lane;
-      br += wave_sum64(b < nb ? a.blk[2 * b] : 0);
-      bl += wave_sum64(b < nb ? a.blk[2 * b + 1] : 0);
-    }
-    const uint64_t rbase = br + a.local[2 * page], lbase = bl + a.local[2 * page + 1];
-    const uint64_t cnt = a.counts[page];
-    bool staged = false;
-    uint32_t mis = 0, lim = 0, rows_c = 0, leaves_c = 0;
-    const bool sized = a.lvdesc[2 * page + 1].y != 0;  // the exact pass parsed this page
-    if (sized && wave_page_setup(w, stage, a, page, pd, true, &staged, &mis, &lim)) {
-      if (staged) wave_levels<true>(LdsSrc{stage, mis}, w, a, pd.num_values, rbase, lbase, &rows_c, &leaves_c);
-      else wave_levels<true>(GlbSrc{a.chunk + pd.byte_off}, w, a, pd.num_values, rbase, lbase, &rows_c, &leaves_c);
-    } else if (lane == 0) {
-      w.err = 0;
-      if (!sized) {  // re-parse for the status the reference would give
-        const StageSrc ss{LdsSrc{nullptr, 0}, GlbSrc{a.chunk + pd.byte_off}, 0};
-        list_parse(ss, &w.err, w.ls, pd, a);
-        if (!w.err) w.err = ST_OUT_OF_SPEC;
-      }
-    }
-    wave_sync();
-    if (lane == 0) {
-      uint32_t err = w.err;
-      if (!err && (rows_c != (uint32_t)(cnt >> 32) || leaves_c != (uint32_t)cnt)) err = ST_OUT_OF_SPEC;
-      const bool ok = err == 0;
-      // the page's values stream, decoded as a flat non-nullable page of `leaves` values
-      a.vpages[page] = PageDesc{pd.byte_off + (ok ? w.ls.vpos : 0), lbase, ok ? pd.byte_len - w.ls.vpos : 0,
-                                ok ? leaves_c : 0, 0};
-      a.status[page] = err;
-      if (page == a.n_pages - 1) {
-        const uint64_t tr = rbase + (cnt >> 32), tl = lbase + (uint32_t)cnt;
-        a.totals[0] = tr;
-        a.totals[1] = tl;
-        if (a.out_offsets) bin_put_off(a.out_offsets, tr, tl, a.ow);  // create_list appends values.len()
-      }
-    }
-    wave_sync();
   }
 }
 
