@@ -3385,6 +3385,61 @@ __global__ __launch_bounds__(NT) void k_list_bscan(ListArgs a) {
   }
 }
 
+// Levels pass: one wave per page.  Bases = the page's in-block bases + the
+// totals of the blocks before it (summed by the wave, 64 blocks per probe).
+// Writes offsets and both bitmaps, the page's values-stream descriptor, its
+// status; the last page also the totals and the final offset.
+__global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
+  __shared__ ListWave waves[NW];
+  __shared__ uint32_t stages[NW][kLvStage / 4 + 16];  // the page's first bytes at byte `mis` (+ pad)
+  const uint32_t lane = threadIdx.x & 63;
+  ListWave& w = waves[threadIdx.x >> 6];
+  uint32_t* stage = stages[threadIdx.x >> 6];
+  for (uint32_t page = blockIdx.x * NW + (threadIdx.x >> 6); page < a.n_pages; page += gridDim.x * NW) {
+    const PageDesc pd = a.pages[page];
+    const uint32_t nb = page / NT;
+    uint64_t br = 0, bl = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+      const uint32_t b = b0 + lane;
+      br += wave_sum64(b < nb ? a.blk[2 * b] : 0);
+      bl += wave_sum64(b < nb ? a.blk[2 * b + 1] : 0);
+    }
+    const uint64_t rbase = br + a.local[2 * page], lbase = bl + a.local[2 * page + 1];
+    const uint64_t cnt = a.counts[page];
+    bool staged = false;
+    uint32_t mis = 0, lim = 0, rows_c = 0, leaves_c = 0;
+    const bool sized = a.lvdesc[2 * page + 1].y != 0;  // the exact pass parsed this page
+    if (sized && wave_page_setup(w, stage, a, page, pd, true, &staged, &mis, &lim)) {
+      if (staged) wave_levels<true>(LdsSrc{stage, mis}, w, a, pd.num_values, rbase, lbase, &rows_c, &leaves_c);
+      else wave_levels<true>(GlbSrc{a.chunk + pd.byte_off}, w, a, pd.num_values, rbase, lbase, &rows_c, &leaves_c);
+    } else if (lane == 0) {
+      w.err = 0;
+      if (!sized) {  // re-parse for the status the reference would give
+        const StageSrc ss{LdsSrc{nullptr, 0}, GlbSrc{a.chunk + pd.byte_off}, 0};
+        list_parse(ss, &w.err, w.ls, pd, a);
+        if (!w.err) w.err = ST_OUT_OF_SPEC;
+      }
+    }
+    wave_sync();
+    if (lane == 0) {
+      uint32_t err = w.err;
+      if (!err && (rows_c != (uint32_t)(cnt >> 32) || leaves_c != (uint32_t)cnt)) err = ST_OUT_OF_SPEC;
+      const bool ok = err == 0;
+      // the page's values stream, decoded as a flat non-nullable page of `leaves` values
+      a.vpages[page] = PageDesc{pd.byte_off + (ok ? w.ls.vpos : 0), lbase, ok ? pd.byte_len - w.ls.vpos : 0,
+                                ok ? leaves_c : 0, 0};
+      a.status[page] = err;
+      if (page == a.n_pages - 1) {
+        const uint64_t tr = rbase + (cnt >> 32), tl = lbase + (uint32_t)cnt;
+        a.totals[0] = tr;
+        a.totals[1] = tl;
+        if (a.out_offsets) bin_put_off(a.out_offsets, tr, tl, a.ow);  // create_list appends values.len()
+      }
+    }
+    wave_sync();
+  }
+}
+
 }  // namespace sbk
 
 namespace sb {
