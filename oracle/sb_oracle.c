@@ -1172,6 +1172,7 @@ static double codec_ratio(int codec, const arr_t* a, const stats_t* s, orc_rng* 
 static int choose(const arr_t* a, const stats_t* s, const orc_write_options* opt, orc_rng* rng) {
   uint32_t fm = opt->forbidden_mask;
   if (opt->forced_codec >= 0 && !(fm & (1u << opt->forced_codec))) {
+    /* DEVIATION 6: forced Bitpacking only for an eligible page */
     int f = opt->forced_codec;
     int ok = a->is_float ? (f == ORC_FREQ || f == ORC_DICT || f == ORC_RLE || f == ORC_PATAS)
                          : (f == ORC_FREQ || f == ORC_DICT || f == ORC_RLE ||

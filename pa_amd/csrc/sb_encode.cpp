@@ -527,6 +527,11 @@ static int choose(const Arr<T>& a, const Stats<T>& s, const Opts& opt, Rng& rng)
   const uint32_t fm = opt.forbidden;
   if (opt.forced >= 0 && !(fm & (1u << opt.forced))) {
     const int f = opt.forced;
+    // DEVIATION: the reference's forced Bitpacking
+    // (check_bitpack_env, integer/mod.rs:259-265) is unconditional; BitPacker4x
+    // needs whole 128-value blocks of non-negative values (bp.rs:46-61 packs a
+    // short last chunk the decoder cannot read back), so an ineligible page
+    // keeps the default codec here.
     const bool ok = Tr<T>::kFloat ? (f == kFreq || f == kDict || f == kRle || f == kPatas)
                                   : (f == kFreq || f == kDict || f == kRle || (f == kBitpacking && bp_eligible(a, s)));
     if (ok) return f;
