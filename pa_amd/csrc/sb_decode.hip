@@ -2429,12 +2429,13 @@ struct LightPage {
   uint32_t codec, ob, ocs, vb, vcs, S, vbpos;
 };
 
+template <int OW>
 __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int nullable, LightPage& lp) {
   uint32_t p;
   if (!light_validity(s, len, n, nullable, &p, &lp.vbpos)) return false;
   if (p + 9 > len) return false;
   lp.codec = s.u8(p);
-  if (lp.codec != 1 && lp.codec != 3) return false;
+  if (lp.codec != 0 && lp.codec != 1 && lp.codec != 3) return false;
   const uint32_t cs = s.u32(p + 1), body = p + 9;
   if (cs > len - body) return false;
   const uint32_t vh = body + cs;
@@ -2445,6 +2446,8 @@ __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int n
   if (lp.vcs > len - lp.vb) return false;
   lp.ob = body;
   lp.ocs = cs;
+  // None: both streams are copied as they lie (copy_from_slice lengths, binary/mod.rs:119-160)
+  if (lp.codec == 0 && (cs != (n + 1) * (uint32_t)OW || lp.vcs != lp.S)) return false;
   return true;
 }
 
@@ -2457,24 +2460,45 @@ __global__ __launch_bounds__(NT) void k_bin_light(BinArgs a) {
   for (uint32_t page = blockIdx.x * NT + threadIdx.x; page < np; page += gridDim.x * NT) {
     const PageDesc pd = a.pages[page];
     LightPage lp;
-    const bool lt = bin_light_parse(GlbSrc{a.chunk + pd.byte_off}, pd.byte_len, pd.num_values, a.nullable, lp);
+    const bool lt = bin_light_parse<OW>(GlbSrc{a.chunk + pd.byte_off}, pd.byte_len, pd.num_values, a.nullable, lp);
     // one atomic per wave and counter (12k contended atomics on one address cost ~100 us)
-    const uint32_t slot = wave_slot(a.job_count, lt, 2), li = wave_slot(&cnt[1], lt, 1), si = wave_slot(&cnt[0], !lt, 1);
-    if (lt) {
+    const bool jobs = lt && lp.codec != 0;  // None pages: copied by k_bin_light_out
+    const uint32_t slot = wave_slot(a.job_count, jobs, 2), li = wave_slot(&cnt[1], lt, 1),
+                   si = wave_slot(&cnt[0], !lt, 1);
+    if (jobs) {
       // Utf8 (32-bit) offsets are expanded straight into the column, rebased
       // (k_inflate xf); LargeUtf8 offsets go through scratch
       a.jobs[slot] = InflateJob{pd.byte_off + lp.ob,
                                 OW == 4 ? kDstBinOffs | (pd.row_off * 4) : kDstScratch | ((pd.row_off + page) * OW),
                                 lp.ocs, (pd.num_values + 1) * (uint32_t)OW, lp.codec, page};
       a.jobs[slot + 1] = InflateJob{pd.byte_off + lp.vb, kDstBinBase | page, lp.vcs, lp.S, lp.codec, page};
+    }
+    if (lt) {
       a.sizes[page] = lp.S;
       a.status[page] = 0;
-      vbpos[page] = lp.vbpos;
+      vbpos[page] = lp.vbpos | (lp.codec == 0 ? 0x80000000u : 0u);  // bit 31: a None page
       light[li] = page;
     } else {
       staged[si] = page;
     }
   }
+}
+
+// len bytes from chunk + src to dst, one workgroup: dword loads realigned by
+// v_alignbyte, dword stores after the head bytes that align dst.
+__device__ void copy_glb(uint64_t src, const uint8_t* chunk, uint8_t* dst, uint64_t len) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t head = (uint32_t)min<uint64_t>(len, (4 - ((uintptr_t)dst & 3)) & 3);
+  if (tid < head) dst[tid] = chunk[src + tid];
+  const uint64_t body = (len - head) >> 2;
+  const uint8_t* s0 = chunk + src + head;
+  const uint32_t sh = (uint32_t)((uintptr_t)s0 & 3);
+  const uint32_t* s32 = (const uint32_t*)((uintptr_t)s0 - sh);
+  uint32_t* d32 = (uint32_t*)(dst + head);
+  for (uint64_t w = tid; w < body; w += NT)
+    d32[w] = sh ? __builtin_amdgcn_alignbyte(s32[w + 1], s32[w], sh) : s32[w];
+  const uint64_t done = head + body * 4;
+  if (tid < len - done) dst[done + tid] = chunk[src + done + tid];
 }
 
 // Header-only pages after k_inflate: offsets rebased from scratch onto the
@@ -2490,6 +2514,27 @@ __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
     const uint32_t n = pd.num_values;
     const uint64_t R = pd.row_off, V = a.bases[page], S = a.sizes[page];
     if (a.status[page]) continue;  // an inflate error stands
+    const uint32_t tag = a.cls[2 * np + page], vb = tag & 0x7FFFFFFFu;
+    const GlbSrc pg{a.chunk + pd.byte_off};
+    if (tag & 0x80000000u) {  // a None page: offsets rebased and values copied from the page in HBM
+      __shared__ LightPage nl_lp;
+      if (tid == 0) {
+        bin_light_parse<OW>(pg, pd.byte_len, n, a.nullable, nl_lp);
+        bad = (ldo<OW>(pg, nl_lp.ob + n * OW) != S || V + S > a.values_cap) ? ST_OUT_OF_SPEC : 0u;  // DEVIATION 7
+      }
+      __syncthreads();
+      const uint32_t e = bad, ob = nl_lp.ob, vpos = nl_lp.vb;
+      __syncthreads();
+      if (e) {
+        if (tid == 0) a.status[page] = e;
+        continue;
+      }
+      if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, ldo<OW>(pg, ob), OW);  // the first page keeps p[0]
+      for (uint32_t k = tid + 1; k <= n; k += NT) bin_put_off(a.out_offsets, R + k, V + ldo<OW>(pg, ob + k * OW), OW);
+      copy_glb(pd.byte_off + vpos, a.chunk, a.out_values + V, S);
+      if (vb) write_validity(pg, vb, n, R, a.out_validity);
+      continue;
+    }
     const uint8_t* xo = a.scratch + (R + page) * OW;
     auto po = [&](uint32_t k) -> uint64_t {
       if constexpr (OW == 8) return ((const uint64_t*)xo)[k];
@@ -2515,8 +2560,7 @@ __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
       if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, po(0), OW);  // the first page keeps its p[0]
       for (uint32_t k = tid + 1; k <= n; k += NT) bin_put_off(a.out_offsets, R + k, V + po(k), OW);
     }
-    const uint32_t vb = a.cls[2 * np + page];
-    if (vb) write_validity(GlbSrc{a.chunk + pd.byte_off}, vb, n, R, a.out_validity);
+    if (vb) write_validity(pg, vb, n, R, a.out_validity);
   }
 }
 

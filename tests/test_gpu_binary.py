@@ -88,15 +88,25 @@ def test_binary_columns(ctx, kind, opt, nullable, phys):
     assert check(ctx, s, validity, nullable, page_rows, O.WriteOptions.make(**OPTS[opt]), phys)
 
 
-def test_binary_page_over_lds_budget_reports_nyi(ctx):
-    """A page whose bytes + expansion exceed one workgroup's LDS (150 KiB)
+def test_binary_page_over_lds_budget(ctx):
+    """A Basic None page larger than one workgroup's LDS (≈300 KiB here) is a
+    header-only page: offsets and values are copied from HBM (k_bin_light_out)."""
+    rng = np.random.default_rng(2)
+    s = strings("long", 2048, rng)
+    check(ctx, s, None, False, 2048, O.WriteOptions.make(), 13)
+    v = rng.random(2048) > 0.3
+    check(ctx, s, v, True, 2048, O.WriteOptions.make(), 13)
+
+
+def test_binary_dict_page_over_lds_budget_reports_nyi(ctx):
+    """A staged (Dict) page whose bytes + expansion exceed one workgroup's LDS
     reports NotYetImplemented, never a wrong answer."""
     import pa_amd
 
     rng = np.random.default_rng(2)
-    s = strings("long", 2048, rng)
+    s = [bytes(rng.integers(0, 256, 200, dtype=np.uint8)) for _ in range(800)] * 4  # a 160 KiB dictionary
     with pytest.raises(pa_amd.StrawboatError) as e:
-        check(ctx, s, None, False, 2048, O.WriteOptions.make(), 13)
+        check(ctx, s, None, False, len(s), O.WriteOptions.make(ratio=2.0, forced=O.DICT), 13)
     assert e.value.status == 2
 
 
