@@ -438,6 +438,54 @@ def read_list_column(chunk, metas, dtype, list_nullable, item_nullable):
             np.concatenate(leafv_all) if item_nullable else None)
 
 
+def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable):
+    """batch read of a leaf under len(list_nullable) list levels (outermost
+    first): per page orc_read_nested_page, then the pages concatenated with
+    each level's offsets moved onto its child's running length ->
+    ([offsets per level], [validity per level | None], values, leaf validity | None)."""
+    L = lib()
+    if not getattr(L, "_nested_ready", False):
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.orc_read_nested_page.argtypes = [P, S, S, I, P, I, I, I, P, P, P, P, P, ctypes.POINTER(S)]
+        L._nested_ready = True
+    dtype = np.dtype(dtype)
+    D = len(list_nullable)
+    src = np.frombuffer(chunk, np.uint8)
+    kind = 1 if dtype.kind == "f" else 0
+    offs = [[] for _ in range(D)]
+    bits = [[] for _ in range(D)]
+    vals, leafv = [], []
+    base = [0] * (D + 1)
+    pos = 0
+    ln = (ctypes.c_int * D)(*[int(x) for x in list_nullable])
+    for length, nlev in metas:
+        page = np.ascontiguousarray(src[pos:pos + length])
+        o = [np.zeros(nlev + 1, np.int64) for _ in range(D)]
+        b = [np.zeros(nlev // 8 + 2, np.uint8) for _ in range(D)]
+        v = np.zeros(nlev + 1, dtype)
+        fb = np.zeros(nlev // 8 + 2, np.uint8)
+        op = (ctypes.c_void_p * D)(*[x.ctypes.data for x in o])
+        bp = (ctypes.c_void_p * D)(*[x.ctypes.data for x in b])
+        cnt = (ctypes.c_size_t * (D + 1))()
+        rows = ctypes.c_size_t()
+        rc = L.orc_read_nested_page(_ptr(page), length, nlev, D, ln, int(item_nullable), kind, dtype.itemsize, op, bp,
+                                    _ptr(v), _ptr(fb), cnt, ctypes.byref(rows))
+        _check(rc, "read_nested_page")
+        for d in range(D):
+            offs[d].append(o[d][:cnt[d]] + base[d + 1])
+            if list_nullable[d]:
+                bits[d].append(np.unpackbits(b[d], bitorder="little")[:cnt[d]].astype(bool))
+        vals.append(v[:cnt[D]])
+        if item_nullable:
+            leafv.append(np.unpackbits(fb, bitorder="little")[:cnt[D]].astype(bool))
+        for d in range(D + 1):
+            base[d] += cnt[d]
+        pos += length
+    out_offs = [np.concatenate(offs[d] + [np.array([base[d + 1]], np.int64)]) for d in range(D)]
+    out_bits = [np.concatenate(bits[d]) if list_nullable[d] else None for d in range(D)]
+    return out_offs, out_bits, np.concatenate(vals), (np.concatenate(leafv) if item_nullable else None)
+
+
 # ---- boolean pages (compression/boolean/*.rs, read/array/boolean.rs) ---------
 def _pack(b) -> np.ndarray:
     return np.packbits(np.asarray(b, bool), bitorder="little")

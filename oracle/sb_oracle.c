@@ -1834,6 +1834,81 @@ int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int l
   return rc;
 }
 
+/* Nested page with `depth` list levels over a primitive leaf (List<List<T>>
+ * ...): read_validity_nested (read/read_basic.rs:65-173) in its general form --
+ * nests[0..depth) are lists (NestedOptional / NestedValid: repeated, nullable
+ * per level), nests[depth] the primitive (NestedPrimitive); cum_sum /
+ * cum_rep over (nullable + repeated) / repeated; a nest is pushed when
+ * `rep <= cum_rep[d] && def >= cum_sum[d]` or the level above was a required
+ * nest that was not valid (is_required: false for lists and primitives, the
+ * arrow2 0.17 nested_utils rule, not vendored -- parity unpinned for struct
+ * nests, which are not supported here).  A list push appends the child's
+ * current length as its offset and `nullable && def > cum_sum[d]` as its
+ * validity; the primitive push counts a leaf slot, valid when
+ * `def != cum_sum[depth]` (:138-146).  Decoding stops after the level whose
+ * successor would start row `additional + 1` (:150-162).  Outputs are
+ * page-local: out_offsets[d] holds counts[d] entries (create_list appends the
+ * child's length, counts[d + 1], read/array/list.rs:48), out_bits[d] the
+ * list validity when list_nullable[d]; counts[depth] = leaf slots. */
+int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int depth, const int* list_nullable,
+                         int item_nullable, int kind, int width, int64_t** out_offsets, uint8_t** out_bits,
+                         uint8_t* out_values, uint8_t* out_leaf_bits, size_t* counts, size_t* out_rows) {
+  if (depth < 1 || depth > 4) return ORC_E_NYI;
+  if (len < 12) return ORC_E_IO;
+  uint32_t additional = rd_u32(page), rep_len = rd_u32(page + 4), def_len = rd_u32(page + 8);
+  size_t pos = 12;
+  if (pos + rep_len > len || pos + rep_len + def_len > len) return ORC_E_IO;
+  const int max_depth = depth + 1;
+  int nullable[5], repeated[5], required[5];
+  for (int d = 0; d < depth; d++) { nullable[d] = list_nullable[d] != 0; repeated[d] = 1; required[d] = 0; }
+  nullable[depth] = item_nullable != 0; repeated[depth] = 0; required[depth] = 0;
+  uint32_t cum_sum[6] = {0}, cum_rep[6] = {0};
+  for (int d = 0; d < max_depth; d++) {
+    cum_sum[d + 1] = cum_sum[d] + (uint32_t)(nullable[d] + repeated[d]);
+    cum_rep[d + 1] = cum_rep[d] + (uint32_t)repeated[d];
+  }
+  uint32_t* rep = (uint32_t*)malloc((num_levels + 1) * 4);
+  uint32_t* def = (uint32_t*)malloc((num_levels + 1) * 4);
+  int rc = orc_hybrid_decode(page + pos, rep_len, bit_width_of(cum_rep[max_depth]), num_levels, rep);
+  if (!rc) rc = orc_hybrid_decode(page + pos + rep_len, def_len, bit_width_of(cum_sum[max_depth]), num_levels, def);
+  if (rc) { free(rep); free(def); return rc; }
+  pos += rep_len + def_len;
+  if (num_levels > 0 && rep[0] != 0) { free(rep); free(def); return ORC_E_OUT_OF_SPEC; }
+  size_t n[5] = {0}, rows = 0;
+  for (size_t l = 0; l < num_levels; l++) {
+    const uint32_t r = rep[l], dv = def[l];
+    if (r == 0) rows++;
+    int is_required = 0;
+    for (int d = 0; d < max_depth; d++) {
+      const int right = r <= cum_rep[d] && dv >= cum_sum[d];
+      if (!(is_required || right)) continue;
+      const int is_valid = nullable[d] && dv > cum_sum[d];
+      if (d < depth) {
+        out_offsets[d][n[d]] = (int64_t)n[d + 1];
+        if (nullable[d]) {
+          if (is_valid) out_bits[d][n[d] >> 3] |= (uint8_t)(1u << (n[d] & 7));
+          else out_bits[d][n[d] >> 3] &= (uint8_t)~(1u << (n[d] & 7));
+        }
+      } else if (nullable[d]) {
+        if (right && dv != cum_sum[d]) out_leaf_bits[n[d] >> 3] |= (uint8_t)(1u << (n[d] & 7));
+        else out_leaf_bits[n[d] >> 3] &= (uint8_t)~(1u << (n[d] & 7));
+      }
+      n[d]++;
+      is_required = required[d] && !is_valid;
+    }
+    uint32_t next_rep = l + 1 < num_levels ? rep[l + 1] : 0;
+    if (next_rep == 0 && rows == additional) break;
+  }
+  free(rep);
+  free(def);
+  if (rows != additional) return ORC_E_OUT_OF_SPEC;
+  rc = kind ? orc_decompress_double(page, len, &pos, width, n[depth], out_values)
+            : orc_decompress_integer(page, len, &pos, width, n[depth], out_values);
+  for (int d = 0; d <= depth; d++) counts[d] = n[d];
+  *out_rows = rows;
+  return rc;
+}
+
 /* ======================================================================= */
 /* boolean pages (compression/boolean/{mod,rle,one_value}.rs,               */
 /* read/array/boolean.rs:59-79, 191-219, write/boolean.rs:24-33)            */

@@ -131,6 +131,9 @@ int orc_write_binary_page(const uint8_t* values, const int64_t* offsets, const u
 int orc_write_list_page(const int64_t* list_offsets, const uint8_t* list_validity, size_t rows, int list_nullable,
                         const uint8_t* child_values, const uint8_t* child_validity, int item_nullable, int kind,
                         int width, int is_signed, const orc_write_options* opt, orc_buf* out, uint64_t* num_levels);
+int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int depth, const int* list_nullable,
+                         int item_nullable, int kind, int width, int64_t** out_offsets, uint8_t** out_bits,
+                         uint8_t* out_values, uint8_t* out_leaf_bits, size_t* counts, size_t* out_rows);
 int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int list_nullable, int item_nullable,
                        int kind, int width, int64_t* out_offsets, uint8_t* out_list_bits, uint8_t* out_values,
                        uint8_t* out_leaf_bits, size_t* out_rows, size_t* out_leaves);

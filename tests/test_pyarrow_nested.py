@@ -139,6 +139,10 @@ def test_levels_match_pyarrow(tmp_path, list_nullable, item_nullable):
         chunk += body + rep + dfb + stream
         metas.append((len(body) + len(rep) + len(dfb) + len(stream), nlev))
     offs, lv, vals, fv = O.read_list_column(chunk, metas, np.int32, list_nullable, item_nullable)
+    (go,), (gb,), gv, gf = O.read_nested_column(chunk, metas, np.int32, (list_nullable,), item_nullable)
+    assert (go == offs).all() and (gv == vals).all()  # the general reader at depth 1
+    assert (gb is None) == (lv is None) and (gb is None or (gb == lv).all())
+    assert (gf is None) == (fv is None) and (gf is None or (gf == fv).all())
     arr = t.column("c").combine_chunks()
     assert (offs == arr.offsets.to_numpy()).all()
     if list_nullable:
@@ -148,3 +152,78 @@ def test_levels_match_pyarrow(tmp_path, list_nullable, item_nullable):
     assert (vals[present] == arr.values.to_numpy(zero_copy_only=False)[present]).all()
     if item_nullable:
         assert (fv == arr.values.is_valid().to_numpy(zero_copy_only=False)).all()
+
+
+def list2_column(rng, rows, n0, n1, ni):
+    def inner():
+        r = rng.random()
+        if n1 and r < 0.1:
+            return None
+        if r < 0.2:
+            return []
+        return [None if ni and rng.random() < 0.15 else int(x) for x in rng.integers(-1000, 1000, int(rng.integers(1, 5)))]
+
+    vals = []
+    for _ in range(rows):
+        r = rng.random()
+        if n0 and r < 0.1:
+            vals.append(None)
+        elif r < 0.2:
+            vals.append([])
+        else:
+            vals.append([inner() for _ in range(int(rng.integers(1, 4)))])
+    leaf = pa.field("item", pa.int32(), nullable=ni)
+    mid = pa.field("item", pa.list_(leaf), nullable=n1)
+    field = pa.field("c", pa.list_(mid), nullable=n0)
+    return pa.table({"c": pa.array(vals, type=field.type)}, schema=pa.schema([field]))
+
+
+@pytest.mark.parametrize("n0", [False, True], ids=["outer_req", "outer_null"])
+@pytest.mark.parametrize("n1", [False, True], ids=["inner_req", "inner_null"])
+@pytest.mark.parametrize("ni", [False, True], ids=["item_req", "item_null"])
+def test_list_of_lists_match_pyarrow(tmp_path, n0, n1, ni):
+    """List<List<Int32>>: the general nested reader (orc_read_nested_page,
+    cum_sum / cum_rep over three nests) against pyarrow's arrays."""
+    rng = np.random.default_rng(11 + 4 * n0 + 2 * n1 + ni)
+    t = list2_column(rng, 8000, n0, n1, ni)
+    path = str(tmp_path / "ll.parquet")
+    pq.write_table(t, path, data_page_version="2.0", compression="NONE", use_dictionary=False,
+                   data_page_size=4096, write_statistics=False)
+    pages = data_pages_v2(path)
+    assert len(pages) > 3
+    leaf_def = int(n0) + 1 + int(n1) + 1
+    max_def = leaf_def + int(ni)
+    chunk, metas = pages_to_chunk(pages, max_def, leaf_def)
+    (o0, o1), (b0, b1), vals, fv = O.read_nested_column(chunk, metas, np.int32, (n0, n1), ni)
+    arr = t.column("c").combine_chunks()
+    inner = arr.values
+    assert (o0 == arr.offsets.to_numpy()).all()
+    assert (o1 == inner.offsets.to_numpy()).all()
+    if n0:
+        assert (b0 == arr.is_valid().to_numpy(zero_copy_only=False)).all()
+    if n1:
+        assert (b1 == inner.is_valid().to_numpy(zero_copy_only=False)).all()
+    leaf = inner.values
+    assert len(vals) == len(leaf)
+    present = leaf.is_valid().to_numpy(zero_copy_only=False)
+    assert (vals[present] == leaf.to_numpy(zero_copy_only=False)[present]).all()
+    if ni:
+        assert (fv == present).all()
+
+
+def pages_to_chunk(pages, max_def, leaf_def):
+    """strawboat nested pages from pyarrow V2 data pages: levels as they are,
+    values = every leaf slot (def >= leaf_def), PLAIN values at the non-null ones."""
+    bw = max_def.bit_length()
+    chunk, metas = b"", []
+    for rows, nlev, rep, dfb, plain in pages:
+        d = O.hybrid_decode(dfb, bw, nlev) if dfb else np.full(nlev, max_def, np.uint32)
+        slot_def = d[d >= leaf_def]
+        page_vals = np.zeros(len(slot_def), np.int32)
+        nn = slot_def == max_def
+        page_vals[nn] = np.frombuffer(plain, np.int32, int(nn.sum()))
+        stream = O.compress(page_vals, None, O.WriteOptions.make())
+        body = rows.to_bytes(4, "little") + len(rep).to_bytes(4, "little") + len(dfb).to_bytes(4, "little")
+        chunk += body + rep + dfb + stream
+        metas.append((len(body) + len(rep) + len(dfb) + len(stream), nlev))
+    return chunk, metas
