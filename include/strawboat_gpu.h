@@ -184,6 +184,41 @@ uint64_t sb_plan_num_leaves(const sb_plan* plan);
  * + the values streams at their leaf bases. */
 sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* plan, const sb_list_out* out);
 
+/* A primitive leaf under 1..4 list levels (List<List<T>> ...): the general
+ * read_validity_nested (read/read_basic.rs:95-164) -- per-level cum_sum /
+ * cum_rep over {nullable, repeated}, lists and primitives never "required" --
+ * then create_list per level (read/array/list.rs:48), pages concatenated with
+ * each level's offsets moved onto its child's running length.  Level 0 is
+ * the outermost list.  PageMeta.num_values is the page's level count. */
+#define SB_MAX_NEST 4
+typedef struct {
+  int32_t physical_type;                /* leaf type (fixed width) */
+  int32_t depth;                        /* list levels, 1..SB_MAX_NEST */
+  int32_t list_nullable[SB_MAX_NEST];   /* list level d is nullable */
+  int32_t item_nullable;                /* the leaf is nullable */
+  int32_t offset_width;                 /* 4 = List, 8 = LargeList (every level) */
+} sb_nested_desc;
+
+/* d_offsets[d]: sb_plan_nested_count(plan, d) + 1 entries; d_validity[d]
+ * over level d's entries (NULL when not nullable); d_values:
+ * sb_plan_nested_count(plan, depth) leaves; d_leaf_validity over the leaves. */
+typedef struct {
+  void* d_offsets[SB_MAX_NEST];
+  uint8_t* d_validity[SB_MAX_NEST];
+  void* d_values;
+  uint8_t* d_leaf_validity;
+} sb_nested_out;
+
+/* Plans a nested column and counts every level's entries on the device
+ * (synchronous); fails with the first bad page's status. */
+sb_status sb_plan_nested_column(sb_ctx* ctx, const sb_nested_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                                const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out);
+/* Entries of level d (0 = the top-level rows; depth = the leaves). */
+uint64_t sb_plan_nested_count(const sb_plan* plan, int32_t level);
+/* Asynchronous decode: the level walk (offsets, bitmaps) + the values
+ * streams at their leaf bases; sb_plan_status reports the first bad page. */
+sb_status sb_decode_nested_planned(sb_ctx* ctx, sb_plan* plan, const sb_nested_out* out);
+
 /* Waits for the plan's last decode and returns the first failing page's
  * status (SB_OK if every page decoded); *h_bad_page = its index or -1. */
 sb_status sb_plan_status(sb_ctx* ctx, sb_plan* plan, int64_t* h_bad_page);

@@ -74,6 +74,10 @@ struct sb_plan {
   bool binary = false;
   bool boolean = false;  // SB_T_BOOLEAN: values are a bitmap (k_bool_decode)
   bool list = false;     // List<primitive>: levels kernels + `inner` (the values streams as flat pages)
+  bool nested = false;   // general nesting (sb_nested_desc): k_nest_walk + `inner`
+  sb_nested_desc ndesc{};
+  uint64_t* d_nest = nullptr;        // [counts n(D+1) | bases n(D+1) | totals D+1]
+  std::vector<uint64_t> nest_totals;  // entries per level
   sb_list_desc ldesc{};
   uint8_t* d_lc = nullptr;  // list state, see list_state_bytes
   bool list_peek = false;   // sizes from the page headers (checked against the levels at plan time)
@@ -197,6 +201,7 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_scratch) (void)hipFree(p->d_scratch);
   if (p->d_bin) (void)hipFree(p->d_bin);
   if (p->d_lc) (void)hipFree(p->d_lc);
+  if (p->d_nest) (void)hipFree(p->d_nest);
   if (p->inner) sb_plan_destroy(p->inner);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
@@ -469,10 +474,12 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
 
 sb_status sb_plan_status(sb_ctx* ctx, sb_plan* p, int64_t* bad) {
   if (!ctx || !p) return fail(ctx, SB_E_ARG, "null argument");
-  if (p->list && p->inner) {  // levels first, then the values streams
-    p->list = false;
+  if ((p->list || p->nested) && p->inner) {  // levels first, then the values streams
+    const bool l = p->list, n = p->nested;
+    p->list = p->nested = false;
     sb_status st = sb_plan_status(ctx, p, bad);
-    p->list = true;
+    p->list = l;
+    p->nested = n;
     if (st) return st;
     return sb_plan_status(ctx, p->inner, bad);
   }
@@ -605,6 +612,140 @@ sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* p, const sb_list_out* out
     if (!lst) lst = list_launch(ctx, p, out, 2, p->list_peek);
     if (lst) return lst;
     sb_primitive_out vo{out->d_values ? out->d_values : out->d_offsets, nullptr};  // (no leaves: nothing written)
+    sb_status st = sb_decode_planned(ctx, p->inner, &vo);
+    if (st) return st;
+  }
+  if (p->timing) {
+    HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
+    p->timed = true;
+  }
+  return SB_OK;
+}
+
+static sb_status nest_launch(sb_ctx* ctx, sb_plan* p, const sb_nested_out* out, int stage) {
+  const uint64_t n = p->n_pages, D = (uint64_t)p->ndesc.depth;
+  sb::NestLaunch L{};
+  L.chunk = p->d_chunk;
+  L.pages = p->d_pages;
+  L.n_pages = (uint32_t)n;
+  L.depth = (uint32_t)D;
+  for (uint64_t d = 0; d < D; d++) L.nullable |= (p->ndesc.list_nullable[d] ? 1u : 0u) << d;
+  L.nullable |= (p->ndesc.item_nullable ? 1u : 0u) << D;
+  L.offset_width = (uint32_t)p->ndesc.offset_width;
+  L.counts = p->d_nest;
+  L.bases = p->d_nest + n * (D + 1);
+  L.totals = p->d_nest + 2 * n * (D + 1);
+  L.vpages = p->inner->d_pages;
+  if (out) {
+    for (uint64_t d = 0; d < D; d++) {
+      L.out_offsets[d] = (uint8_t*)out->d_offsets[d];
+      L.out_validity[d] = (uint32_t*)out->d_validity[d];
+    }
+    L.out_leaf_validity = (uint32_t*)out->d_leaf_validity;
+  }
+  L.status = p->d_status;
+  if (sb::launch_nest(stage, L, ctx->stream))
+    return fail(ctx, SB_E_DEVICE, "nested launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return SB_OK;
+}
+
+sb_status sb_plan_nested_column(sb_ctx* ctx, const sb_nested_desc* d, const uint8_t* d_chunk, uint64_t chunk_len,
+                                const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out) {
+  if (!ctx || !d || !out) return fail(ctx, SB_E_ARG, "null argument");
+  bool is_float;
+  if (!type_width(d->physical_type, &is_float) || d->physical_type == SB_T_BOOLEAN)
+    return fail(ctx, SB_E_NYI, "nested leaf type %d not supported", d->physical_type);
+  if (d->depth < 1 || d->depth > SB_MAX_NEST) return fail(ctx, SB_E_NYI, "nesting depth %d not supported", d->depth);
+  if (d->offset_width != 4 && d->offset_width != 8) return fail(ctx, SB_E_ARG, "offset width must be 4 or 8");
+  sb_column_desc cd{d->physical_type, 0};
+  sb_plan* inner = nullptr;
+  sb_status st = sb_plan_column(ctx, &cd, d_chunk, chunk_len, h_metas, n_pages, &inner);
+  if (st) return st;
+  sb_plan* p = new sb_plan();
+  p->desc = cd;
+  p->nested = true;
+  p->ndesc = *d;
+  p->inner = inner;
+  p->d_chunk = d_chunk;
+  p->chunk_len = chunk_len;
+  p->n_pages = n_pages;
+  p->width = inner->width;
+  p->is_float = is_float;
+  const uint64_t D = (uint64_t)d->depth, np = n_pages ? n_pages : 1;
+  hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
+  if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&p->d_nest, (2 * np * (D + 1) + D + 1) * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipEventCreate(&p->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&p->ev1);
+  if (e == hipSuccess && n_pages)  // the level pages (inner's table becomes the values streams)
+    e = hipMemcpyAsync(p->d_pages, inner->d_pages, n_pages * sizeof(sb::PageDesc), hipMemcpyDeviceToDevice, ctx->stream);
+  if (e != hipSuccess) {
+    sb_plan_destroy(p);
+    return fail(ctx, SB_E_DEVICE, "nested plan alloc: %s", hipGetErrorString(e));
+  }
+  p->nest_totals.assign(D + 1, 0);
+  if (n_pages) {  // count every level once: the caller allocates from the totals, decodes use the bases
+    if (nest_launch(ctx, p, nullptr, 0) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "nested counting failed: %s", hipGetErrorString(hipGetLastError()));
+    }
+    std::vector<uint32_t> stv(n_pages);
+    std::vector<uint64_t> cnt(n_pages * (D + 1)), bases(n_pages * (D + 1));
+    (void)hipMemcpy(stv.data(), p->d_status, n_pages * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(cnt.data(), p->d_nest, cnt.size() * 8, hipMemcpyDeviceToHost);
+    for (uint64_t i = 0; i < n_pages; i++) {
+      if (stv[i]) {
+        sb_plan_destroy(p);
+        return fail(ctx, (sb_status)stv[i], "page %llu: %s", (unsigned long long)i, sb_status_str((int)stv[i]));
+      }
+      for (uint64_t k = 0; k <= D; k++) {
+        bases[i * (D + 1) + k] = p->nest_totals[k];
+        p->nest_totals[k] += cnt[i * (D + 1) + k];
+      }
+    }
+    e = hipMemcpy(p->d_nest + n_pages * (D + 1), bases.data(), bases.size() * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_nest + 2 * n_pages * (D + 1), p->nest_totals.data(), (D + 1) * 8,
+                                       hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "nested plan upload: %s", hipGetErrorString(e));
+    }
+  }
+  p->n_rows = p->nest_totals[0];
+  p->n_leaves = p->nest_totals[D];
+  *out = p;
+  return SB_OK;
+}
+
+uint64_t sb_plan_nested_count(const sb_plan* p, int32_t level) {
+  if (!p || !p->nested || level < 0 || level > p->ndesc.depth) return 0;
+  return p->nest_totals[(size_t)level];
+}
+
+sb_status sb_decode_nested_planned(sb_ctx* ctx, sb_plan* p, const sb_nested_out* out) {
+  if (!ctx || !p || !out) return fail(ctx, SB_E_ARG, "null argument");
+  if (!p->nested) return fail(ctx, SB_E_ARG, "not a nested plan");
+  const int D = p->ndesc.depth;
+  for (int d = 0; d < D; d++) {
+    if (!out->d_offsets[d]) return fail(ctx, SB_E_ARG, "offsets of level %d are null", d);
+    if (p->ndesc.list_nullable[d] && p->nest_totals[d] && !out->d_validity[d])
+      return fail(ctx, SB_E_ARG, "validity of level %d is null", d);
+  }
+  if (p->n_leaves && !out->d_values) return fail(ctx, SB_E_ARG, "values buffer is null");
+  if (p->ndesc.item_nullable && p->n_leaves && !out->d_leaf_validity) return fail(ctx, SB_E_ARG, "leaf validity is null");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
+  for (int d = 0; d < D; d++)
+    if (p->ndesc.list_nullable[d] && p->nest_totals[d])
+      HIP_TRY(ctx, hipMemsetAsync(out->d_validity[d], 0, (p->nest_totals[d] + 31) / 32 * 4, ctx->stream));
+  if (p->ndesc.item_nullable && p->n_leaves)
+    HIP_TRY(ctx, hipMemsetAsync(out->d_leaf_validity, 0, (p->n_leaves + 31) / 32 * 4, ctx->stream));
+  if (!p->n_pages) {
+    for (int d = 0; d < D; d++) HIP_TRY(ctx, hipMemsetAsync(out->d_offsets[d], 0, (size_t)p->ndesc.offset_width, ctx->stream));
+  } else {
+    sb_status lst = nest_launch(ctx, p, out, 1);
+    if (lst) return lst;
+    sb_primitive_out vo{out->d_values ? out->d_values : out->d_offsets[0], nullptr};  // (no leaves: nothing written)
     sb_status st = sb_decode_planned(ctx, p->inner, &vo);
     if (st) return st;
   }

@@ -3484,6 +3484,221 @@ __global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
   }
 }
 
+// ===========================================================================
+// General nesting: a leaf under `depth` list levels (List<List<T>> ...),
+// read_validity_nested (read/read_basic.rs:95-164) level by level: nests
+// 0..depth-1 are lists (repeated; nullable per level), nest `depth` the
+// primitive; cum_sum / cum_rep over (nullable + repeated) / repeated; a nest
+// is pushed when rep <= cum_rep[d] && def >= cum_sum[d] (is_required is false
+// for lists and primitives, so the chain rule never fires).  One wave per
+// page, one level per lane per step: ballots give each level's pushes and
+// ranks; a list push's offset is its child's running count; validity bits
+// are compacted to push order and OR-ed into the (zeroed) bitmaps.
+// ===========================================================================
+struct NestArgs {
+  const uint8_t* chunk;
+  const PageDesc* pages;
+  uint32_t n_pages, depth, nullable, ow;
+  uint64_t* counts;
+  const uint64_t* bases;
+  const uint64_t* totals;
+  PageDesc* vpages;
+  uint8_t* out_offsets[kMaxNest];
+  uint32_t* out_validity[kMaxNest];
+  uint32_t* out_leaf_validity;
+  uint32_t* status;
+};
+
+// A window of hybrid runs (parquet2 HybridRleDecoder) over the levels of the
+// current 64-level step, parsed incrementally by one lane: the run holding
+// the step's first level plus every run up to the step's end (each run
+// covers >= 1 level, so <= 65 entries), so a stream may hold any number of
+// runs (pyarrow's writer mixes many RLE and bit-packed runs).
+struct RunWin {
+  uint32_t n, p, end, covered, bw;
+  uint32_t start[68];
+  uint32_t arg[68];  // bit-packed: 0x80000000 | payload position; RLE: the value
+};
+
+// lane 0: make the window cover levels [l0, lend)
+__device__ bool runwin_advance(const GlbSrc& s, RunWin& R, uint32_t l0, uint32_t lend, uint32_t* err) {
+  uint32_t k = R.n;
+  while (k > 0 && R.start[k - 1] > l0) k--;
+  if (k > 1) {  // keep the run holding l0
+    for (uint32_t i = k - 1; i < R.n; i++) {
+      R.start[i - (k - 1)] = R.start[i];
+      R.arg[i - (k - 1)] = R.arg[i];
+    }
+    R.n -= k - 1;
+  }
+  while (R.covered < lend) {
+    if (R.n >= 66) { put_err(err, ST_NYI); return false; }
+    uint32_t h = 0, sft = 0;
+    for (;;) {  // ULEB128 header
+      if (R.p >= R.end || sft > 28) { put_err(err, ST_OUT_OF_SPEC); return false; }
+      const uint32_t c = s.u8(R.p++);
+      h |= (c & 0x7Fu) << sft;
+      if (!(c & 0x80)) break;
+      sft += 7;
+    }
+    uint32_t cnt, arg;
+    if (h & 1) {  // bit-packed: h >> 1 groups of 8, clamped to the bytes present
+      const uint64_t want = (uint64_t)(h >> 1) * R.bw;
+      const uint32_t have = (uint32_t)min<uint64_t>(want, R.end - R.p);
+      cnt = (uint32_t)min<uint64_t>((uint64_t)(h >> 1) * 8, (uint64_t)have * 8 / max(R.bw, 1u));
+      arg = 0x80000000u | R.p;
+      R.p += have;
+    } else {  // RLE: h >> 1 repeats of a ceil(bw / 8)-byte value
+      const uint32_t vb = (R.bw + 7) / 8;
+      if (R.p + vb > R.end) { put_err(err, ST_OUT_OF_SPEC); return false; }
+      arg = 0;
+      for (uint32_t b = 0; b < vb; b++) arg |= s.u8(R.p + b) << (8 * b);
+      R.p += vb;
+      cnt = h >> 1;
+    }
+    if (cnt == 0) continue;  // an empty run yields no levels
+    R.start[R.n] = R.covered;
+    R.arg[R.n] = arg;
+    R.n++;
+    R.covered += cnt;
+  }
+  R.start[R.n] = R.covered;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t runwin_at(const GlbSrc& s, const RunWin& R, uint32_t i) {
+  uint32_t lo = 0, hi = R.n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (R.start[mid] <= i) lo = mid; else hi = mid;
+  }
+  const uint32_t a = R.arg[lo];
+  if (!(a & 0x80000000u)) return a;
+  const uint32_t bit = (i - R.start[lo]) * R.bw;
+  return (s.u32((a & 0x7FFFFFFFu) + (bit >> 3)) >> (bit & 7)) & ((1u << R.bw) - 1);
+}
+
+struct NestWave {
+  RunWin rep, def;
+  uint32_t err, rows, vpos;
+};
+
+__device__ __forceinline__ uint64_t compress64(uint64_t v, uint64_t m) {
+  const uint32_t lo = compress32((uint32_t)v, (uint32_t)m), hi = compress32((uint32_t)(v >> 32), (uint32_t)(m >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << __popc((uint32_t)m));
+}
+
+// n (<= 64) bits at bit position pos of a zeroed bitmap, OR-ed (lanes 0..2)
+__device__ __forceinline__ void put_bits64(uint32_t* bm, uint64_t pos, uint64_t v, uint32_t n) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (!n || !v || lane > 2) return;
+  const uint32_t sh = (uint32_t)(pos & 31);
+  const uint64_t w0 = pos >> 5;
+  const uint32_t word = lane == 0 ? (uint32_t)(v << sh)
+                      : lane == 1 ? (uint32_t)(sh ? (v >> (32 - sh)) : (v >> 32))
+                                  : (uint32_t)(sh ? (v >> (64 - sh)) : 0u);
+  if (word) atomicOr(&bm[w0 + lane], word);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(NT) void k_nest_walk(NestArgs a) {
+  __shared__ NestWave waves[NW];
+  const uint32_t lane = threadIdx.x & 63, D = a.depth;
+  NestWave& w = waves[threadIdx.x >> 6];
+  uint32_t cum_sum[kMaxNest + 2], cum_rep[kMaxNest + 2];
+  cum_sum[0] = cum_rep[0] = 0;
+  for (uint32_t d = 0; d <= D; d++) {
+    const uint32_t nl = (a.nullable >> d) & 1, rp = d < D ? 1u : 0u;
+    cum_sum[d + 1] = cum_sum[d] + nl + rp;
+    cum_rep[d + 1] = cum_rep[d] + rp;
+  }
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint32_t page = blockIdx.x * NW + (threadIdx.x >> 6); page < a.n_pages; page += gridDim.x * NW) {
+    const PageDesc pd = a.pages[page];
+    const GlbSrc s{a.chunk + pd.byte_off};
+    const uint32_t L = pd.num_values;
+    if (lane == 0) {
+      w.err = 0;
+      const uint32_t len = pd.byte_len;
+      if (len < 12) {
+        w.err = ST_IO;
+      } else {
+        const uint32_t rows = s.u32(0), rl = s.u32(4), dl = s.u32(8);
+        if ((uint64_t)12 + rl + dl > len) {
+          w.err = ST_IO;
+        } else {
+          w.rows = rows;
+          w.vpos = 12 + rl + dl;
+          w.rep = RunWin{0, 12, 12 + rl, 0, 32u - __clz(cum_rep[D + 1])};
+          w.def = RunWin{0, 12 + rl, 12 + rl + dl, 0, 32u - __clz(cum_sum[D + 1])};
+          if (L > 0 && rows == 0) w.err = ST_OUT_OF_SPEC;
+        }
+      }
+    }
+    wave_sync();
+    uint64_t carry[kMaxNest + 1] = {0, 0, 0, 0, 0}, base[kMaxNest + 1] = {0, 0, 0, 0, 0};
+    if (WRITE)
+      for (uint32_t d = 0; d <= D; d++) base[d] = a.bases[(uint64_t)page * (D + 1) + d];
+    uint32_t rows_seen = 0;
+    const uint32_t rows = w.rows;
+    if (!w.err) {
+      for (uint32_t l0 = 0; l0 < L; l0 += 64) {
+        if (lane == 0 && runwin_advance(s, w.rep, l0, min(l0 + 64, L), &w.err))
+          runwin_advance(s, w.def, l0, min(l0 + 64, L), &w.err);
+        wave_sync();
+        if (w.err) break;
+        const uint32_t l = l0 + lane;
+        const bool in = l < L;
+        const uint32_t r = in ? runwin_at(s, w.rep, l) : 0u, dv = in ? runwin_at(s, w.def, l) : 0u;
+        if (l == 0 && r != 0) w.err = ST_OUT_OF_SPEC;  // the first level starts no row
+        const uint64_t rs = __ballot(in && r == 0);
+        // consumed: inclusive row count <= rows (read_basic.rs:150-162)
+        const bool cons = in && rows_seen + (uint32_t)__popcll(rs & (below | (1ull << lane))) <= rows;
+        uint64_t push[kMaxNest + 1];
+        for (uint32_t d = 0; d <= D; d++) push[d] = __ballot(cons && r <= cum_rep[d] && dv >= cum_sum[d]);
+        if (WRITE) {
+          for (uint32_t d = 0; d <= D; d++) {
+            const bool me = (push[d] >> lane) & 1;
+            const uint64_t pos = base[d] + carry[d] + (uint32_t)__popcll(push[d] & below);
+            if (d < D && me) {  // offset = the child's count before this level
+              const uint64_t v = base[d + 1] + carry[d + 1] + (uint32_t)__popcll(push[d + 1] & below);
+              bin_put_off(a.out_offsets[d], pos, v, (int)a.ow);
+            }
+            if ((a.nullable >> d) & 1) {
+              const uint64_t vm = __ballot(me && dv > cum_sum[d]);
+              const uint32_t np = (uint32_t)__popcll(push[d]);
+              uint32_t* bm = d < D ? a.out_validity[d] : a.out_leaf_validity;
+              put_bits64(bm, base[d] + carry[d], compress64(vm, push[d]), np);
+            }
+            (void)pos;
+          }
+        }
+        for (uint32_t d = 0; d <= D; d++) carry[d] += (uint32_t)__popcll(push[d]);
+        rows_seen += (uint32_t)__popcll(rs);
+        if (rows_seen > rows) break;  // every later level is past the last row
+      }
+      if (lane == 0 && min(rows_seen, rows) != rows) w.err = ST_OUT_OF_SPEC;  // levels ended early
+    }
+    wave_sync();
+    if (lane == 0) {
+      uint32_t err = w.err;
+      if (!WRITE) {
+        for (uint32_t d = 0; d <= D; d++) a.counts[(uint64_t)page * (D + 1) + d] = err ? 0 : carry[d];
+      } else {
+        for (uint32_t d = 0; d <= D; d++)
+          if (!err && carry[d] != a.counts[(uint64_t)page * (D + 1) + d]) err = ST_OUT_OF_SPEC;
+        const bool ok = err == 0;
+        a.vpages[page] = PageDesc{pd.byte_off + (ok ? w.vpos : 0), base[D], ok ? pd.byte_len - w.vpos : 0,
+                                  ok ? (uint32_t)carry[D] : 0u, 0};
+        if (page == a.n_pages - 1)  // create_list appends each child's length
+          for (uint32_t d = 0; d < D; d++) bin_put_off(a.out_offsets[d], a.totals[d], a.totals[d + 1], (int)a.ow);
+      }
+      a.status[page] = err;
+    }
+    wave_sync();
+  }
+}
+
 }  // namespace sbk
 
 namespace sb {
@@ -3586,6 +3801,22 @@ int launch_list(int stage, const ListLaunch& L, void* stream) {
   } else {
     hipLaunchKernelGGL(sbk::k_list_levels, dim3(grid), dim3(sbk::NT), 0, st, a);
   }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}  // namespace sb
+
+namespace sb {
+int launch_nest(int stage, const NestLaunch& L, void* stream) {
+  if (L.n_pages == 0) return 0;
+  sbk::NestArgs a{L.chunk, L.pages, L.n_pages, L.depth, L.nullable, L.offset_width, L.counts, L.bases, L.totals,
+                  L.vpages, {}, {}, L.out_leaf_validity, L.status};
+  for (int d = 0; d < kMaxNest; d++) {
+    a.out_offsets[d] = L.out_offsets[d];
+    a.out_validity[d] = L.out_validity[d];
+  }
+  const uint32_t grid = std::min<uint32_t>((L.n_pages + sbk::NW - 1) / sbk::NW, kListGrid);
+  if (stage == 0) hipLaunchKernelGGL(sbk::k_nest_walk<false>, dim3(grid), dim3(sbk::NT), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(sbk::k_nest_walk<true>, dim3(grid), dim3(sbk::NT), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb

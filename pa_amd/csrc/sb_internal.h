@@ -169,4 +169,27 @@ struct ListLaunch {
 constexpr uint32_t kListGrid = 2048;
 int launch_list(int stage, const ListLaunch& a, void* stream);
 
+// A leaf under depth (1..4) list levels, the general level walk
+// (read_validity_nested with cum_sum / cum_rep): stage 0 counts each page's
+// entries per level, stage 1 writes offsets, bitmaps and the values-stream
+// descriptors from host-scanned bases.
+constexpr int kMaxNest = 4;
+struct NestLaunch {
+  const uint8_t* chunk;
+  const PageDesc* pages;
+  uint32_t n_pages;
+  uint32_t depth;
+  uint32_t nullable;       // bit d: list level d nullable (d < depth); bit depth: the leaf
+  uint32_t offset_width;
+  uint64_t* counts;        // [n_pages][depth + 1] entries per level (stage 0 out)
+  const uint64_t* bases;   // [n_pages][depth + 1] first entry of each level (stage 1 in)
+  const uint64_t* totals;  // [depth + 1]
+  PageDesc* vpages;
+  uint8_t* out_offsets[kMaxNest];
+  uint32_t* out_validity[kMaxNest];
+  uint32_t* out_leaf_validity;
+  uint32_t* status;
+};
+int launch_nest(int stage, const NestLaunch& a, void* stream);
+
 }  // namespace sb

@@ -187,3 +187,109 @@ def batch_read_list(chunk, page_metas: Sequence[PageMeta], dtype, list_nullable:
         return dec.decode()
     finally:
         dec.close()
+
+
+MAX_NEST = 4
+
+
+class NestedDescC(ctypes.Structure):
+    _fields_ = [("physical_type", ctypes.c_int32), ("depth", ctypes.c_int32),
+                ("list_nullable", ctypes.c_int32 * MAX_NEST), ("item_nullable", ctypes.c_int32),
+                ("offset_width", ctypes.c_int32)]
+
+
+class NestedOutC(ctypes.Structure):
+    _fields_ = [("d_offsets", ctypes.c_void_p * MAX_NEST), ("d_validity", ctypes.c_void_p * MAX_NEST),
+                ("d_values", ctypes.c_void_p), ("d_leaf_validity", ctypes.c_void_p)]
+
+
+def _nested_lib():
+    L = N.lib()
+    if not getattr(L, "_nested_ready", False):
+        P, U64, I32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32
+        L.sb_plan_nested_column.argtypes = [P, ctypes.POINTER(NestedDescC), P, U64, ctypes.POINTER(N.PageMetaC), U64,
+                                            ctypes.POINTER(ctypes.c_void_p)]
+        L.sb_plan_nested_column.restype = I32
+        L.sb_plan_nested_count.argtypes = [P, I32]
+        L.sb_plan_nested_count.restype = U64
+        L.sb_decode_nested_planned.argtypes = [P, P, ctypes.POINTER(NestedOutC)]
+        L.sb_decode_nested_planned.restype = I32
+        L._nested_ready = True
+    return L
+
+
+class NestedColumnDecoder:
+    """A leaf under len(list_nullable) list levels (List<List<T>> ..., level 0
+    outermost): read_validity_nested in its general form (read_basic.rs:95-164)
+    + create_list per level.  decode() -> (offsets per level, validity per
+    level | None, values, leaf validity | None) device tensors."""
+
+    def __init__(self, chunk, page_metas: Sequence[PageMeta], dtype, list_nullable, item_nullable: bool,
+                 ctx: Optional[Context] = None, large: bool = False):
+        import torch
+
+        self._torch = torch
+        self.ctx = resolve_context(ctx, chunk)
+        self.dtype = np.dtype(dtype)
+        self.list_nullable = tuple(bool(x) for x in list_nullable)
+        self.depth = len(self.list_nullable)
+        if not 1 <= self.depth <= MAX_NEST:
+            raise N.StrawboatError(N.E_NYI, f"nesting depth {self.depth} not supported")
+        self.item_nullable = bool(item_nullable)
+        self.offset_width = 8 if large else 4
+        self.chunk = _as_device_bytes(chunk, self.ctx.device)
+        self.metas = list(page_metas)
+        L = _nested_lib()
+        metas = (N.PageMetaC * max(1, len(self.metas)))(*[N.PageMetaC(m.length, m.num_values) for m in self.metas])
+        ln = (ctypes.c_int32 * MAX_NEST)(*([int(x) for x in self.list_nullable] + [0] * (MAX_NEST - self.depth)))
+        desc = NestedDescC(physical_type(self.dtype), self.depth, ln, int(self.item_nullable), self.offset_width)
+        h = ctypes.c_void_p()
+        st = L.sb_plan_nested_column(self.ctx._h, ctypes.byref(desc), ctypes.c_void_p(self.chunk.data_ptr()),
+                                     self.chunk.numel(), metas, len(self.metas), ctypes.byref(h))
+        if st:
+            raise N.StrawboatError(st, self.ctx.error())
+        self._h = h
+        self.counts = [int(L.sb_plan_nested_count(h, d)) for d in range(self.depth + 1)]
+
+    def alloc_outputs(self):
+        torch = self._torch
+        dev = f"cuda:{self.ctx.device}"
+        odt = torch.int64 if self.offset_width == 8 else torch.int32
+        bm = lambda n: torch.empty(max((n + 31) // 32, 1) * 4, dtype=torch.uint8, device=dev)  # noqa: E731
+        offs = [torch.empty(self.counts[d] + 1, dtype=odt, device=dev) for d in range(self.depth)]
+        valid = [bm(self.counts[d]) if self.list_nullable[d] else None for d in range(self.depth)]
+        tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[self.dtype.itemsize]
+        values = torch.empty(max(self.counts[self.depth], 1), dtype=tdt, device=dev)
+        leaf = bm(self.counts[self.depth]) if self.item_nullable else None
+        return offs, valid, values, leaf
+
+    def decode(self, outs=None):
+        offs, valid, values, leaf = outs or self.alloc_outputs()
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        o = NestedOutC()
+        for d in range(self.depth):
+            o.d_offsets[d] = p(offs[d])
+            o.d_validity[d] = p(valid[d])
+        o.d_values = p(values)
+        o.d_leaf_validity = p(leaf)
+        L = _nested_lib()
+        st = L.sb_decode_nested_planned(self.ctx._h, self._h, ctypes.byref(o))
+        if st:
+            raise N.StrawboatError(st, self.ctx.error())
+        bad = ctypes.c_int64(-1)
+        st = N.lib().sb_plan_status(self.ctx._h, self._h, ctypes.byref(bad))
+        if st:
+            raise N.StrawboatError(st, self.ctx.error())
+        return offs, valid, values, leaf
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().sb_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+

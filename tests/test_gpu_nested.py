@@ -1,0 +1,96 @@
+"""General nesting on the GPU (sb_plan_nested_column / k_nest_walk): a
+primitive leaf under 1, 2 or 3 list levels in every nullability, pages built
+from pyarrow's parquet Data Page V2 rep / def streams (tests/
+test_pyarrow_nested.py) with the leaf values stream under several codecs,
+decoded bit-exactly against the oracle's general reader
+(orc_read_nested_page, itself pinned against pyarrow)."""
+import itertools
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+pa = pytest.importorskip("pyarrow")
+pq = pytest.importorskip("pyarrow.parquet")
+
+from tests.test_pyarrow_nested import data_pages_v2  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pa_amd
+
+    return pa_amd.default_context(0)
+
+
+def nested_values(rng, depth, nulls, leaf_null, n):
+    def build(level):
+        r = rng.random()
+        if nulls[level] and r < 0.1:
+            return None
+        if r < 0.2:
+            return []
+        if level == depth - 1:
+            return [None if leaf_null and rng.random() < 0.15 else int(x)
+                    for x in rng.integers(-10**6, 10**6, int(rng.integers(1, 5)))]
+        return [build(level + 1) for _ in range(int(rng.integers(1, 4)))]
+
+    t = pa.int64()
+    f = pa.field("item", t, nullable=leaf_null)
+    for level in reversed(range(depth)):
+        f = pa.field("item" if level else "c", pa.list_(f), nullable=nulls[level])
+    return pa.table({"c": pa.array([build(0) for _ in range(n)], type=f.type)}, schema=pa.schema([f]))
+
+
+def chunk_of(tmp_path, t, depth, nulls, leaf_null, opts):
+    path = str(tmp_path / "n.parquet")
+    pq.write_table(t, path, data_page_version="2.0", compression="NONE", use_dictionary=False, data_page_size=4096,
+                   write_statistics=False)
+    leaf_def = sum(int(x) + 1 for x in nulls)
+    max_def = leaf_def + int(leaf_null)
+    bw = max_def.bit_length()
+    chunk, metas = b"", []
+    for rows, nlev, rep, dfb, plain in data_pages_v2(path):
+        d = O.hybrid_decode(dfb, bw, nlev) if dfb else np.full(nlev, max_def, np.uint32)
+        slot_def = d[d >= leaf_def]
+        vals = np.zeros(len(slot_def), np.int64)
+        nn = slot_def == max_def
+        vals[nn] = np.frombuffer(plain, np.int64, int(nn.sum()))
+        stream = O.compress(vals, None, opts)
+        body = rows.to_bytes(4, "little") + len(rep).to_bytes(4, "little") + len(dfb).to_bytes(4, "little")
+        chunk += body + rep + dfb + stream
+        metas.append((len(body) + len(rep) + len(dfb) + len(stream), nlev))
+    return chunk, metas
+
+
+CODECS = {"none": dict(), "lz4": dict(default_codec=O.LZ4), "adaptive": dict(ratio=1.2)}
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+@pytest.mark.parametrize("codec", list(CODECS))
+def test_nested_depths(ctx, tmp_path, depth, codec):
+    import pa_amd
+
+    for nulls in itertools.product([False, True], repeat=depth):
+        for leaf_null in (False, True):
+            rng = np.random.default_rng(depth * 100 + sum(nulls) * 10 + leaf_null)
+            t = nested_values(rng, depth, nulls, leaf_null, 3000)
+            chunk, metas = chunk_of(tmp_path, t, depth, nulls, leaf_null, O.WriteOptions.make(**CODECS[codec]))
+            eo, eb, ev, ef = O.read_nested_column(chunk, metas, np.int64, nulls, leaf_null)
+            dec = pa_amd.NestedColumnDecoder(chunk, [pa_amd.PageMeta(l, m) for l, m in metas], np.int64, nulls,
+                                             leaf_null, ctx)
+            go, gb, gv, gf = dec.decode()
+            for d in range(depth):
+                assert (go[d].cpu().numpy().astype(np.int64) == eo[d]).all(), (nulls, leaf_null, d)
+                if nulls[d]:
+                    n = len(eo[d]) - 1
+                    assert (pa_amd.read.unpack_bitmap(gb[d], n).cpu().numpy() == eb[d]).all(), (nulls, d)
+            assert (gv.cpu().numpy()[:len(ev)] == ev).all()
+            if leaf_null:
+                assert (pa_amd.read.unpack_bitmap(gf, len(ev)).cpu().numpy() == ef).all()
+            dec.close()
