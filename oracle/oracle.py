@@ -438,12 +438,15 @@ def read_list_column(chunk, metas, dtype, list_nullable, item_nullable):
             np.concatenate(leafv_all) if item_nullable else None)
 
 
-def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable):
+def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable, leaf="fixed", offset_width=4):
     """batch read of a leaf under len(list_nullable) list levels (outermost
     first): per page orc_read_nested_page, then the pages concatenated with
     each level's offsets moved onto its child's running length ->
-    ([offsets per level], [validity per level | None], values, leaf validity | None)."""
-    L = lib()
+    ([offsets per level], [validity per level | None], values, leaf validity | None).
+    leaf="binary": values = (offsets int64, bytes) of the concatenated per-page
+    Utf8 arrays (each page's values[p0:pn], arrow concatenate);
+    leaf="bool": values = a bool array."""
+    L = _bin_lib()
     if not getattr(L, "_nested_ready", False):
         P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
         L.orc_read_nested_page.argtypes = [P, S, S, I, P, I, I, I, P, P, P, P, P, ctypes.POINTER(S)]
@@ -451,7 +454,9 @@ def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable):
     dtype = np.dtype(dtype)
     D = len(list_nullable)
     src = np.frombuffer(chunk, np.uint8)
-    kind = 1 if dtype.kind == "f" else 0
+    kind = {"binary": 2, "bool": 3}.get(leaf, 1 if dtype.kind == "f" else 0)
+    width = offset_width if leaf == "binary" else dtype.itemsize
+    bin_offs, bin_vals, vbase = [np.zeros(1, np.int64)], [], 0
     offs = [[] for _ in range(D)]
     bits = [[] for _ in range(D)]
     vals, leafv = [], []
@@ -462,20 +467,34 @@ def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable):
         page = np.ascontiguousarray(src[pos:pos + length])
         o = [np.zeros(nlev + 1, np.int64) for _ in range(D)]
         b = [np.zeros(nlev // 8 + 2, np.uint8) for _ in range(D)]
-        v = np.zeros(nlev + 1, dtype)
+        v = np.zeros(nlev + 1, dtype) if kind < 2 else np.zeros(nlev // 8 + 2, np.uint8)
         fb = np.zeros(nlev // 8 + 2, np.uint8)
         op = (ctypes.c_void_p * D)(*[x.ctypes.data for x in o])
         bp = (ctypes.c_void_p * D)(*[x.ctypes.data for x in b])
         cnt = (ctypes.c_size_t * (D + 1))()
         rows = ctypes.c_size_t()
-        rc = L.orc_read_nested_page(_ptr(page), length, nlev, D, ln, int(item_nullable), kind, dtype.itemsize, op, bp,
-                                    _ptr(v), _ptr(fb), cnt, ctypes.byref(rows))
-        _check(rc, "read_nested_page")
+        bv = _BinVec()
+        vptr = ctypes.addressof(bv) if kind == 2 else _ptr(v)
+        try:
+            rc = L.orc_read_nested_page(_ptr(page), length, nlev, D, ln, int(item_nullable), kind, width, op, bp,
+                                        vptr, _ptr(fb), cnt, ctypes.byref(rows))
+            _check(rc, "read_nested_page")
+            if kind == 2:
+                po = np.ctypeslib.as_array(bv.offsets, shape=(bv.n_off,)).copy() if bv.n_off else np.zeros(1, np.int64)
+                pv = ctypes.string_at(bv.values, bv.n_val) if bv.n_val else b""
+                bin_offs.append(po[1:] - po[0] + vbase)
+                bin_vals.append(pv[po[0]:po[-1]])
+                vbase += int(po[-1] - po[0])
+        finally:
+            L.orc_binvec_free(ctypes.byref(bv))
         for d in range(D):
             offs[d].append(o[d][:cnt[d]] + base[d + 1])
             if list_nullable[d]:
                 bits[d].append(np.unpackbits(b[d], bitorder="little")[:cnt[d]].astype(bool))
-        vals.append(v[:cnt[D]])
+        if kind < 2:
+            vals.append(v[:cnt[D]])
+        elif kind == 3:
+            vals.append(np.unpackbits(v, bitorder="little")[:cnt[D]].astype(bool))
         if item_nullable:
             leafv.append(np.unpackbits(fb, bitorder="little")[:cnt[D]].astype(bool))
         for d in range(D + 1):
@@ -483,7 +502,8 @@ def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable):
         pos += length
     out_offs = [np.concatenate(offs[d] + [np.array([base[d + 1]], np.int64)]) for d in range(D)]
     out_bits = [np.concatenate(bits[d]) if list_nullable[d] else None for d in range(D)]
-    return out_offs, out_bits, np.concatenate(vals), (np.concatenate(leafv) if item_nullable else None)
+    values = (np.concatenate(bin_offs), b"".join(bin_vals)) if kind == 2 else np.concatenate(vals)
+    return out_offs, out_bits, values, (np.concatenate(leafv) if item_nullable else None)
 
 
 # ---- boolean pages (compression/boolean/*.rs, read/array/boolean.rs) ---------

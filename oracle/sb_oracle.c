@@ -1902,8 +1902,14 @@ int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int
   free(rep);
   free(def);
   if (rows != additional) return ORC_E_OUT_OF_SPEC;
-  rc = kind ? orc_decompress_double(page, len, &pos, width, n[depth], out_values)
-            : orc_decompress_integer(page, len, &pos, width, n[depth], out_values);
+  /* the leaf's values (read_nested_integer / _binary / _boolean): kind 0 / 1 =
+   * integer / double stream of `width` bytes, 2 = decompress_binary with
+   * offset width `width` into the orc_binvec at out_values, 3 =
+   * decompress_boolean into the bitmap at out_values */
+  if (kind == 2) rc = orc_decompress_binary(page, len, &pos, n[depth], width, (orc_binvec*)out_values);
+  else if (kind == 3) rc = orc_decompress_boolean(page, len, &pos, n[depth], out_values);
+  else rc = kind ? orc_decompress_double(page, len, &pos, width, n[depth], out_values)
+                 : orc_decompress_integer(page, len, &pos, width, n[depth], out_values);
   for (int d = 0; d <= depth; d++) counts[d] = n[d];
   *out_rows = rows;
   return rc;

@@ -78,8 +78,8 @@ class Compact:
             out[fid] = self.value(t)
 
 
-def data_pages_v2(path):
-    """(rows, levels, rep bytes, def bytes, values bytes) of each data page of column 0."""
+def data_pages_v2(path, with_encoding=False):
+    """(rows, levels, rep bytes, def bytes, values bytes[, values encoding]) of each data page of column 0."""
     f = pq.ParquetFile(path)
     cm = f.metadata.row_group(0).column(0)
     raw = open(path, "rb").read()
@@ -94,7 +94,8 @@ def data_pages_v2(path):
             continue
         v2 = h[8]
         dl, rl = v2[5], v2[6]
-        pages.append((v2[3], v2[1], body[:rl], body[rl:rl + dl], body[rl + dl:]))
+        pg = (v2[3], v2[1], body[:rl], body[rl:rl + dl], body[rl + dl:])
+        pages.append(pg + (v2[4],) if with_encoding else pg)
     return pages
 
 
@@ -227,3 +228,99 @@ def pages_to_chunk(pages, max_def, leaf_def):
         chunk += body + rep + dfb + stream
         metas.append((len(body) + len(rep) + len(dfb) + len(stream), nlev))
     return chunk, metas
+
+
+def leaf_pages(pages, max_def, leaf_def, encode):
+    """strawboat nested pages whose values section is encode(slot_def, plain, encoding)."""
+    bw = max_def.bit_length()
+    chunk, metas = b"", []
+    for rows, nlev, rep, dfb, plain, enc in pages:
+        d = O.hybrid_decode(dfb, bw, nlev) if dfb else np.full(nlev, max_def, np.uint32)
+        stream = encode(d[d >= leaf_def], plain, enc)
+        body = rows.to_bytes(4, "little") + len(rep).to_bytes(4, "little") + len(dfb).to_bytes(4, "little")
+        chunk += body + rep + dfb + stream
+        metas.append((len(body) + len(rep) + len(dfb) + len(stream), nlev))
+    return chunk, metas
+
+
+def utf8_stream(slot_def, plain, max_def, opts=None):
+    """PLAIN BYTE_ARRAY values ([u32 len][bytes]) of the non-null slots -> a
+    compress_binary stream over every leaf slot (null slots empty)."""
+    strs, p = [], 0
+    for dv in slot_def:
+        if dv == max_def:
+            n = int.from_bytes(plain[p:p + 4], "little")
+            strs.append(plain[p + 4:p + 4 + n])
+            p += 4 + n
+        else:
+            strs.append(b"")
+    vals, offs = O.strings_to_arrow(strs)
+    return O.write_binary_page(vals, offs, None, False, opts or O.WriteOptions.make())
+
+
+def bool_stream(slot_def, plain, max_def, opts=None, encoding=0):
+    """PLAIN (bit-packed) or RLE ([u32 len][hybrid, bit width 1]) booleans of
+    the non-null slots -> a compress_boolean stream over every leaf slot (null
+    slots false)."""
+    nn = slot_def == max_def
+    if encoding == 3:
+        bits = O.hybrid_decode(plain[4:4 + int.from_bytes(plain[:4], "little")], 1, int(nn.sum())).astype(bool)
+    else:
+        bits = np.unpackbits(np.frombuffer(plain, np.uint8), bitorder="little")[:int(nn.sum())].astype(bool)
+    v = np.zeros(len(slot_def), bool)
+    v[nn] = bits
+    return O.write_bool_page(v, None, False, opts or O.WriteOptions.make(), offset=0, n=len(v))
+
+
+@pytest.mark.parametrize("leaf", ["utf8", "bool"])
+@pytest.mark.parametrize("list_nullable", [False, True], ids=["list_req", "list_null"])
+@pytest.mark.parametrize("item_nullable", [False, True], ids=["item_req", "item_null"])
+def test_list_of_utf8_bool_match_pyarrow(tmp_path, leaf, list_nullable, item_nullable):
+    rng = np.random.default_rng(31 + 2 * list_nullable + item_nullable)
+    vals = []
+    for _ in range(6000):
+        r = rng.random()
+        if list_nullable and r < 0.1:
+            vals.append(None)
+        elif r < 0.2:
+            vals.append([])
+        else:
+            k = int(rng.integers(1, 6))
+            if leaf == "utf8":
+                vals.append([None if item_nullable and rng.random() < 0.15 else str(x) * int(rng.integers(0, 3))
+                             for x in rng.integers(0, 10**6, k)])
+            else:
+                vals.append([None if item_nullable and rng.random() < 0.15 else bool(x) for x in rng.integers(0, 2, k)])
+    t_item = pa.utf8() if leaf == "utf8" else pa.bool_()
+    field = pa.field("c", pa.list_(pa.field("item", t_item, nullable=item_nullable)), nullable=list_nullable)
+    t = pa.table({"c": pa.array(vals, type=field.type)}, schema=pa.schema([field]))
+    path = str(tmp_path / "lu.parquet")
+    pq.write_table(t, path, data_page_version="2.0", compression="NONE", use_dictionary=False,
+                   data_page_size=4096, write_statistics=False)
+    leaf_def = int(list_nullable) + 1
+    max_def = leaf_def + int(item_nullable)
+    if leaf == "utf8":
+        encode = lambda sd, pl, e: utf8_stream(sd, pl, max_def)  # noqa: E731
+    else:
+        encode = lambda sd, pl, e: bool_stream(sd, pl, max_def, encoding=e)  # noqa: E731
+    chunk, metas = leaf_pages(data_pages_v2(path, True), max_def, leaf_def, encode)
+    (offs,), (lv,), values, fv = O.read_nested_column(chunk, metas, np.uint8, (list_nullable,), item_nullable,
+                                                      leaf="binary" if leaf == "utf8" else "bool")
+    arr = t.column("c").combine_chunks()
+    assert (offs == arr.offsets.to_numpy()).all()
+    if list_nullable:
+        assert (lv == arr.is_valid().to_numpy(zero_copy_only=False)).all()
+    items = arr.values
+    present = items.is_valid().to_numpy(zero_copy_only=False)
+    if item_nullable:
+        assert (fv == present).all()
+    if leaf == "utf8":
+        vo, vb = values
+        got = [vb[vo[i]:vo[i + 1]] for i in range(len(vo) - 1)]
+        exp = items.to_pylist()
+        assert len(got) == len(exp)
+        assert all(g == e.encode() for g, e, ok in zip(got, exp, present) if ok)
+    else:
+        exp = np.array([bool(x) for x in items.to_pylist()], bool) if len(items) else np.zeros(0, bool)
+        assert len(values) == len(exp)
+        assert (values[present] == exp[present]).all()
