@@ -192,7 +192,7 @@ sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* plan, const sb_list_out* 
  * the outermost list.  PageMeta.num_values is the page's level count. */
 #define SB_MAX_NEST 4
 typedef struct {
-  int32_t physical_type;                /* leaf type (fixed width) */
+  int32_t physical_type;                /* leaf type: fixed width, Boolean, Binary / Utf8 (Large too) */
   int32_t depth;                        /* list levels, 1..SB_MAX_NEST */
   int32_t list_nullable[SB_MAX_NEST];   /* list level d is nullable */
   int32_t item_nullable;                /* the leaf is nullable */
@@ -200,13 +200,19 @@ typedef struct {
 } sb_nested_desc;
 
 /* d_offsets[d]: sb_plan_nested_count(plan, d) + 1 entries; d_validity[d]
- * over level d's entries (NULL when not nullable); d_values:
- * sb_plan_nested_count(plan, depth) leaves; d_leaf_validity over the leaves. */
+ * over level d's entries (NULL when not nullable); d_leaf_validity over the
+ * leaves.  Leaf values: fixed width -- d_values holds
+ * sb_plan_nested_count(plan, depth) values; Boolean -- d_values is their
+ * bitmap; Binary / Utf8 -- d_leaf_offsets holds leaves + 1 offsets (the
+ * physical type's width) and d_values values_capacity >=
+ * sb_plan_values_bytes(plan) bytes (read_nested_binary, pages concatenated). */
 typedef struct {
   void* d_offsets[SB_MAX_NEST];
   uint8_t* d_validity[SB_MAX_NEST];
   void* d_values;
   uint8_t* d_leaf_validity;
+  void* d_leaf_offsets;
+  uint64_t values_capacity;
 } sb_nested_out;
 
 /* Plans a nested column and counts every level's entries on the device

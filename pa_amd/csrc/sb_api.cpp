@@ -211,9 +211,33 @@ void sb_plan_destroy(sb_plan* p) {
 uint64_t sb_plan_num_rows(const sb_plan* p) { return p ? p->n_rows : 0; }
 uint64_t sb_plan_num_pages(const sb_plan* p) { return p ? p->n_pages : 0; }
 
+// The page table of a plan: page i at byte pages[i].byte_off of the chunk,
+// rows [row_off, row_off + num_values) of the output (sb_plan_column: the
+// running sums of the PageMeta; nested leaves: each page's values stream at
+// its leaf base).
+static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                            std::vector<sb::PageDesc> pages, sb_plan** out);
+
 sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
                          const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out) {
   if (!ctx || !desc || !out || (!h_metas && n_pages)) return fail(ctx, SB_E_ARG, "null argument");
+  if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
+  std::vector<sb::PageDesc> pages(n_pages);
+  uint64_t off = 0, rows = 0;
+  for (uint64_t i = 0; i < n_pages; i++) {
+    const sb_page_meta& m = h_metas[i];
+    if (m.length > 0xFFFFFFFFull || m.num_values > 0xFFFFFFFFull)
+      return fail(ctx, SB_E_ARG, "page %llu exceeds u32 sizes", (unsigned long long)i);
+    pages[i] = sb::PageDesc{off, rows, (uint32_t)m.length, (uint32_t)m.num_values, 0};
+    off += m.length;
+    rows += m.num_values;
+  }
+  return plan_pages(ctx, desc, d_chunk, chunk_len, std::move(pages), out);
+}
+
+static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                            std::vector<sb::PageDesc> pages, sb_plan** out) {
+  const uint64_t n_pages = pages.size();
   bool is_float;
   int width = type_width(desc->physical_type, &is_float);
   const int ptype = desc->physical_type;
@@ -224,20 +248,17 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
 
-  std::vector<sb::PageDesc> pages(n_pages);
   std::vector<uint32_t> staged, global;
-  uint64_t off = 0, rows = 0;
+  uint64_t rows = 0;
   uint32_t max_stage = 0, max_bool = 0;
   bool needs_zero = false;
   for (uint64_t i = 0; i < n_pages; i++) {
-    const sb_page_meta& m = h_metas[i];
-    if (m.length > 0xFFFFFFFFull || m.num_values > 0xFFFFFFFFull)
-      return fail(ctx, SB_E_ARG, "page %llu exceeds u32 sizes", (unsigned long long)i);
-    if (off + m.length > chunk_len)
+    const sb::PageDesc& pd = pages[i];
+    const sb_page_meta m{pd.byte_len, pd.num_values};
+    if (pd.byte_off + m.length > chunk_len)
       return fail(ctx, SB_E_ARG, "page %llu overruns the column chunk", (unsigned long long)i);
-    pages[i] = sb::PageDesc{off, rows, (uint32_t)m.length, (uint32_t)m.num_values, 0};
     // a 32-bit validity word shared by two pages is merged with atomics
-    if ((rows & 31) || (m.num_values & 31)) needs_zero = true;
+    if ((pd.row_off & 31) || (m.num_values & 31)) needs_zero = true;
     if (is_bool) {  // page + its expanded bitmap, as k_bool_decode lays them out in LDS
       const uint64_t need = ((m.length + 15 + sb::kStagePad + 15) & ~15ull) + (((m.num_values + 7) / 8 + 15) & ~15ull) +
                             sb::kStagePad + sb::kZTablesBytes;  // (+ the Zstd decoder's tables)
@@ -249,8 +270,7 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     } else {
       global.push_back((uint32_t)i);
     }
-    off += m.length;
-    rows += m.num_values;
+    rows = std::max<uint64_t>(rows, pd.row_off + m.num_values);
   }
 
   sb_plan* p = new sb_plan();
@@ -635,7 +655,8 @@ static sb_status nest_launch(sb_ctx* ctx, sb_plan* p, const sb_nested_out* out, 
   L.counts = p->d_nest;
   L.bases = p->d_nest + n * (D + 1);
   L.totals = p->d_nest + 2 * n * (D + 1);
-  L.vpages = p->inner->d_pages;
+  L.vpages = p->inner ? p->inner->d_pages : nullptr;
+  L.vpos = p->d_nest ? (uint32_t*)(p->d_nest + 2 * n * (D + 1) + D + 1) : nullptr;
   if (out) {
     for (uint64_t d = 0; d < D; d++) {
       L.out_offsets[d] = (uint8_t*)out->d_offsets[d];
@@ -651,48 +672,58 @@ static sb_status nest_launch(sb_ctx* ctx, sb_plan* p, const sb_nested_out* out, 
 
 sb_status sb_plan_nested_column(sb_ctx* ctx, const sb_nested_desc* d, const uint8_t* d_chunk, uint64_t chunk_len,
                                 const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out) {
-  if (!ctx || !d || !out) return fail(ctx, SB_E_ARG, "null argument");
+  if (!ctx || !d || !out || (!h_metas && n_pages)) return fail(ctx, SB_E_ARG, "null argument");
+  const int t = d->physical_type;
   bool is_float;
-  if (!type_width(d->physical_type, &is_float) || d->physical_type == SB_T_BOOLEAN)
-    return fail(ctx, SB_E_NYI, "nested leaf type %d not supported", d->physical_type);
+  const bool leaf_bin = t == SB_T_BINARY || t == SB_T_UTF8 || t == SB_T_LARGE_BINARY || t == SB_T_LARGE_UTF8;
+  if (!type_width(t, &is_float) && t != SB_T_BOOLEAN && !leaf_bin)
+    return fail(ctx, SB_E_NYI, "nested leaf type %d not supported", t);
   if (d->depth < 1 || d->depth > SB_MAX_NEST) return fail(ctx, SB_E_NYI, "nesting depth %d not supported", d->depth);
   if (d->offset_width != 4 && d->offset_width != 8) return fail(ctx, SB_E_ARG, "offset width must be 4 or 8");
-  sb_column_desc cd{d->physical_type, 0};
-  sb_plan* inner = nullptr;
-  sb_status st = sb_plan_column(ctx, &cd, d_chunk, chunk_len, h_metas, n_pages, &inner);
-  if (st) return st;
+  if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  std::vector<sb::PageDesc> lpages(n_pages);  // the level pages, back to back
+  uint64_t off = 0;
+  for (uint64_t i = 0; i < n_pages; i++) {
+    if (h_metas[i].length > 0xFFFFFFFFull || h_metas[i].num_values > 0xFFFFFFFFull || off + h_metas[i].length > chunk_len)
+      return fail(ctx, SB_E_ARG, "page %llu: bad size", (unsigned long long)i);
+    lpages[i] = sb::PageDesc{off, 0, (uint32_t)h_metas[i].length, (uint32_t)h_metas[i].num_values, 0};
+    off += h_metas[i].length;
+  }
   sb_plan* p = new sb_plan();
-  p->desc = cd;
+  p->desc = sb_column_desc{t, 0};
   p->nested = true;
   p->ndesc = *d;
-  p->inner = inner;
   p->d_chunk = d_chunk;
   p->chunk_len = chunk_len;
   p->n_pages = n_pages;
-  p->width = inner->width;
   p->is_float = is_float;
   const uint64_t D = (uint64_t)d->depth, np = n_pages ? n_pages : 1;
   hipError_t e = hipMalloc(&p->d_pages, np * sizeof(sb::PageDesc));
   if (e == hipSuccess) e = hipMalloc(&p->d_status, np * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMalloc(&p->d_nest, (2 * np * (D + 1) + D + 1) * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&p->d_nest, (2 * np * (D + 1) + D + 1) * sizeof(uint64_t) + np * sizeof(uint32_t));
   if (e == hipSuccess) e = hipEventCreate(&p->ev0);
   if (e == hipSuccess) e = hipEventCreate(&p->ev1);
-  if (e == hipSuccess && n_pages)  // the level pages (inner's table becomes the values streams)
-    e = hipMemcpyAsync(p->d_pages, inner->d_pages, n_pages * sizeof(sb::PageDesc), hipMemcpyDeviceToDevice, ctx->stream);
+  if (e == hipSuccess && n_pages)
+    e = hipMemcpy(p->d_pages, lpages.data(), n_pages * sizeof(sb::PageDesc), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     sb_plan_destroy(p);
     return fail(ctx, SB_E_DEVICE, "nested plan alloc: %s", hipGetErrorString(e));
   }
   p->nest_totals.assign(D + 1, 0);
-  if (n_pages) {  // count every level once: the caller allocates from the totals, decodes use the bases
+  // count every level once: the caller allocates from the totals, decodes
+  // use the bases; the leaf values streams become the pages of `inner`
+  std::vector<sb::PageDesc> vpages(n_pages);
+  if (n_pages) {
     if (nest_launch(ctx, p, nullptr, 0) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "nested counting failed: %s", hipGetErrorString(hipGetLastError()));
     }
-    std::vector<uint32_t> stv(n_pages);
+    std::vector<uint32_t> stv(n_pages), vpos(n_pages);
     std::vector<uint64_t> cnt(n_pages * (D + 1)), bases(n_pages * (D + 1));
     (void)hipMemcpy(stv.data(), p->d_status, n_pages * 4, hipMemcpyDeviceToHost);
     (void)hipMemcpy(cnt.data(), p->d_nest, cnt.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(vpos.data(), p->d_nest + 2 * n_pages * (D + 1) + D + 1, n_pages * 4, hipMemcpyDeviceToHost);
     for (uint64_t i = 0; i < n_pages; i++) {
       if (stv[i]) {
         sb_plan_destroy(p);
@@ -702,6 +733,8 @@ sb_status sb_plan_nested_column(sb_ctx* ctx, const sb_nested_desc* d, const uint
         bases[i * (D + 1) + k] = p->nest_totals[k];
         p->nest_totals[k] += cnt[i * (D + 1) + k];
       }
+      vpages[i] = sb::PageDesc{lpages[i].byte_off + vpos[i], bases[i * (D + 1) + D], lpages[i].byte_len - vpos[i],
+                               (uint32_t)cnt[i * (D + 1) + D], 0};
     }
     e = hipMemcpy(p->d_nest + n_pages * (D + 1), bases.data(), bases.size() * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_nest + 2 * n_pages * (D + 1), p->nest_totals.data(), (D + 1) * 8,
@@ -711,8 +744,16 @@ sb_status sb_plan_nested_column(sb_ctx* ctx, const sb_nested_desc* d, const uint
       return fail(ctx, SB_E_DEVICE, "nested plan upload: %s", hipGetErrorString(e));
     }
   }
+  const sb_column_desc cd{t, 0};
+  sb_status st = plan_pages(ctx, &cd, d_chunk, chunk_len, std::move(vpages), &p->inner);
+  if (st) {
+    sb_plan_destroy(p);
+    return st;
+  }
+  p->width = p->inner->width;
   p->n_rows = p->nest_totals[0];
   p->n_leaves = p->nest_totals[D];
+  p->values_bytes = p->inner->values_bytes;
   *out = p;
   return SB_OK;
 }
@@ -732,6 +773,7 @@ sb_status sb_decode_nested_planned(sb_ctx* ctx, sb_plan* p, const sb_nested_out*
       return fail(ctx, SB_E_ARG, "validity of level %d is null", d);
   }
   if (p->n_leaves && !out->d_values) return fail(ctx, SB_E_ARG, "values buffer is null");
+  if (p->inner && p->inner->binary && !out->d_leaf_offsets) return fail(ctx, SB_E_ARG, "leaf offsets are null");
   if (p->ndesc.item_nullable && p->n_leaves && !out->d_leaf_validity) return fail(ctx, SB_E_ARG, "leaf validity is null");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
@@ -745,8 +787,14 @@ sb_status sb_decode_nested_planned(sb_ctx* ctx, sb_plan* p, const sb_nested_out*
   } else {
     sb_status lst = nest_launch(ctx, p, out, 1);
     if (lst) return lst;
-    sb_primitive_out vo{out->d_values ? out->d_values : out->d_offsets[0], nullptr};  // (no leaves: nothing written)
-    sb_status st = sb_decode_planned(ctx, p->inner, &vo);
+    sb_status st;
+    if (p->inner->binary) {
+      sb_binary_out bo{out->d_leaf_offsets, (uint8_t*)out->d_values, out->values_capacity, nullptr};
+      st = sb_decode_binary_planned(ctx, p->inner, &bo);
+    } else {
+      sb_primitive_out vo{out->d_values ? out->d_values : out->d_offsets[0], nullptr};  // (no leaves: nothing written)
+      st = sb_decode_planned(ctx, p->inner, &vo);
+    }
     if (st) return st;
   }
   if (p->timing) {

@@ -3507,6 +3507,7 @@ struct NestArgs {
   uint32_t* out_validity[kMaxNest];
   uint32_t* out_leaf_validity;
   uint32_t* status;
+  uint32_t* vpos;
 };
 
 // A window of hybrid runs (parquet2 HybridRleDecoder) over the levels of the
@@ -3684,6 +3685,7 @@ __global__ __launch_bounds__(NT) void k_nest_walk(NestArgs a) {
       uint32_t err = w.err;
       if (!WRITE) {
         for (uint32_t d = 0; d <= D; d++) a.counts[(uint64_t)page * (D + 1) + d] = err ? 0 : carry[d];
+        a.vpos[page] = err ? 0u : w.vpos;
       } else {
         for (uint32_t d = 0; d <= D; d++)
           if (!err && carry[d] != a.counts[(uint64_t)page * (D + 1) + d]) err = ST_OUT_OF_SPEC;
@@ -3809,7 +3811,7 @@ namespace sb {
 int launch_nest(int stage, const NestLaunch& L, void* stream) {
   if (L.n_pages == 0) return 0;
   sbk::NestArgs a{L.chunk, L.pages, L.n_pages, L.depth, L.nullable, L.offset_width, L.counts, L.bases, L.totals,
-                  L.vpages, {}, {}, L.out_leaf_validity, L.status};
+                  L.vpages, {}, {}, L.out_leaf_validity, L.status, L.vpos};
   for (int d = 0; d < kMaxNest; d++) {
     a.out_offsets[d] = L.out_offsets[d];
     a.out_validity[d] = L.out_validity[d];

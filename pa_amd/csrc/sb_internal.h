@@ -189,6 +189,7 @@ struct NestLaunch {
   uint32_t* out_validity[kMaxNest];
   uint32_t* out_leaf_validity;
   uint32_t* status;
+  uint32_t* vpos;          // stage 0 out: each page's values-stream position
 };
 int launch_nest(int stage, const NestLaunch& a, void* stream);
 

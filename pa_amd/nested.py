@@ -19,6 +19,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native as N
+from .binary import BINARY, LARGE_BINARY, LARGE_UTF8, UTF8
 from .read import Context, PageMeta, resolve_context, physical_type, _as_device_bytes
 
 
@@ -200,7 +201,8 @@ class NestedDescC(ctypes.Structure):
 
 class NestedOutC(ctypes.Structure):
     _fields_ = [("d_offsets", ctypes.c_void_p * MAX_NEST), ("d_validity", ctypes.c_void_p * MAX_NEST),
-                ("d_values", ctypes.c_void_p), ("d_leaf_validity", ctypes.c_void_p)]
+                ("d_values", ctypes.c_void_p), ("d_leaf_validity", ctypes.c_void_p), ("d_leaf_offsets", ctypes.c_void_p),
+                ("values_capacity", ctypes.c_uint64)]
 
 
 def _nested_lib():
@@ -214,6 +216,8 @@ def _nested_lib():
         L.sb_plan_nested_count.restype = U64
         L.sb_decode_nested_planned.argtypes = [P, P, ctypes.POINTER(NestedOutC)]
         L.sb_decode_nested_planned.restype = I32
+        L.sb_plan_values_bytes.argtypes = [P]
+        L.sb_plan_values_bytes.restype = U64
         L._nested_ready = True
     return L
 
@@ -222,10 +226,12 @@ class NestedColumnDecoder:
     """A leaf under len(list_nullable) list levels (List<List<T>> ..., level 0
     outermost): read_validity_nested in its general form (read_basic.rs:95-164)
     + create_list per level.  decode() -> (offsets per level, validity per
-    level | None, values, leaf validity | None) device tensors."""
+    level | None, values, leaf validity | None) device tensors; values is a
+    bitmap for a Boolean leaf (dtype bool) and (leaf offsets, value bytes) for
+    a Binary / Utf8 leaf (physical_type=pa_amd.UTF8 ...)."""
 
     def __init__(self, chunk, page_metas: Sequence[PageMeta], dtype, list_nullable, item_nullable: bool,
-                 ctx: Optional[Context] = None, large: bool = False):
+                 ctx: Optional[Context] = None, large: bool = False, physical_type: Optional[int] = None):
         import torch
 
         self._torch = torch
@@ -242,7 +248,9 @@ class NestedColumnDecoder:
         L = _nested_lib()
         metas = (N.PageMetaC * max(1, len(self.metas)))(*[N.PageMetaC(m.length, m.num_values) for m in self.metas])
         ln = (ctypes.c_int32 * MAX_NEST)(*([int(x) for x in self.list_nullable] + [0] * (MAX_NEST - self.depth)))
-        desc = NestedDescC(physical_type(self.dtype), self.depth, ln, int(self.item_nullable), self.offset_width)
+        self.phys = physical_type if physical_type is not None else globals()["physical_type"](self.dtype)
+        self.binary = self.phys in (BINARY, UTF8, LARGE_BINARY, LARGE_UTF8)
+        desc = NestedDescC(self.phys, self.depth, ln, int(self.item_nullable), self.offset_width)
         h = ctypes.c_void_p()
         st = L.sb_plan_nested_column(self.ctx._h, ctypes.byref(desc), ctypes.c_void_p(self.chunk.data_ptr()),
                                      self.chunk.numel(), metas, len(self.metas), ctypes.byref(h))
@@ -250,6 +258,7 @@ class NestedColumnDecoder:
             raise N.StrawboatError(st, self.ctx.error())
         self._h = h
         self.counts = [int(L.sb_plan_nested_count(h, d)) for d in range(self.depth + 1)]
+        self.values_bytes = int(L.sb_plan_values_bytes(h))
 
     def alloc_outputs(self):
         torch = self._torch
@@ -258,9 +267,17 @@ class NestedColumnDecoder:
         bm = lambda n: torch.empty(max((n + 31) // 32, 1) * 4, dtype=torch.uint8, device=dev)  # noqa: E731
         offs = [torch.empty(self.counts[d] + 1, dtype=odt, device=dev) for d in range(self.depth)]
         valid = [bm(self.counts[d]) if self.list_nullable[d] else None for d in range(self.depth)]
-        tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[self.dtype.itemsize]
-        values = torch.empty(max(self.counts[self.depth], 1), dtype=tdt, device=dev)
-        leaf = bm(self.counts[self.depth]) if self.item_nullable else None
+        nleaf = self.counts[self.depth]
+        if self.binary:
+            lo = torch.zeros(nleaf + 1, dtype=torch.int64 if self.phys in (LARGE_BINARY, LARGE_UTF8) else torch.int32,
+                             device=dev)
+            values = (lo, torch.empty(max(self.values_bytes, 16), dtype=torch.uint8, device=dev))
+        elif self.phys == N.BOOLEAN:
+            values = torch.zeros(max((nleaf + 31) // 32, 1) * 4, dtype=torch.uint8, device=dev)
+        else:
+            tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[self.dtype.itemsize]
+            values = torch.empty(max(nleaf, 1), dtype=tdt, device=dev)
+        leaf = bm(nleaf) if self.item_nullable else None
         return offs, valid, values, leaf
 
     def decode(self, outs=None):
@@ -270,7 +287,12 @@ class NestedColumnDecoder:
         for d in range(self.depth):
             o.d_offsets[d] = p(offs[d])
             o.d_validity[d] = p(valid[d])
-        o.d_values = p(values)
+        if self.binary:
+            o.d_leaf_offsets = p(values[0])
+            o.d_values = p(values[1])
+            o.values_capacity = values[1].numel()
+        else:
+            o.d_values = p(values)
         o.d_leaf_validity = p(leaf)
         L = _nested_lib()
         st = L.sb_decode_nested_planned(self.ctx._h, self._h, ctypes.byref(o))

@@ -94,3 +94,70 @@ def test_nested_depths(ctx, tmp_path, depth, codec):
             if leaf_null:
                 assert (pa_amd.read.unpack_bitmap(gf, len(ev)).cpu().numpy() == ef).all()
             dec.close()
+
+
+@pytest.mark.parametrize("leaf", ["utf8", "bool"])
+@pytest.mark.parametrize("depth", [1, 2])
+@pytest.mark.parametrize("codec", ["none", "lz4", "adaptive"])
+def test_nested_utf8_bool_leaves(ctx, tmp_path, leaf, depth, codec):
+    """List<Utf8>, List<Boolean> (and one level deeper): the level walk, then
+    the leaf's values streams through the binary / boolean kernels at their
+    leaf bases, against the oracle's general reader."""
+    import pa_amd
+    from tests.test_pyarrow_nested import bool_stream, leaf_pages, utf8_stream
+
+    opts = O.WriteOptions.make(**CODECS[codec])
+    for nulls in itertools.product([False, True], repeat=depth):
+        for leaf_null in (False, True):
+            rng = np.random.default_rng(7 + depth * 10 + sum(nulls) + 3 * leaf_null)
+
+            def build(level):
+                r = rng.random()
+                if nulls[level] and r < 0.1:
+                    return None
+                if r < 0.2:
+                    return []
+                k = int(rng.integers(1, 5))
+                if level == depth - 1:
+                    if leaf == "utf8":
+                        return [None if leaf_null and rng.random() < 0.15 else str(x) * int(rng.integers(0, 3))
+                                for x in rng.integers(0, 1000, k)]
+                    return [None if leaf_null and rng.random() < 0.15 else bool(x) for x in rng.integers(0, 2, k)]
+                return [build(level + 1) for _ in range(k)]
+
+            f = pa.field("item", pa.utf8() if leaf == "utf8" else pa.bool_(), nullable=leaf_null)
+            for level in reversed(range(depth)):
+                f = pa.field("item" if level else "c", pa.list_(f), nullable=nulls[level])
+            t = pa.table({"c": pa.array([build(0) for _ in range(3000)], type=f.type)}, schema=pa.schema([f]))
+            path = str(tmp_path / "u.parquet")
+            pq.write_table(t, path, data_page_version="2.0", compression="NONE", use_dictionary=False,
+                           data_page_size=4096, write_statistics=False)
+            leaf_def = sum(int(x) + 1 for x in nulls)
+            max_def = leaf_def + int(leaf_null)
+            if leaf == "utf8":
+                enc = lambda sd, pl, e: utf8_stream(sd, pl, max_def, opts)  # noqa: E731
+            else:
+                enc = lambda sd, pl, e: bool_stream(sd, pl, max_def, opts, encoding=e)  # noqa: E731
+            chunk, metas = leaf_pages(data_pages_v2(path, True), max_def, leaf_def, enc)
+            eo, eb, ev, ef = O.read_nested_column(chunk, metas, np.uint8, nulls, leaf_null,
+                                                  leaf="binary" if leaf == "utf8" else "bool")
+            pm = [pa_amd.PageMeta(l, m) for l, m in metas]
+            if leaf == "utf8":
+                dec = pa_amd.NestedColumnDecoder(chunk, pm, np.uint8, nulls, leaf_null, ctx, physical_type=pa_amd.UTF8)
+            else:
+                dec = pa_amd.NestedColumnDecoder(chunk, pm, np.bool_, nulls, leaf_null, ctx)
+            go, gb, gv, gf = dec.decode()
+            for d in range(depth):
+                assert (go[d].cpu().numpy().astype(np.int64) == eo[d]).all(), (nulls, leaf_null, d)
+                if nulls[d]:
+                    assert (pa_amd.read.unpack_bitmap(gb[d], len(eo[d]) - 1).cpu().numpy() == eb[d]).all()
+            nleaf = len(eo[-1]) and int(eo[-1][-1])
+            if leaf == "utf8":
+                lo, vb = gv
+                assert (lo.cpu().numpy().astype(np.int64) == ev[0]).all()
+                assert vb.cpu().numpy()[:len(ev[1])].tobytes() == ev[1]
+            else:
+                assert (pa_amd.read.unpack_bitmap(gv, nleaf).cpu().numpy() == ev).all()
+            if leaf_null:
+                assert (pa_amd.read.unpack_bitmap(gf, nleaf).cpu().numpy() == ef).all()
+            dec.close()
