@@ -8,7 +8,6 @@
 
 #include <cstdarg>
 #include <cstdio>
-#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -82,9 +81,6 @@ struct sb_plan {
   sb_list_desc ldesc{};
   uint8_t* d_lc = nullptr;  // list state, see list_state_bytes
   bool list_peek = false;   // sizes from the page headers (checked against the levels at plan time)
-  sb::ListStepDesc* d_lsteps = nullptr;  // one per step (lsteps_page: one per page)
-  bool lsteps_page = getenv("SB_LIST_PAGE") != nullptr;  // (experiment switch)
-  uint32_t n_lsteps = 0;
   sb_plan* inner = nullptr;
   uint64_t n_leaves = 0;
   int offset_width = 0;
@@ -206,7 +202,6 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_bin) (void)hipFree(p->d_bin);
   if (p->d_lc) (void)hipFree(p->d_lc);
   if (p->d_nest) (void)hipFree(p->d_nest);
-  if (p->d_lsteps) (void)hipFree(p->d_lsteps);
   if (p->inner) sb_plan_destroy(p->inner);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
@@ -548,11 +543,6 @@ static sb_status list_launch(sb_ctx* ctx, sb_plan* p, const sb_list_out* out, in
                    out ? (uint32_t*)out->d_leaf_validity : nullptr, p->d_status};
   if (out && p->ldesc.list_nullable) L.zw_list = (p->n_rows + 31) / 32;
   if (out && p->ldesc.item_nullable) L.zw_leaf = (p->n_leaves + 31) / 32;
-  if (peek && p->d_lsteps) {
-    L.steps = p->d_lsteps;
-    L.n_steps = p->n_lsteps;
-    L.page_mode = p->lsteps_page ? 1u : 0u;
-  }
   if (sb::launch_list(stage, L, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "list launch failed: %s", hipGetErrorString(hipGetLastError()));
   return SB_OK;
@@ -617,28 +607,6 @@ sb_status sb_plan_list_column(sb_ctx* ctx, const sb_list_desc* d, const uint8_t*
     (void)hipMemcpy(peek.data(), p->d_lc, n_pages * 8, hipMemcpyDeviceToHost);
     p->list_peek = peek == exact;
     if (!p->list_peek) (void)hipMemcpy(p->d_lc, exact.data(), n_pages * 8, hipMemcpyHostToDevice);
-    // Pages of the writer's shape (one bit-packed run per level stream, def
-    // width <= 2: the exact pass's fast flag) are walked one wave per step.
-    std::vector<uint32_t> lvd(8 * n_pages);
-    (void)hipMemcpy(lvd.data(), (uint64_t*)p->d_lc + 3 * n_pages + 2 * list_nblk(n_pages) + 2, lvd.size() * 4,
-                    hipMemcpyDeviceToHost);
-    bool fast = p->list_peek;
-    for (uint64_t i = 0; i < n_pages && fast; i++) fast = (lvd[8 * i + 3] & 1) && lvd[8 * i + 5];
-    std::vector<sb::PageDesc> hp(n_pages);
-    if (fast) (void)hipMemcpy(hp.data(), p->d_pages, n_pages * sizeof(sb::PageDesc), hipMemcpyDeviceToHost);
-    std::vector<sb::ListStepDesc> steps;
-    for (uint64_t i = 0; i < n_pages && fast; i++) {
-      const uint32_t ns = std::max<uint32_t>(1, (hp[i].num_values + sb::kListStep - 1) / sb::kListStep);
-      const uint32_t* d = &lvd[8 * i];  // (rows, vpos, rep payload, fast | bw << 1), (def payload, ok, -, -)
-      for (uint32_t k = 0; k < (p->lsteps_page ? 1u : ns); k++)
-        steps.push_back(sb::ListStepDesc{hp[i].byte_off, (uint32_t)i, k << 2 | (d[3] >> 1), d[2], d[4], d[0],
-                                         hp[i].num_values});
-    }
-    if (getenv("SB_LIST_OLD")) fast = false;  // (experiment switch)
-    if (fast && hipMalloc(&p->d_lsteps, steps.size() * sizeof(sb::ListStepDesc)) == hipSuccess) {
-      (void)hipMemcpy(p->d_lsteps, steps.data(), steps.size() * sizeof(sb::ListStepDesc), hipMemcpyHostToDevice);
-      p->n_lsteps = (uint32_t)steps.size();
-    }
   }
   *out = p;
   return SB_OK;
@@ -658,9 +626,10 @@ sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* p, const sb_list_out* out
     HIP_TRY(ctx, hipMemsetAsync(out->d_offsets, 0, (size_t)p->ldesc.offset_width, ctx->stream));
   } else {
     // sizes (exact pass, or the headers), global bases + zeroed bitmaps, the
-    // levels walk, then the values streams at their leaf bases.  (Running the
-    // values decode beside the walk on a second stream was measured slower on
-    // C4: 242 vs 214 us, the two kernels contend for the same CUs.)
+    // levels walk, then the values streams at their leaf bases.  (Measured
+    // on C4 and not kept: the values decode beside the walk on a second
+    // stream, 242 vs 214 us, the kernels contend for the same CUs; a walk
+    // with one wave per 2048-level step, 113-119 vs 108 us.)
     sb_status lst = p->list_peek ? SB_OK : list_launch(ctx, p, out, 0, false);
     if (!lst) lst = list_launch(ctx, p, out, 1, p->list_peek);
     if (!lst) lst = list_launch(ctx, p, out, 3, p->list_peek);

@@ -3019,8 +3019,6 @@ struct ListArgs {
   uint32_t* out_leaf_validity;
   uint32_t* status;
   uint64_t zw_list, zw_leaf;  // k_list_vbase: bitmap words to zero
-  const ListStepDesc* steps;  // k_list_steps: every kLvStep-level step (page_mode: every page's first)
-  uint32_t n_steps, page_mode;
 };
 
 // Header + run tables (one lane).
@@ -3171,7 +3169,6 @@ __device__ __forceinline__ void wave_put_bits(const uint32_t* bm, uint32_t n, ui
 
 constexpr uint32_t kLvStage = 4160;      // page bytes staged per wave (header + level streams)
 constexpr uint32_t kLvStep = 64 * kLvK;  // levels per wave step (2048)
-static_assert(kLvStep == kListStep, "the host's step table uses the walk's step");
 
 struct ListWave {
   ListShared ls;
@@ -3484,7 +3481,6 @@ __global__ __launch_bounds__(NT) void k_list_vbase(ListArgs a) {
       a.local[2 * p] = rbase;
       a.local[2 * p + 1] = lbase;
       if (a.peek) {
-        a.status[p] = 0;  // k_list_steps only max-merges errors
         const PageDesc pd = a.pages[p];
         const GlbSrc g{a.chunk + pd.byte_off};
         const uint64_t vpos = pd.byte_len >= 12 ? 12ull + g.u32(4) + g.u32(8) : ~0ull;
@@ -3552,297 +3548,6 @@ __global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
       }
     }
     wave_sync();
-  }
-}
-
-// Levels pass over steps: one wave per kLvStep-level step of a page (plans
-// whose pages all have the writer's shape -- one bit-packed run per level
-// stream, def width <= 2 -- and header sizes).  A step's row / leaf carries
-// are the popcounts of its page's earlier steps, recounted by the wave from
-// the level streams (every earlier step is whole, so no tail masks), so the
-// steps of a page run in parallel instead of one wave walking the page.
-// Level bytes come from HBM with branch-free loads issued together (no
-// staging): a writer-shaped page's level streams are followed inside the
-// page by the values header (>= 9 bytes, checked by the header sizing), so a
-// lane's 4 + 8 byte reads never leave the page.  The page's terminal step --
-// the one that reaches its last row, else its last step -- checks the
-// consumed rows / leaves against the sizes; errors are max-merged into the
-// status k_list_vbase zeroed.
-struct ListStepWave {
-  alignas(16) uint16_t obuf[4 * 9 * 64];  // >= kLvStep + 8: nine quads a lane, every read in bounds
-  uint32_t lbits[kLvStep / 32 + 4];
-  uint32_t fbits[kLvStep / 32 + 4];
-};
-
-// Offsets of the rows starting in a nibble of levels: entry k of (rsm nibble
-// << 4 | leaf nibble) = the leaves before the nibble's k-th row start.
-__device__ __forceinline__ uint2 nib_entry(uint32_t idx) {
-  const uint32_t r4 = idx >> 4, f4 = idx & 15;
-  uint32_t e[4] = {0, 0, 0, 0}, k = 0;
-  for (uint32_t b = 0; b < 4; b++)
-    if (r4 >> b & 1) e[k++] = __popc(f4 & ((1u << b) - 1));
-  return make_uint2(e[0] | e[1] << 16, e[2] | e[3] << 16);
-}
-
-// 32 bits at byte p (any alignment), from the aligned words around it.
-__device__ __forceinline__ uint32_t ld_any32(const uint8_t* p) {
-  const uint32_t* q = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
-  return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)((uintptr_t)p & 3));
-}
-
-// Even bits of x to the low half, odd bits to the high half (Hacker's
-// Delight 7-2 unshuffle).
-__device__ __forceinline__ uint32_t unshuffle32(uint32_t x) {
-  uint32_t t;
-  t = (x ^ (x >> 1)) & 0x22222222u; x = x ^ t ^ (t << 1);
-  t = (x ^ (x >> 2)) & 0x0C0C0C0Cu; x = x ^ t ^ (t << 2);
-  t = (x ^ (x >> 4)) & 0x00F000F0u; x = x ^ t ^ (t << 4);
-  t = (x ^ (x >> 8)) & 0x0000FF00u; x = x ^ t ^ (t << 8);
-  return x;
-}
-
-__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
-  return __builtin_amdgcn_readlane(wave_incl_scan(v), 63);
-}
-
-// Levels (def >= t) among the 32 levels of a lane whose def bits are (d0, d1):
-// a count over whole 2-bit (bw 2) or 1-bit (bw 1) fields.
-__device__ __forceinline__ uint32_t ge_count(uint32_t d0, uint32_t d1, uint32_t bw, uint32_t t) {
-  if (t == 0) return 32;
-  if (bw == 1) return t == 1 ? __popc(d0) : 0u;
-  constexpr uint32_t E = 0x55555555u;
-  if (t == 1) return __popc((d0 | d0 >> 1) & E) + __popc((d1 | d1 >> 1) & E);
-  if (t == 2) return __popc(d0 & ~E) + __popc(d1 & ~E);
-  return __popc(d0 & d0 >> 1 & E) + __popc(d1 & d1 >> 1 & E);
-}
-
-#ifndef SB_LS_WAVES
-#define SB_LS_WAVES 4
-#endif
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SB_LS_WAVES))) void k_list_steps(ListArgs a) {
-  __shared__ ListStepWave waves[NW];
-  __shared__ uint2 nib[256];
-  __shared__ uint8_t pext4[256];  // [v << 4 | m]: the bits of v at m's set positions, packed low
-  nib[threadIdx.x] = nib_entry(threadIdx.x);
-  {
-    const uint32_t v = threadIdx.x >> 4, m = threadIdx.x & 15;
-    uint32_t r = 0, k = 0;
-    for (uint32_t b = 0; b < 4; b++)
-      if (m >> b & 1) r |= (v >> b & 1) << k++;
-    pext4[threadIdx.x] = (uint8_t)r;
-  }
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63;
-  ListStepWave& w = waves[threadIdx.x >> 6];
-  const uint32_t cs1 = a.nl + 1;
-  for (uint32_t it = blockIdx.x * NW + (threadIdx.x >> 6); it < a.n_steps; it += gridDim.x * NW) {
-    const ListStepDesc sd = a.steps[it];
-    const uint32_t page = sd.page, t0s = (sd.step_bw >> 2) * kLvStep, bw = sd.step_bw & 3;
-    const uint32_t rows = sd.rows, L = sd.levels;
-    const uint8_t* pr = a.chunk + sd.byte_off + sd.rp;  // rep payload
-    const uint8_t* pf = a.chunk + sd.byte_off + sd.dp;  // def payload
-    // every load the step needs, issued together: its bases and sizes, its
-    // level bits, the earlier steps' level bits
-    const uint64_t rbase = a.local[2 * page], lbase = a.local[2 * page + 1], cnt = a.counts[page];
-    const uint32_t i0s = t0s + lane * kLvK, i0c = i0s < L ? i0s : 0u;  // (lanes past the levels read level 0, masked below)
-    uint32_t rw = ld_any32(pr + i0c / 8), dlo = ld_any32(pf + i0c * bw / 8), dhi = bw == 2 ? ld_any32(pf + i0c / 4 + 4) : 0u;
-    // earlier steps, four at a time: all loads first (clamped to step 0 past
-    // t0, their counts masked), then the popcounts
-    uint32_t cr = 0, cl = 0;
-#ifdef SB_V_ST_NOCARRY
-    for (uint32_t q0 = 0; q0 < 0; q0 += 4 * kLvStep) {
-#else
-    for (uint32_t q0 = 0; q0 < t0s; q0 += 4 * kLvStep) {
-#endif
-      uint32_t r[4], x0[4], x1[4];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t q = q0 + k * kLvStep, qc = (q < t0s ? q : 0u) + lane * kLvK;
-        r[k] = ld_any32(pr + qc / 8);
-        x0[k] = ld_any32(pf + qc * bw / 8);
-        x1[k] = bw == 2 ? ld_any32(pf + qc / 4 + 4) : 0u;
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) {
-        const bool in = q0 + k * kLvStep < t0s;
-        cr += in ? __popc(~r[k]) : 0u;
-        cl += in ? ge_count(x0[k], x1[k], bw, cs1) : 0u;
-      }
-    }
-    uint32_t carry_r = t0s ? wave_total(cr) : 0u, carry_l = t0s ? wave_total(cl) : 0u;
-    // page mode: this wave walks every step of the page, the next step's
-    // level bits loaded while the current one is processed
-    const uint32_t t_end = a.page_mode ? max(L, 1u) : t0s + 1;
-    for (uint32_t t0 = t0s; t0 < t_end; t0 += kLvStep) {
-    if (carry_r > rows) break;  // past the page's last row (uniform)
-    const uint32_t i0 = t0 + lane * kLvK, t1 = t0 + kLvStep;
-    uint32_t nrw = 0, ndlo = 0, ndhi = 0;
-    if (t1 < t_end) {
-      const uint32_t i1 = t1 + lane * kLvK, i1c = i1 < L ? i1 : 0u;
-      nrw = ld_any32(pr + i1c / 8);
-      ndlo = ld_any32(pf + i1c * bw / 8);
-      ndhi = bw == 2 ? ld_any32(pf + i1c / 4 + 4) : 0u;
-    }
-    // masks of this lane's 32 levels
-    const uint32_t vm = i0 >= L ? 0u : L - i0 >= 32 ? 0xFFFFFFFFu : ((1u << (L - i0)) - 1);
-    uint32_t lo, hi;
-    if (bw == 2) {
-      const uint32_t ua = unshuffle32(dlo), ub = unshuffle32(dhi);
-      lo = __builtin_amdgcn_perm(ub, ua, 0x05040100u);
-      hi = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
-    } else {
-      lo = dlo;
-      hi = 0;
-    }
-    auto ge = [&](uint32_t t) -> uint32_t { return t == 0 ? 0xFFFFFFFFu : t == 1 ? (lo | hi) : t == 2 ? hi : (hi & lo); };
-    const uint32_t m_rsm = ~rw & vm, m_lfm = ge(cs1) & vm, m_lvm = ge(1) & vm, m_fvm = ge(cs1 + 1) & vm;
-    uint32_t err = (t0 == 0 && lane == 0 && L > 0 && !(m_rsm & 1)) ? (uint32_t)ST_OUT_OF_SPEC : 0u;  // level 0 starts no row
-    // row / leaf positions of this lane's levels
-    const uint32_t pk = ((uint32_t)__popc(m_rsm) << 16) | (uint32_t)__popc(m_lfm);
-    const uint32_t incl = wave_incl_scan(pk), tot = __builtin_amdgcn_readlane(incl, 63), ex = incl - pk;
-    const uint32_t rb = carry_r + (ex >> 16), lb = carry_l + (ex & 0xFFFFu);
-    uint32_t cm = vm;
-    if (rb + __popc(m_rsm) > rows) {
-      if (rb >= rows + 1) cm = 0;
-      else {  // cut at the (rows - rb + 1)-th row start
-        uint32_t x = m_rsm;
-        for (uint32_t k = rows - rb; k; k--) x &= x - 1;
-        cm = (x & (0u - x)) - 1;
-      }
-    }
-    const uint32_t rsm = m_rsm & cm, lfm = m_lfm & cm;
-    const uint64_t g0 = rbase + carry_r, v0 = lbase + carry_l;
-    const uint32_t al = a.ow == 4 ? (uint32_t)(g0 & 3) : (uint32_t)(g0 & 1);  // obuf index of row 0
-    for (uint32_t i = lane; i < kLvStep / 32 + 4; i += 64) w.lbits[i] = w.fbits[i] = 0;
-    const uint32_t nr = __popc(rsm), nf = __popc(lfm);
-    const uint32_t j0 = al + (rb - carry_r), lrel = lb - carry_l;
-    // offsets (step-relative leaf counts) of the lane's rows, a nibble at a
-    // time from the table; the entries a nibble writes past its rows are
-    // overwritten by the lane's later nibbles, and the (<= 4) that spill into
-    // the next lanes' first rows are rewritten below
-    // (with the validity bits of the rows and leaves, packed by pext4); the
-    // table reads are issued first, then the writes
-    uint16_t* ob = w.obuf;
-    uint2 ne[8];
-    uint32_t pl[8], pf4[8];
-#pragma unroll
-    for (uint32_t n = 0; n < 8; n++) {
-      const uint32_t r4 = (rsm >> (4 * n)) & 15u, f4 = (lfm >> (4 * n)) & 15u;
-      ne[n] = nib[r4 << 4 | f4];
-      pl[n] = pext4[((m_lvm >> (4 * n)) & 15u) << 4 | r4];
-      pf4[n] = pext4[((m_fvm >> (4 * n)) & 15u) << 4 | f4];
-    }
-    uint32_t j = j0, base = lrel, vl = 0, vf = 0;
-#ifndef SB_V_ST_NONIB
-#pragma unroll
-    for (uint32_t n = 0; n < 8; n++) {
-#else
-    for (uint32_t n = 0; n < 0; n++) {
-#endif
-      const uint32_t r4 = (rsm >> (4 * n)) & 15u, f4 = (lfm >> (4 * n)) & 15u;
-      vl |= pl[n] << (j - j0);
-      vf |= pf4[n] << (base - lrel);
-      const uint32_t b2 = base * 0x10001u;
-      const uint32_t x = ne[n].x + b2, y = ne[n].y + b2;  // entries < 2^16: no carry between halves
-#ifdef SB_V_ST_MASKW
-      const uint32_t c4 = __popc(r4);
-      if (c4 > 0) ob[j] = (uint16_t)x;
-      if (c4 > 1) ob[j + 1] = (uint16_t)(x >> 16);
-      if (c4 > 2) ob[j + 2] = (uint16_t)y;
-      if (c4 > 3) ob[j + 3] = (uint16_t)(y >> 16);
-#else
-      ob[j] = (uint16_t)x;
-      ob[j + 1] = (uint16_t)(x >> 16);
-      ob[j + 2] = (uint16_t)y;
-      ob[j + 3] = (uint16_t)(y >> 16);
-#endif
-      j += __popc(r4);
-      base += __popc(f4);
-    }
-    wave_sync();
-#ifndef SB_V_ST_MASKW
-    {
-      uint32_t x = rsm;
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) {
-        if (x) {
-          const uint32_t low = x & (0u - x);
-          ob[j0 + k] = (uint16_t)(lrel + __popc(lfm & (low - 1)));
-          x &= x - 1;
-        }
-      }
-    }
-#endif
-    wave_sync();
-    if (a.nl) lds_or_bits(w.lbits + 1, rb - carry_r, vl, nr);
-    if (a.ni) lds_or_bits(w.fbits + 1, lrel, vf, nf);
-    const uint32_t ctot = wave_total((nr << 16) | nf);
-    const uint32_t tr = ctot >> 16, tl = ctot & 0xFFFFu;
-    wave_sync();
-#ifdef SB_V_ST_NOOFF
-    if (a.ow == 0) {
-    } else if (a.ow == 1) {
-#else
-    if (a.ow == 4) {  // quads of rows on 16-byte boundaries: obuf[4q .. 4q + 3] -> o[4q - al ..]
-#endif
-      uint32_t* o = (uint32_t*)a.out_offsets + (g0 - al);
-      const uint32_t v32 = (uint32_t)v0, nq = (al + tr + 3) >> 2;
-      for (uint32_t q = lane; q < nq; q += 64) {
-        const uint2 pq = *(const uint2*)(w.obuf + 4 * q);
-        const uint32_t e0 = v32 + (pq.x & 0xFFFFu), e1 = v32 + (pq.x >> 16), e2 = v32 + (pq.y & 0xFFFFu),
-                       e3 = v32 + (pq.y >> 16);
-        const uint32_t q0 = 4 * q;
-        if (q0 >= al && q0 + 4 <= al + tr) {
-          st_out((u32x4*)(o + q0), u32x4{e0, e1, e2, e3});
-        } else {
-          const uint32_t e[4] = {e0, e1, e2, e3};
-#pragma unroll
-          for (uint32_t k = 0; k < 4; k++)
-            if (q0 + k >= al && q0 + k < al + tr) o[q0 + k] = e[k];
-        }
-      }
-#ifdef SB_V_ST_NOOFF
-    } else if (a.ow == 2) {
-#else
-    } else {
-#endif
-      uint64_t* o = (uint64_t*)a.out_offsets + (g0 - al);
-      const uint32_t nq = (al + tr + 1) >> 1;
-      for (uint32_t q = lane; q < nq; q += 64) {
-        const uint32_t q0 = 2 * q;
-        const uint64_t x0 = v0 + w.obuf[q0], x1 = v0 + w.obuf[q0 + 1];
-        if (q0 >= al && q0 + 2 <= al + tr) {
-          st_out((u32x4*)(o + q0), u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)});
-        } else {
-          if (q0 >= al && q0 < al + tr) o[q0] = x0;
-          if (q0 + 1 >= al && q0 + 1 < al + tr) o[q0 + 1] = x1;
-        }
-      }
-    }
-#ifndef SB_V_ST_NOBITS
-    if (a.nl) wave_put_bits(w.lbits + 1, tr, g0, a.out_list_validity);
-    if (a.ni) wave_put_bits(w.fbits + 1, tl, v0, a.out_leaf_validity);
-#endif
-    // terminal step: the consumed rows / leaves against the sizes
-    const uint32_t sr = tot >> 16;
-    if (carry_r + sr > rows || t0 + kLvStep >= L) {
-      const uint32_t rc = min(carry_r + sr, rows), lc = carry_l + tl;
-      if (lane == 0 && (rc != rows || rc != (uint32_t)(cnt >> 32) || lc != (uint32_t)cnt)) err = ST_OUT_OF_SPEC;
-      if (lane == 0 && page == a.n_pages - 1) {
-        const uint64_t tr2 = rbase + (cnt >> 32), tl2 = lbase + (uint32_t)cnt;
-        a.totals[0] = tr2;
-        a.totals[1] = tl2;
-        if (a.out_offsets) bin_put_off(a.out_offsets, tr2, tl2, a.ow);  // create_list appends values.len()
-      }
-    }
-    if (lane == 0 && err) atomicMax(&a.status[page], err);
-    wave_sync();
-    carry_r += tot >> 16;
-    carry_l += tot & 0xFFFFu;
-    rw = nrw;
-    dlo = ndlo;
-    dhi = ndhi;
-    }
   }
 }
 
@@ -4153,7 +3858,7 @@ namespace sb {
 int launch_list(int stage, const ListLaunch& L, void* stream) {
   sbk::ListArgs a{L.chunk, L.pages, L.n_pages, L.list_nullable, L.item_nullable, L.offset_width, L.width, L.peek,
                   L.counts, L.local, L.blk, L.totals, (uint4*)L.lvdesc, L.vpages, L.out_offsets, L.out_list_validity,
-                  L.out_leaf_validity, L.status, L.zw_list, L.zw_leaf, L.steps, L.n_steps, L.page_mode};
+                  L.out_leaf_validity, L.status, L.zw_list, L.zw_leaf};
   if (L.n_pages == 0) return 0;
   const uint32_t grid = std::min<uint32_t>((L.n_pages + sbk::NW - 1) / sbk::NW, kListGrid);
   const uint32_t nblk = (L.n_pages + sbk::NT - 1) / sbk::NT;
@@ -4166,9 +3871,6 @@ int launch_list(int stage, const ListLaunch& L, void* stream) {
     const uint64_t zw = std::max(L.zw_list, L.zw_leaf);
     const uint32_t zg = (uint32_t)std::min<uint64_t>((zw / 4 + sbk::NT - 1) / sbk::NT, 1024);
     hipLaunchKernelGGL(sbk::k_list_vbase, dim3(std::max(nblk, zg)), dim3(sbk::NT), 0, st, a);
-  } else if (L.steps) {  // one wave per step
-    const uint32_t sgrid = std::min<uint32_t>((L.n_steps + sbk::NW - 1) / sbk::NW, 65535u);
-    hipLaunchKernelGGL(sbk::k_list_steps, dim3(sgrid), dim3(sbk::NT), 0, st, a);
   } else {
     hipLaunchKernelGGL(sbk::k_list_levels, dim3(grid), dim3(sbk::NT), 0, st, a);
   }

@@ -166,22 +166,8 @@ struct ListLaunch {
   uint32_t* out_leaf_validity;
   uint32_t* status;
   uint64_t zw_list, zw_leaf;  // stage 3: validity bitmap words to zero (0: none)
-  const struct ListStepDesc* steps;  // stage 2: one wave per step (k_list_steps); null: a wave per page
-  uint32_t n_steps, page_mode;        // page_mode: steps[] holds each page's first step, one wave walks the page
 };
-// A kListStep-level step of a writer-shaped List page (one bit-packed run
-// per level stream), from the plan's header parse: the walk reads nothing
-// else before the step's level bits.
-struct ListStepDesc {
-  uint64_t byte_off;  // the page
-  uint32_t page;
-  uint32_t step_bw;   // step << 2 | def bit width
-  uint32_t rp, dp;    // rep / def payload offsets in the page
-  uint32_t rows, levels;
-};
-static_assert(sizeof(ListStepDesc) == 32, "step descriptor is 32 bytes");
 constexpr uint32_t kListGrid = 2048;
-constexpr uint32_t kListStep = 2048;  // levels per wave step of the levels walk (k_list_steps items)
 int launch_list(int stage, const ListLaunch& a, void* stream);
 
 // A leaf under depth (1..4) list levels, the general level walk
