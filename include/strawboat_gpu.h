@@ -354,6 +354,54 @@ sb_status sb_write_footer(const uint8_t* h_schema, uint64_t schema_len, const ui
                           uint8_t** h_out, uint64_t* out_len);
 void sb_free(void* p);
 
+/* ---- file reader: footer, schema, file -> HBM staging ------------------- */
+/* One leaf of the schema in arrow2's to_leaves order (write/common.rs:68),
+ * i.e. the order of the file's columns: its logical type (the IPC Schema.fbs
+ * Type union tag), the reader's physical type (0 when no page path exists,
+ * e.g. Decimal, Float16), and the list levels above it. */
+#define SB_LEAF_STRUCT 1u          /* a Struct lies on the path (not decoded here) */
+#define SB_LEAF_MAP 2u             /* a Map lies on the path (not decoded here) */
+#define SB_LEAF_FIXED_SIZE_LIST 4u /* a FixedSizeList lies on the path (not decoded here) */
+#define SB_LEAF_UNION 8u           /* a Union lies on the path (not decoded here) */
+#define SB_LEAF_TOO_DEEP 16u       /* more than SB_MAX_NEST list levels */
+typedef struct {
+  char name[64];                      /* the leaf field's name (truncated) */
+  int32_t arrow_type;                 /* Schema.fbs Type tag: Int 2, FloatingPoint 3, Binary 4, Utf8 5, Bool 6, ... */
+  int32_t physical_type;              /* sb_physical_type, 0 = none */
+  int32_t nullable;                   /* the leaf field's nullable flag */
+  int32_t depth;                      /* list levels above the leaf */
+  int32_t list_nullable[SB_MAX_NEST]; /* per list level, outermost first */
+  int32_t large_list[SB_MAX_NEST];    /* LargeList (i64 offsets) per level */
+  uint32_t flags;                     /* SB_LEAF_* */
+  int32_t top_field;                  /* index of the top-level field it belongs to */
+} sb_leaf_info;
+
+/* infer_schema (read/reader.rs:227-241) + arrow2 deserialize_schema: the
+ * footer's schema bytes (an IPC Message flatbuffer, or an encapsulated
+ * message with its FF FF FF FF prefix) -> leaves.  Host only. */
+sb_status sb_parse_schema(const uint8_t* h_bytes, uint64_t len, sb_leaf_info* h_leaves, uint64_t cap,
+                          uint64_t* n_leaves, uint64_t* n_fields);
+
+typedef struct sb_file sb_file;
+/* read_meta / read_meta_async (reader.rs:168-225): opens the file and reads
+ * its footer with one 64 KiB pre-read of the tail (DEFAULT_FOOTER_SIZE),
+ * reading again only when the footer is larger.  Host only. */
+sb_status sb_file_open(const char* path, sb_file** out);
+void sb_file_close(sb_file* f);
+const char* sb_file_last_error(const sb_file* f);
+uint64_t sb_file_num_columns(const sb_file* f);
+/* ColumnMeta of leaf column `col`: its offset, chunk bytes, page metas (owned by f). */
+sb_status sb_file_column(const sb_file* f, uint64_t col, uint64_t* offset, uint64_t* chunk_len, uint64_t* n_pages,
+                         const sb_page_meta** h_pages);
+sb_status sb_file_schema(const sb_file* f, const uint8_t** h_bytes, uint64_t* len);
+/* The NativeReader page source (reader.rs:60-131) as one staged copy: file
+ * bytes [offset, offset + len) -> d_dst through the device's two pinned 16 MiB buffers
+ * (parallel pread of chunk k+1 overlaps the DMA of chunk k on the device's
+ * copy stream).  The context's stream waits for the copy, so decodes issued
+ * on it afterwards read the bytes; the call returns once the last chunk is
+ * read and queued, so the next column's upload overlaps this one's decode. */
+sb_status sb_file_upload(sb_ctx* ctx, sb_file* f, uint64_t offset, uint64_t len, void* d_dst);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,7 +13,7 @@ from .read import (  # noqa: F401
     read_meta,
     unpack_bitmap,
 )
-from .write import NativeWriter, WriteOptions, encode_column, encode_column_device, encode_page, page_seed  # noqa: F401,E402
+from .write import NativeWriter, WriteOptions, assemble_file, encode_column, encode_column_device, encode_page, page_seed  # noqa: F401,E402
 from .shard import (Shard, exclusive_bases, gather_sizes, rebase_offsets, shard_base, shard_pages,  # noqa: F401,E402
                     shard_slice)
 from .binary import (  # noqa: F401,E402
@@ -21,3 +21,4 @@ from .binary import (  # noqa: F401,E402
     encode_binary_column_device,
 )
 from .nested import ListColumnDecoder, NestedColumnDecoder, batch_read_list, encode_list_column  # noqa: F401,E402
+from .file import Leaf, StrawboatFile, parse_schema  # noqa: F401,E402

@@ -29,8 +29,11 @@ EXPORTED = [
     "sb_encode_list_column", "sb_plan_list_column", "sb_plan_num_leaves", "sb_decode_list_planned",
     "sb_encode_device_bound", "sb_encode_column_device", "sb_lz4_compress_host", "sb_snappy_compress_host",
     "sb_encode_binary_device_bound", "sb_encode_binary_column_device", "sb_plan_nested_column",
-    "sb_plan_nested_count", "sb_decode_nested_planned",
+    "sb_plan_nested_count", "sb_decode_nested_planned", "sb_parse_schema", "sb_file_open", "sb_file_close",
+    "sb_file_last_error", "sb_file_num_columns", "sb_file_column", "sb_file_schema", "sb_file_upload",
 ]
+
+MAX_NEST = 4
 
 
 class StrawboatError(RuntimeError):
@@ -58,6 +61,13 @@ class WriteOptionsC(ctypes.Structure):
         ("forced_codec", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
     ]
+
+
+class LeafInfoC(ctypes.Structure):
+    """sb_leaf_info"""
+    _fields_ = [("name", ctypes.c_char * 64), ("arrow_type", ctypes.c_int32), ("physical_type", ctypes.c_int32),
+                ("nullable", ctypes.c_int32), ("depth", ctypes.c_int32), ("list_nullable", ctypes.c_int32 * MAX_NEST),
+                ("large_list", ctypes.c_int32 * MAX_NEST), ("flags", ctypes.c_uint32), ("top_field", ctypes.c_int32)]
 
 
 class PrimitiveOutC(ctypes.Structure):
@@ -139,5 +149,22 @@ def lib():
     L.sb_write_footer.restype = I32
     L.sb_free.argtypes = [P]
     L.sb_free.restype = None
+    L.sb_parse_schema.argtypes = [P, U64, ctypes.POINTER(LeafInfoC), U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]
+    L.sb_parse_schema.restype = I32
+    L.sb_file_open.argtypes = [ctypes.c_char_p, PP]
+    L.sb_file_open.restype = I32
+    L.sb_file_close.argtypes = [P]
+    L.sb_file_close.restype = None
+    L.sb_file_last_error.argtypes = [P]
+    L.sb_file_last_error.restype = ctypes.c_char_p
+    L.sb_file_num_columns.argtypes = [P]
+    L.sb_file_num_columns.restype = U64
+    L.sb_file_column.argtypes = [P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64),
+                                 ctypes.POINTER(ctypes.POINTER(PageMetaC))]
+    L.sb_file_column.restype = I32
+    L.sb_file_schema.argtypes = [P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(U64)]
+    L.sb_file_schema.restype = I32
+    L.sb_file_upload.argtypes = [P, P, U64, U64, P]
+    L.sb_file_upload.restype = I32
     _lib = L
     return L

@@ -194,20 +194,38 @@ class NativeWriter:
     def finish(self) -> bytes:
         if self.state != "written":
             raise N.StrawboatError(N.E_OUT_OF_SPEC, "The strawboat file must be written before it can be finished")
-        offs = (ctypes.c_uint64 * max(1, len(self.metas)))(*[m.offset for m in self.metas])
-        nps = (ctypes.c_uint64 * max(1, len(self.metas)))(*[len(m.pages) for m in self.metas])
-        allp = [p for m in self.metas for p in m.pages]
-        pages = (N.PageMetaC * max(1, len(allp)))(*[N.PageMetaC(p.length, p.num_values) for p in allp])
-        sch = (ctypes.c_uint8 * max(1, len(self.schema_bytes))).from_buffer_copy(self.schema_bytes or b"\x00")
-        out = ctypes.POINTER(ctypes.c_uint8)()
-        olen = ctypes.c_uint64()
-        st = N.lib().sb_write_footer(sch, len(self.schema_bytes), offs, nps, len(self.metas), pages,
-                                     ctypes.byref(out), ctypes.byref(olen))
-        if st:
-            raise N.StrawboatError(st, "finish")
-        self.buf += _take(out, olen.value)
+        self.buf += footer_bytes(self.metas, self.schema_bytes)
         self.state = "finished"
         return bytes(self.buf)
 
     def total_size(self) -> int:
         return len(self.buf)
+
+
+def footer_bytes(metas: Sequence[ColumnMeta], schema_bytes: bytes = b"") -> bytes:
+    """The footer NativeWriter::finish writes (writer.rs:128-167): schema,
+    column metas, schema size, meta size, EOS."""
+    offs = (ctypes.c_uint64 * max(1, len(metas)))(*[m.offset for m in metas])
+    nps = (ctypes.c_uint64 * max(1, len(metas)))(*[len(m.pages) for m in metas])
+    allp = [p for m in metas for p in m.pages]
+    pages = (N.PageMetaC * max(1, len(allp)))(*[N.PageMetaC(p.length, p.num_values) for p in allp])
+    sch = (ctypes.c_uint8 * max(1, len(schema_bytes))).from_buffer_copy(schema_bytes or b"\x00")
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_uint64()
+    st = N.lib().sb_write_footer(sch, len(schema_bytes), offs, nps, len(metas), pages, ctypes.byref(out),
+                                 ctypes.byref(olen))
+    if st:
+        raise N.StrawboatError(st, "footer")
+    return _take(out, olen.value)
+
+
+def assemble_file(columns: Sequence[Tuple[bytes, Sequence[PageMeta]]], schema_bytes: bytes = b"") -> bytes:
+    """A whole file from encoded column chunks (any leaf kind: flat,
+    binary, list), in leaf order: header, chunks back to back, footer."""
+    buf = bytearray(ARROW_MAGIC + b"\x00\x00")
+    metas = []
+    for chunk, pages in columns:
+        metas.append(ColumnMeta(len(buf), list(pages)))
+        buf += chunk
+    buf += footer_bytes(metas, schema_bytes)
+    return bytes(buf)

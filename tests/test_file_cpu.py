@@ -1,0 +1,121 @@
+"""File side of the reader on the host (no GPU): the IPC schema parse
+(infer_schema, read/reader.rs:227-241) checked leaf by leaf against
+pyarrow's own type tree, and the footer read (read_meta / read_meta_async
+with its 64 KiB pre-read, reader.rs:168-225) against the Python restatement
+read_meta, including footers larger than the pre-read."""
+import numpy as np
+import pytest
+
+pa = pytest.importorskip("pyarrow")
+
+import pa_amd  # noqa: E402
+from pa_amd import _native as N  # noqa: E402
+
+PHYS = {pa.int8(): N.INT8, pa.int16(): N.INT16, pa.int32(): N.INT32, pa.int64(): N.INT64, pa.uint8(): N.UINT8,
+        pa.uint16(): N.UINT16, pa.uint32(): N.UINT32, pa.uint64(): N.UINT64, pa.float32(): N.FLOAT32,
+        pa.float64(): N.FLOAT64, pa.bool_(): N.BOOLEAN, pa.binary(): 11, pa.large_binary(): 12, pa.utf8(): 13,
+        pa.large_utf8(): 14, pa.date32(): N.INT32, pa.date64(): N.INT64, pa.timestamp("us"): N.INT64,
+        pa.time32("s"): N.INT32, pa.time64("ns"): N.INT64, pa.duration("ms"): N.INT64, pa.float16(): 0,
+        pa.decimal128(9, 2): 0}
+
+
+def expected_leaves(schema):
+    """arrow2 to_leaves order, from pyarrow's type tree."""
+    out = []
+
+    def walk(f, top, lists, flags):
+        t = f.type
+        if pa.types.is_list(t) or pa.types.is_large_list(t):
+            walk(t.value_field, top, lists + [(f.nullable, pa.types.is_large_list(t))], flags)
+        elif pa.types.is_struct(t):
+            for i in range(t.num_fields):
+                walk(t.field(i), top, lists, flags | 1)
+        else:
+            out.append((f.name, PHYS[t], f.nullable, len(lists), [x[0] for x in lists], [x[1] for x in lists], flags, top))
+
+    for i, f in enumerate(schema):
+        walk(f, i, [], 0)
+    return out
+
+
+SCHEMAS = [
+    pa.schema([pa.field("a", pa.int32(), False)]),
+    pa.schema([pa.field(n, t, bool(i % 2)) for i, (t, n) in enumerate(
+        [(pa.int8(), "i8"), (pa.uint16(), "u16"), (pa.int64(), "i64"), (pa.uint64(), "u64"), (pa.float32(), "f"),
+         (pa.float64(), "d"), (pa.bool_(), "b"), (pa.utf8(), "s"), (pa.large_utf8(), "ls"), (pa.binary(), "bin"),
+         (pa.large_binary(), "lbin"), (pa.date32(), "d32"), (pa.date64(), "d64"), (pa.timestamp("us"), "ts"),
+         (pa.time32("s"), "t32"), (pa.time64("ns"), "t64"), (pa.duration("ms"), "dur"), (pa.float16(), "half"),
+         (pa.decimal128(9, 2), "dec")])]),
+    pa.schema([pa.field("l", pa.list_(pa.field("item", pa.int32(), True)), True),
+               pa.field("ll", pa.list_(pa.field("x", pa.list_(pa.field("y", pa.utf8(), False)), False)), True),
+               pa.field("L", pa.large_list(pa.bool_()), False)]),
+    pa.schema([pa.field("st", pa.struct([pa.field("x", pa.int16()), pa.field("y", pa.list_(pa.float64()))])),
+               pa.field("z", pa.uint8())]),
+    pa.schema([pa.field("col_%d" % i, pa.int64()) for i in range(300)]),
+]
+
+
+@pytest.mark.parametrize("k", range(len(SCHEMAS)))
+@pytest.mark.parametrize("framing", ["message", "encapsulated"])
+def test_parse_schema_matches_pyarrow(k, framing):
+    s = SCHEMAS[k]
+    b = s.serialize().to_pybytes()
+    if framing == "message":  # arrow2 schema_to_bytes: the Message flatbuffer alone
+        b = b[8:]
+    got = [(l.name, l.physical_type, l.nullable, l.depth, l.list_nullable, l.large_list, l.flags, l.top_field)
+           for l in pa_amd.parse_schema(b)]
+    assert got == expected_leaves(s)
+
+
+@pytest.mark.parametrize("bad", [b"", b"\x00" * 3, b"\xff\xff\xff\xff\x08\x00\x00\x00", bytes(range(64)),
+                                 b"\x10\x00\x00\x00" + b"\xff" * 60])
+def test_parse_schema_rejects_garbage(bad):
+    with pytest.raises(pa_amd.StrawboatError):
+        pa_amd.parse_schema(bad)
+
+
+def test_parse_schema_truncated_never_crashes():
+    b = SCHEMAS[2].serialize().to_pybytes()[8:]
+    for n in range(0, len(b), 7):
+        try:
+            pa_amd.parse_schema(b[:n])
+        except pa_amd.StrawboatError:
+            pass
+
+
+def _file(tmp_path, cols, schema, name="t.sb"):
+    data = pa_amd.assemble_file(cols, schema.serialize().to_pybytes()[8:])
+    p = tmp_path / name
+    p.write_bytes(data)
+    return p, data
+
+
+@pytest.mark.parametrize("page_rows", [4096, 7])  # 7 rows a page: a footer far past the 64 KiB pre-read
+def test_file_open_matches_read_meta(tmp_path, page_rows):
+    rng = np.random.default_rng(1)
+    opts = pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=page_rows)
+    a = rng.integers(0, 1000, 20000).astype(np.int32)
+    b = rng.random(20000)
+    cols = [pa_amd.encode_column(a, None, False, opts), pa_amd.encode_column(b, rng.random(20000) > 0.3, True, opts)]
+    schema = pa.schema([pa.field("a", pa.int32(), False), pa.field("b", pa.float64(), True)])
+    p, data = _file(tmp_path, cols, schema)
+    with pa_amd.StrawboatFile(p) as f:
+        assert f.columns == pa_amd.read_meta(data)
+        assert [l.name for l in f.leaves] == ["a", "b"]
+        assert f.schema_bytes == schema.serialize().to_pybytes()[8:]
+        for c, (chunk, pages) in enumerate(cols):
+            assert f.columns[c].pages == list(pages)
+            off = f.columns[c].offset
+            assert data[off:off + f.columns[c].total_len()] == chunk
+
+
+def test_file_open_errors(tmp_path):
+    with pytest.raises(pa_amd.StrawboatError):
+        pa_amd.StrawboatFile(tmp_path / "missing.sb")
+    p = tmp_path / "short.sb"
+    p.write_bytes(b"ARROW2\x00\x00")
+    with pytest.raises(pa_amd.StrawboatError):
+        pa_amd.StrawboatFile(p)
+    p.write_bytes(b"ARROW2\x00\x00" + b"\x00" * 8 + (1 << 30).to_bytes(4, "little") + b"\xff" * 4 + b"\x00" * 4)
+    with pytest.raises(pa_amd.StrawboatError):
+        pa_amd.StrawboatFile(p)
