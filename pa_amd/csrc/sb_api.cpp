@@ -64,6 +64,7 @@ struct sb_plan {
   uint32_t* d_status = nullptr;
   uint32_t* d_lists = nullptr;  // [staged list | global list]
   uint32_t* d_light = nullptr;  // fixed width: per-page header-only tags (k_fix_light)
+  bool has_zstd_big = false;    // some header-only jobs are Zstd frames (k_zinflate)
   uint32_t* d_defer = nullptr;  // [defer count x2 | inflate job count x2 | work list...]
   sb::InflateJob* d_jobs = nullptr;  // fixed: one per page; binary: two per page
   uint8_t* d_scratch = nullptr;      // binary: expanded offsets streams
@@ -337,6 +338,10 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
     if (!n_light) {
       (void)hipFree(p->d_light);
       p->d_light = nullptr;
+    } else {  // any Zstd leaves too large for the deferred pass?  (k_zinflate is launched only then)
+      std::vector<sb::InflateJob> jobs(n_light);
+      if (hipMemcpy(jobs.data(), p->d_jobs, n_light * sizeof(sb::InflateJob), hipMemcpyDeviceToHost) == hipSuccess)
+        for (const auto& j : jobs) p->has_zstd_big |= j.codec == 2;
     }
   }
   if (p->binary && n_pages) {  // size every page's values once: they are fixed for the plan
@@ -476,6 +481,8 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
                         (uint8_t*)out->d_values, nullptr, nullptr, p->d_status};
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "zstd inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   if (p->deferred_state != 0 && p->n_pages) {
     // pages whose leaf stream is LZ4 / Zstd / Snappy / Patas, listed by the pass above

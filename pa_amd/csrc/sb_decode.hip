@@ -69,6 +69,7 @@ struct LdsSrc {
     uint32_t i = p >> 2;
     return __builtin_amdgcn_alignbyte(w[i + 1], w[i], p & 3);
   }
+  __device__ __forceinline__ LdsSrc at(uint32_t o) const { return LdsSrc{w, base + o}; }
   __device__ __forceinline__ uint64_t u64(uint32_t p) const {
     p += base;
     uint32_t i = p >> 2, sh = p & 3;
@@ -93,6 +94,7 @@ struct LdsSrc {
 // leaves the bytes the page owns.
 struct GlbSrc {
   const uint8_t* p;
+  __device__ __forceinline__ GlbSrc at(uint32_t o) const { return GlbSrc{p + o}; }
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
   __device__ __forceinline__ uint32_t u32(uint32_t i) const {
     uintptr_t a = (uintptr_t)(p + i);
@@ -2023,7 +2025,10 @@ __global__ __launch_bounds__(NT) void k_fix_light(LaunchArgs a, uint32_t n_pages
     if (lt) {
       codec = s.u8(p);
       cs = s.u32(p + 1);
-      lt = cs <= len - (p + 9) && (codec == 1 || codec == 3 || (flt && codec == 16));
+      // Zstd leaves whose page + expansion exceed the deferred pass's LDS
+      // expand straight into the column (k_zinflate)
+      const bool zbig = codec == 2 && (uint64_t)len + (uint64_t)n * W + kZTablesMax + 1024 > kDeferredLds;
+      lt = cs <= len - (p + 9) && (codec == 1 || codec == 3 || (flt && codec == 16) || zbig);
     }
     const uint32_t slot = wave_slot(a.job_count + a.parity, lt, 1);
     if (lt) {
@@ -2142,6 +2147,7 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
   const uint32_t n = a.count ? *a.count : a.n_jobs;
   for (uint32_t j = blockIdx.x * kInfWaves + wv; j < n; j += gridDim.x * kInfWaves) {
     const InflateJob jb = a.jobs[j];
+    if (jb.codec == 2) continue;  // k_zinflate's
     const uint64_t kind = jb.dst >> 62, off = jb.dst & kDstMask;
 #ifdef SB_V_SKIPSCRATCH
     if (kind == 1) continue;
@@ -2186,6 +2192,27 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
     }
 #endif
     if (st && lane == 0) a.status[jb.page] = st;
+  }
+}
+
+// Zstd frames larger than a workgroup's LDS (a leaf stream of a page whose
+// expansion does not fit the deferred pass): one wave per job reads the
+// frame from HBM and writes the output straight into the column; only the
+// decoder's FSE / Huffman tables and sequence batches live in LDS.  Output
+// bytes are stored and re-read (matches, literals at the window's tail) by
+// the same wave in program order.
+constexpr uint32_t kZinfWaves = 1;
+__global__ __launch_bounds__(64) void k_zinflate(InflateLaunch a) {
+  __shared__ u32x4 tabs[kZTablesMax / 16];
+  const uint32_t n = a.count ? *a.count : a.n_jobs;
+  for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
+    const InflateJob jb = a.jobs[j];
+    if (jb.codec != 2) continue;
+    const uint64_t kind = jb.dst >> 62, off = jb.dst & kDstMask;
+    if (kind != 0) continue;  // fixed-width leaves only (binary streams stay on the staged path)
+    uint8_t* dst = a.out + off;
+    const uint32_t st = zs::zstd_decode(GlbSrc{a.chunk + jb.src}, jb.csize, dst, jb.usize, (lds_u8*)&tabs[0], kZTablesMax);
+    if (st && (threadIdx.x & 63) == 0) a.status[jb.page] = st;
   }
 }
 
@@ -2295,6 +2322,12 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
       return false;
     }
     tab = (uint2*)(lds + bi.tab);
+#ifdef SB_V_BIN_NOWALK  // timing only: every entry is the first (wrong bytes, consistent sizes)
+    if (k && q + 8 <= end && s.u64(q) <= end - q - 8)
+      for (uint32_t e = 0; e < k; e++) tab[e] = make_uint2(q + 8, (uint32_t)s.u64(q));
+    q = end;
+    if (false)
+#endif
     for (uint32_t e = 0; e < k; e++) {  // u64 len + bytes per entry
       if (q + 8 > end) { set_err(sh, ST_IO); return false; }
       const uint64_t l = s.u64(q);
@@ -2333,6 +2366,11 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     if (bi.tab + 8 * (uint64_t)ep + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
     tab = (uint2*)(lds + bi.tab);
     uint64_t sum = 0;
+#ifdef SB_V_BIN_NOWALK
+    if (ep && q + 8 <= end && s.u64(q) <= end - q - 8)
+      for (uint32_t e = 0; e < ep; e++) { tab[e] = make_uint2(q + 8, (uint32_t)s.u64(q)); sum += s.u64(q); }
+    if (false)
+#endif
     for (uint32_t e = 0; e < ep; e++) {
       if (q + 8 > end) { set_err(sh, ST_IO); return false; }
       const uint64_t l = s.u64(q);
@@ -3840,6 +3878,12 @@ int launch_inflate(const InflateLaunch& a, void* stream) {
   if (a.n_jobs == 0) return 0;
   const uint32_t grid = std::min<uint32_t>((a.n_jobs + sbk::kInfWaves - 1) / sbk::kInfWaves, kInflateGrid);
   hipLaunchKernelGGL(sbk::k_inflate, dim3(grid), dim3(64 * sbk::kInfWaves), 0, (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_zinflate(const InflateLaunch& a, void* stream) {
+  if (a.n_jobs == 0) return 0;
+  const uint32_t grid = std::min<uint32_t>(a.n_jobs, 1024u);
+  hipLaunchKernelGGL(sbk::k_zinflate, dim3(grid), dim3(64), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb

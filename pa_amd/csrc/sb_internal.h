@@ -83,6 +83,8 @@ struct InflateLaunch {
   uint8_t* offs;  // kDstBinOffs jobs: the column's 32-bit offsets (dword-aligned)
 };
 int launch_inflate(const InflateLaunch& a, void* stream);
+// Zstd jobs (codec 2) of the same list: one wave per frame, tables in LDS, output in HBM.
+int launch_zinflate(const InflateLaunch& a, void* stream);
 constexpr uint32_t kInflateGrid = 2048;  // 4-wave workgroups: 8 waves per SIMD on 256 CUs
 
 // Launch entry points (sb_decode.hip).

@@ -94,13 +94,14 @@ __device__ __forceinline__ uint32_t hibit(uint32_t v) { return 31u - __builtin_c
 // Backward bit stream (RFC 8878 4.1): the highest set bit of the last byte
 // marks the end; bits are consumed from there down.  Bits below the stream
 // start read as zero and drive pos negative (libzstd's "overflow" state).
+template <class Src>
 struct RevBits {
-  LdsSrc in;
+  Src in;
   int32_t pos;  // bits not yet consumed
   int32_t wlo;  // stream bit of cont bit 0 (a multiple of 8)
   uint64_t cont;
-  __device__ bool init(const LdsSrc& src, uint32_t start, uint32_t len) {
-    in = LdsSrc{src.w, src.base + start};
+  __device__ bool init(const Src& src, uint32_t start, uint32_t len) {
+    in = src.at(start);
     pos = 0;
     wlo = 0;
     cont = 0;
@@ -154,7 +155,8 @@ __device__ __forceinline__ uint64_t mkcell(int kind, uint32_t s, uint32_t nb, ui
 
 // FSE_readNCount (RFC 8878 4.1.1; libzstd fse_decompress.c): normalized
 // counts, forward bits.  Returns the header bytes used, 0 on error.
-__device__ uint32_t read_ncount(const LdsSrc& in, uint32_t p, uint32_t avail, lds_s16* norm, uint32_t maxsym,
+template <class Src>
+__device__ uint32_t read_ncount(const Src& in, uint32_t p, uint32_t avail, lds_s16* norm, uint32_t maxsym,
                                 uint32_t maxlog, uint32_t* al_out, uint32_t* nsym_out) {
   if (!avail) return 0;
   uint32_t bp = 0;
@@ -248,7 +250,8 @@ __device__ bool build_fse(const Tabs& t, uint32_t nsym, uint32_t al, lds_u64* ce
 
 // Huffman tree description (RFC 8878 4.2.1) + the single-symbol decoding
 // table (libzstd HUF_readStats / HUF_readDTableX1).  Lane 0.
-__device__ uint32_t read_huf(const LdsSrc& in, uint32_t p, uint32_t avail, const Tabs& t, bool big, uint32_t* tl_out,
+template <class Src>
+__device__ uint32_t read_huf(const Src& in, uint32_t p, uint32_t avail, const Tabs& t, bool big, uint32_t* tl_out,
                              uint32_t* used) {
   if (!avail) return ST_CODEC;
   const uint32_t hb = in.u8(p);
@@ -265,7 +268,7 @@ __device__ uint32_t read_huf(const LdsSrc& in, uint32_t p, uint32_t avail, const
     uint32_t al = 0, nsym = 0;
     const uint32_t nc = read_ncount(in, p + 1, cs, t.norm, 255, 6, &al, &nsym);
     if (!nc || !build_fse(t, nsym, al, t.hwt, K_RAW)) return ST_CODEC;
-    RevBits br;
+    RevBits<Src> br;
     if (!br.init(in, p + 1 + nc, cs - nc)) return ST_CODEC;
     uint32_t s1 = br.read(al), s2 = br.read(al);
     for (;;) {
@@ -335,7 +338,8 @@ __device__ uint32_t read_huf(const LdsSrc& in, uint32_t p, uint32_t avail, const
 
 // One sequence table (RFC 8878 3.1.1.3.2.1): Predefined / RLE /
 // FSE_Compressed / Repeat.  Lane 0; *q advances past the description.
-__device__ uint32_t seq_table(const LdsSrc& in, uint32_t* q, uint32_t bend, uint32_t mode, int kind, const Tabs& t,
+template <class Src>
+__device__ uint32_t seq_table(const Src& in, uint32_t* q, uint32_t bend, uint32_t mode, int kind, const Tabs& t,
                               lds_u64* cells, uint32_t* al, bool* have, bool* pre) {
   const uint32_t maxsym = kind == K_LL ? 35 : kind == K_ML ? 52 : 31;
   const uint32_t maxlog = kind == K_OF ? 8 : 9;
@@ -375,12 +379,14 @@ __device__ uint32_t seq_table(const LdsSrc& in, uint32_t* q, uint32_t bend, uint
 }
 
 // wave copies (all 64 lanes, wave-uniform arguments)
-__device__ __forceinline__ void copy_fwd(lds_u8* out, uint32_t dst, uint32_t src, uint32_t n) {  // dst <= src
+template <class O>
+__device__ __forceinline__ void copy_fwd(O out, uint32_t dst, uint32_t src, uint32_t n) {  // dst <= src
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t c = 0; c < n; c += 64)
     if (lane < n - c) out[dst + c + lane] = out[src + c + lane];
 }
-__device__ __forceinline__ void copy_match(lds_u8* out, uint32_t d, uint32_t off, uint32_t ml) {
+template <class O>
+__device__ __forceinline__ void copy_match(O out, uint32_t d, uint32_t off, uint32_t ml) {
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t c = 0; c < ml; c += 64) {
     if (lane < ml - c) {
@@ -390,12 +396,14 @@ __device__ __forceinline__ void copy_match(lds_u8* out, uint32_t d, uint32_t off
     }
   }
 }
-__device__ __forceinline__ void copy_in(lds_u8* out, uint32_t dst, const LdsSrc& in, uint32_t src, uint32_t n) {
+template <class O, class Src>
+__device__ __forceinline__ void copy_in(O out, uint32_t dst, const Src& in, uint32_t src, uint32_t n) {
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t c = 0; c < n; c += 64)
     if (lane < n - c) out[dst + c + lane] = (uint8_t)in.u8(src + c + lane);
 }
-__device__ __forceinline__ void fill(lds_u8* out, uint32_t dst, uint8_t b, uint32_t n) {
+template <class O>
+__device__ __forceinline__ void fill(O out, uint32_t dst, uint8_t b, uint32_t n) {
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t c = 0; c < n; c += 64)
     if (lane < n - c) out[dst + c + lane] = b;
@@ -404,7 +412,8 @@ __device__ __forceinline__ void fill(lds_u8* out, uint32_t dst, uint8_t b, uint3
 // Execute a decoded batch: t.seq = [ll | ml | off | dst | lit src] x 64.
 // op0 / lp0: output and literal positions at the batch start, wend: the
 // output position after it.
-__device__ void exec_batch(lds_u8* out, const Tabs& t, uint32_t cnt, uint32_t op0, uint32_t lp0, uint32_t wend) {
+template <class O>
+__device__ void exec_batch(O out, const Tabs& t, uint32_t cnt, uint32_t op0, uint32_t lp0, uint32_t wend) {
   const uint32_t lane = threadIdx.x & 63;
   const bool v = lane < cnt;
   uint32_t ll = 0, ml = 0, off = 1, d = 0, ls = 0;
@@ -448,7 +457,8 @@ __device__ void exec_batch(lds_u8* out, const Tabs& t, uint32_t cnt, uint32_t op
 // Decode one Zstd frame of csize bytes (in[0, csize)) into out[0, olen).
 // All 64 lanes of the wave call it; `tb` is a 16-aligned LDS area of tcap >=
 // kZTablesBytes bytes.  Returns a wave-uniform status.
-__device__ uint32_t zstd_to_lds(const LdsSrc& in, uint32_t csize, lds_u8* out, uint32_t olen, lds_u8* tb,
+template <class Src, class O>
+__device__ uint32_t zstd_decode(const Src& in, uint32_t csize, O out, uint32_t olen, lds_u8* tb,
                                 uint32_t tcap) {
   const uint32_t lane = threadIdx.x & 63;
   const Tabs t(tb);
@@ -585,7 +595,7 @@ __device__ uint32_t zstd_to_lds(const LdsSrc& in, uint32_t csize, lds_u8* out, u
         }
         bool bad = false;
         if (lane < ns) {
-          RevBits br;
+          RevBits<Src> br;
           if (!br.init(in, sst, sln)) {
             bad = true;
           } else {
@@ -621,7 +631,7 @@ __device__ uint32_t zstd_to_lds(const LdsSrc& in, uint32_t csize, lds_u8* out, u
         if (q >= bend) return ST_CODEC;
         const uint32_t modes = in.u8(q++);
         if (modes & 3) return ST_CODEC;
-        RevBits br;
+        RevBits<Src> br;
         uint32_t sLL = 0, sML = 0, sOF = 0;
         if (lane == 0) {
           uint32_t qq = q;
@@ -711,6 +721,12 @@ __device__ uint32_t zstd_to_lds(const LdsSrc& in, uint32_t csize, lds_u8* out, u
   if (op != olen) return ST_CODEC;
   zsync();
   return ST_OK;
+}
+
+// The LDS-to-LDS form every staged caller uses.
+__device__ __forceinline__ uint32_t zstd_to_lds(const LdsSrc& in, uint32_t csize, lds_u8* out, uint32_t olen, lds_u8* tb,
+                                                uint32_t tcap) {
+  return zstd_decode(in, csize, out, olen, tb, tcap);
 }
 
 }  // namespace zs

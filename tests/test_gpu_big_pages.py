@@ -2,8 +2,8 @@
 caller sets no page size): the fixed-width HBM-source kernel
 (k_decode_global), k_inflate on a 8 MiB LZ4 stream, and a header-only Utf8
 None page copied from HBM -- each bit-exact against the oracle.  A Float64
-Zstd page that large still reports NotYetImplemented (its expansion does not
-fit the deferred pass's LDS)."""
+Zstd leaf page whose expansion exceeds the deferred pass's LDS decodes
+through k_zinflate (frame read from HBM, output written to the column)."""
 import numpy as np
 import pytest
 
@@ -59,15 +59,35 @@ def test_float64_lz4_1m_page(ctx):
     assert (pa_amd.read.unpack_bitmap(gm, N).cpu().numpy() == em).all()
 
 
-def test_float64_zstd_1m_page_reports_nyi(ctx):
+@pytest.mark.parametrize("rows", [N, 40_000, 3 << 20])
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+@pytest.mark.parametrize("dt", [np.float64, np.int32], ids=["f64", "i32"])
+def test_zstd_big_page(ctx, rows, nullable, dt):
+    """A Zstd leaf page whose expansion exceeds the deferred pass's LDS:
+    k_zinflate, one wave reading the frame from HBM and writing the column."""
     import pa_amd
 
     rng = np.random.default_rng(3)
-    v = np.round(rng.standard_normal(N) * 1e4, 2)
-    chunk, metas = one_page(pa_amd, v, None, False, default_compression=2)
-    with pytest.raises(pa_amd.StrawboatError) as e:
-        pa_amd.ColumnDecoder(chunk, metas, np.float64, False, ctx).decode()
-    assert e.value.status == 2
+    v = np.round(rng.standard_normal(rows) * 1e4, 2) if dt == np.float64 else rng.integers(0, 1 << 20, rows).astype(dt)
+    valid = rng.random(rows) > 0.1 if nullable else None
+    chunk, metas = one_page(pa_amd, v, valid, nullable, default_compression=2)
+    got, gm = pa_amd.ColumnDecoder(chunk, metas, dt, nullable, ctx).decode()
+    ev, em = O.read_column(chunk, [(m.length, m.num_values) for m in metas], dt, nullable)
+    assert got.cpu().numpy().tobytes() == ev.tobytes()
+    if nullable:
+        assert (pa_amd.read.unpack_bitmap(gm, rows).cpu().numpy() == em).all()
+
+
+def test_zstd_big_pages_many(ctx):
+    """Several big Zstd pages in one column, each its own k_zinflate job."""
+    import pa_amd
+
+    rng = np.random.default_rng(5)
+    v = rng.integers(0, 1000, 5 * 65536 + 17).astype(np.int64)
+    chunk, metas = pa_amd.encode_column(v, None, False, pa_amd.WriteOptions(default_compression=2, max_page_size=65536))
+    assert len(metas) == 6
+    got, _ = pa_amd.ColumnDecoder(chunk, metas, np.int64, False, ctx).decode()
+    assert (got.cpu().numpy() == v).all()
 
 
 @pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
