@@ -363,6 +363,11 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
     (void)hipMemcpy(st.data(), p->d_status, n_pages * 4, hipMemcpyDeviceToHost);
     (void)hipMemcpy(&p->values_bytes, p->d_bin + 2 * np, 8, hipMemcpyDeviceToHost);
     (void)hipMemcpy(&p->n_bin_jobs, p->d_defer + 2, 4, hipMemcpyDeviceToHost);
+    if (p->n_bin_jobs) {  // streams of big Zstd Basic pages (k_zinflate)
+      std::vector<sb::InflateJob> jobs(p->n_bin_jobs);
+      if (hipMemcpy(jobs.data(), p->d_jobs, jobs.size() * sizeof(sb::InflateJob), hipMemcpyDeviceToHost) == hipSuccess)
+        for (const auto& j : jobs) p->has_zstd_big |= j.codec == 2;
+    }
     uint32_t need = sb::kDeferredLds;
     (void)hipMemcpy(&need, p->d_bin + 2 * np + 1, 4, hipMemcpyDeviceToHost);
     p->bin_lds = std::min<uint32_t>(std::max<uint32_t>((need + 1023) & ~1023u, 4096), sb::kDeferredLds);
@@ -416,6 +421,8 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
                         p->d_bin + np, p->d_status, (uint8_t*)out->d_offsets};
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "zstd inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
   if (sb::launch_binary(1, p->offset_width, L, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));

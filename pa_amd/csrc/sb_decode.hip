@@ -2195,8 +2195,9 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
   }
 }
 
-// Zstd frames larger than a workgroup's LDS (a leaf stream of a page whose
-// expansion does not fit the deferred pass): one wave per job reads the
+// Zstd frames larger than a workgroup's LDS (a fixed-width leaf stream, or a
+// binary Basic page's offsets / values streams, whose expansion does not fit
+// the staged passes): one wave per job reads the
 // frame from HBM and writes the output straight into the column; only the
 // decoder's FSE / Huffman tables and sequence batches live in LDS.  Output
 // bytes are stored and re-read (matches, literals at the window's tail) by
@@ -2209,8 +2210,8 @@ __global__ __launch_bounds__(64) void k_zinflate(InflateLaunch a) {
     const InflateJob jb = a.jobs[j];
     if (jb.codec != 2) continue;
     const uint64_t kind = jb.dst >> 62, off = jb.dst & kDstMask;
-    if (kind != 0) continue;  // fixed-width leaves only (binary streams stay on the staged path)
-    uint8_t* dst = a.out + off;
+    if (kind == 3) continue;  // (Zstd offsets streams go through scratch)
+    uint8_t* dst = kind == 1 ? a.scratch + off : kind == 2 ? a.out + a.bases[off] : a.out + off;
     const uint32_t st = zs::zstd_decode(GlbSrc{a.chunk + jb.src}, jb.csize, dst, jb.usize, (lds_u8*)&tabs[0], kZTablesMax);
     if (st && (threadIdx.x & 63) == 0) a.status[jb.page] = st;
   }
@@ -2473,7 +2474,7 @@ __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int n
   if (!light_validity(s, len, n, nullable, &p, &lp.vbpos)) return false;
   if (p + 9 > len) return false;
   lp.codec = s.u8(p);
-  if (lp.codec != 0 && lp.codec != 1 && lp.codec != 3) return false;
+  if (lp.codec > 3) return false;
   const uint32_t cs = s.u32(p + 1), body = p + 9;
   if (cs > len - body) return false;
   const uint32_t vh = body + cs;
@@ -2486,6 +2487,8 @@ __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int n
   lp.ocs = cs;
   // None: both streams are copied as they lie (copy_from_slice lengths, binary/mod.rs:119-160)
   if (lp.codec == 0 && (cs != (n + 1) * (uint32_t)OW || lp.vcs != lp.S)) return false;
+  // Zstd: only pages whose streams do not fit the staged pass's LDS (k_zinflate)
+  if (lp.codec == 2 && (uint64_t)len + (uint64_t)(n + 1) * OW + lp.S + kZTablesMax + 1024 <= kDeferredLds) return false;
   return true;
 }
 
@@ -2507,14 +2510,16 @@ __global__ __launch_bounds__(NT) void k_bin_light(BinArgs a) {
       // Utf8 (32-bit) offsets are expanded straight into the column, rebased
       // (k_inflate xf); LargeUtf8 offsets go through scratch
       a.jobs[slot] = InflateJob{pd.byte_off + lp.ob,
-                                OW == 4 ? kDstBinOffs | (pd.row_off * 4) : kDstScratch | ((pd.row_off + page) * OW),
+                                OW == 4 && lp.codec != 2 ? kDstBinOffs | (pd.row_off * 4)
+                                                         : kDstScratch | ((pd.row_off + page) * OW),
                                 lp.ocs, (pd.num_values + 1) * (uint32_t)OW, lp.codec, page};
       a.jobs[slot + 1] = InflateJob{pd.byte_off + lp.vb, kDstBinBase | page, lp.vcs, lp.S, lp.codec, page};
     }
     if (lt) {
       a.sizes[page] = lp.S;
       a.status[page] = 0;
-      vbpos[page] = lp.vbpos | (lp.codec == 0 ? 0x80000000u : 0u);  // bit 31: a None page
+      // bit 31: a None page; bit 30: offsets expanded into scratch (Zstd)
+      vbpos[page] = lp.vbpos | (lp.codec == 0 ? 0x80000000u : 0u) | (lp.codec == 2 ? 0x40000000u : 0u);
       light[li] = page;
     } else {
       staged[si] = page;
@@ -2552,7 +2557,8 @@ __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
     const uint32_t n = pd.num_values;
     const uint64_t R = pd.row_off, V = a.bases[page], S = a.sizes[page];
     if (a.status[page]) continue;  // an inflate error stands
-    const uint32_t tag = a.cls[2 * np + page], vb = tag & 0x7FFFFFFFu;
+    const uint32_t tag = a.cls[2 * np + page], vb = tag & 0x3FFFFFFFu;
+    const bool scr = OW == 8 || (tag & 0x40000000u);  // offsets in scratch (else rebased in place by k_inflate)
     const GlbSrc pg{a.chunk + pd.byte_off};
     if (tag & 0x80000000u) {  // a None page: offsets rebased and values copied from the page in HBM
       __shared__ LightPage nl_lp;
@@ -2581,7 +2587,7 @@ __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
     // p[n] must be the values stream's length (DEVIATION: the reference only
     // fails once the column's last offset passes its values, at try_new)
     if (tid == 0) {
-      if constexpr (OW == 4)  // rebased in place by k_inflate
+      if (!scr)  // rebased in place by k_inflate
         bad = ((uint32_t)((const uint32_t*)a.out_offsets)[R + n] != (uint32_t)(V + S) || V + S > a.values_cap) ? ST_OUT_OF_SPEC
                                                                                         : 0u;
       else
@@ -2594,7 +2600,7 @@ __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
       if (tid == 0) a.status[page] = e;
       continue;
     }
-    if constexpr (OW == 8) {
+    if (scr) {
       if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, po(0), OW);  // the first page keeps its p[0]
       for (uint32_t k = tid + 1; k <= n; k += NT) bin_put_off(a.out_offsets, R + k, V + po(k), OW);
     }

@@ -106,3 +106,29 @@ def test_utf8_none_1m_page(ctx, nullable):
     assert gv.cpu().numpy()[:len(ev)].tobytes() == ev
     if nullable:
         assert (pa_amd.read.unpack_bitmap(gm, N).cpu().numpy() == em).all()
+
+
+@pytest.mark.parametrize("phys", ["UTF8", "LARGE_UTF8"])
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+def test_utf8_zstd_big_page(ctx, phys, nullable):
+    """A Basic Zstd Utf8 page too large for the staged passes: both streams
+    through k_zinflate (offsets via scratch, values at the page's base)."""
+    import pa_amd
+
+    rng = np.random.default_rng(6)
+    n = 300_000
+    strs = [str(x).encode() * int(rng.integers(0, 3)) for x in rng.integers(0, 10**9, n)]
+    vals, offs = pa_amd.binary.strings_to_arrow(strs)
+    valid = rng.random(n) > 0.1 if nullable else None
+    pt = getattr(pa_amd, phys)
+    chunk, metas = pa_amd.encode_binary_column(vals, offs, valid, nullable,
+                                               pa_amd.WriteOptions(default_compression=2, max_page_size=100_000),
+                                               physical_type=pt)
+    assert len(metas) == 3
+    o, v, m = pa_amd.BinaryColumnDecoder(chunk, metas, pt, nullable, ctx).decode()
+    eo, ev, em = O.read_binary_column(chunk, [(x.length, x.num_values) for x in metas], nullable,
+                                      offset_width=8 if phys == "LARGE_UTF8" else 4)
+    assert (o.cpu().numpy() == eo).all()
+    assert v.cpu().numpy()[:len(ev)].tobytes() == ev
+    if nullable:
+        assert (pa_amd.read.unpack_bitmap(m, n).cpu().numpy() == em).all()
