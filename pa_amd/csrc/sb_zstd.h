@@ -458,7 +458,7 @@ __device__ void exec_batch(O out, const Tabs& t, uint32_t cnt, uint32_t op0, uin
 // All 64 lanes of the wave call it; `tb` is a 16-aligned LDS area of tcap >=
 // kZTablesBytes bytes.  Returns a wave-uniform status.
 template <class Src, class O>
-__device__ uint32_t zstd_decode(const Src& in, uint32_t csize, O out, uint32_t olen, lds_u8* tb,
+__device__ __attribute__((noinline)) uint32_t zstd_decode(const Src& in, uint32_t csize, O out, uint32_t olen, lds_u8* tb,
                                 uint32_t tcap) {
   const uint32_t lane = threadIdx.x & 63;
   const Tabs t(tb);
@@ -723,8 +723,10 @@ __device__ uint32_t zstd_decode(const Src& in, uint32_t csize, O out, uint32_t o
   return ST_OK;
 }
 
-// The LDS-to-LDS form every staged caller uses.
-__device__ __forceinline__ uint32_t zstd_to_lds(const LdsSrc& in, uint32_t csize, lds_u8* out, uint32_t olen, lds_u8* tb,
+// The LDS-to-LDS form every staged caller uses (one out-of-line copy of the
+// decoder: inlined into every kernel that can meet a Zstd stream, it grew
+// their code enough to slow the C5 decode by a quarter).
+__device__ __attribute__((noinline)) uint32_t zstd_to_lds(const LdsSrc& in, uint32_t csize, lds_u8* out, uint32_t olen, lds_u8* tb,
                                                 uint32_t tcap) {
   return zstd_decode(in, csize, out, olen, tb, tcap);
 }
