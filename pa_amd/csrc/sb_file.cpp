@@ -119,14 +119,20 @@ int32_t leaf_physical(Fb& fb, int tag, uint64_t ty) {
   return 0;
 }
 
+// Flatbuffer child vectors may alias one table many times (a malicious
+// footer can make a nest of Structs with two aliased children each visit
+// 2^level fields): the walk is capped by the number of fields it visits.
+constexpr uint64_t kMaxSchemaFields = 1u << 16;
+
 struct Walk {
   Fb& fb;
   std::vector<sb_leaf_info>& out;
   int top = 0;
   bool fail = false;
+  uint64_t visits = 0;
 
   void field(uint64_t f, sb_leaf_info path, int level) {
-    if (!f || level > 64 || !fb.ok) {
+    if (!f || level > 64 || !fb.ok || ++visits > kMaxSchemaFields) {
       fail = true;
       return;
     }
@@ -153,7 +159,7 @@ struct Walk {
     }
     if (tag == kStruct || tag == kUnion) {
       path.flags |= tag == kStruct ? SB_LEAF_STRUCT : SB_LEAF_UNION;
-      for (uint32_t k = 0; k < nch; k++) field(child(k), path, level + 1);
+      for (uint32_t k = 0; k < nch && !fail; k++) field(child(k), path, level + 1);
       return;
     }
     sb_leaf_info li = path;
@@ -257,6 +263,7 @@ struct Staging {
   hipStream_t copy = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
   hipEvent_t done = nullptr;
+  hipEvent_t before = nullptr;  // the context stream's work queued before an upload
   bool pending[2] = {false, false};
 };
 Staging g_staging[kMaxDevices];
@@ -264,7 +271,8 @@ Staging g_staging[kMaxDevices];
 bool staging_init(Staging& s) {
   if (s.ready) return true;
   bool ok = hipStreamCreateWithFlags(&s.copy, hipStreamNonBlocking) == hipSuccess &&
-            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&s.before, hipEventDisableTiming) == hipSuccess;
   for (int k = 0; k < 2 && ok; k++)
     ok = hipHostMalloc((void**)&s.pin[k], kStageChunk, hipHostMallocDefault) == hipSuccess &&
          hipEventCreateWithFlags(&s.ev[k], hipEventDisableTiming) == hipSuccess;
@@ -350,7 +358,10 @@ sb_status sb_file_column(const sb_file* f, uint64_t col, uint64_t* offset, uint6
   if (!f || col >= f->col_off.size()) return SB_E_ARG;
   const uint64_t a = f->col_start[col], b = f->col_start[col + 1];
   uint64_t len = 0;
-  for (uint64_t i = a; i < b; i++) len += f->pages[i].length;
+  for (uint64_t i = a; i < b; i++) {  // overflow-checked: each page bounded by the file
+    if (f->pages[i].length > f->size || len > f->size - f->pages[i].length) return SB_E_OUT_OF_SPEC;
+    len += f->pages[i].length;
+  }
   if (f->col_off[col] > f->size || len > f->size - f->col_off[col]) return SB_E_OUT_OF_SPEC;
   if (offset) *offset = f->col_off[col];
   if (chunk_len) *chunk_len = len;
@@ -380,6 +391,13 @@ sb_status sb_file_upload(sb_ctx* ctx, sb_file* f, uint64_t offset, uint64_t len,
   std::lock_guard<std::mutex> lock(sg.mu);
   if (!staging_init(sg)) return file_fail(f, SB_E_DEVICE, "staging buffers");
   uint8_t* dst = (uint8_t*)d_dst;
+  // The copies run on the staging stream: they must not overwrite d_dst
+  // while work queued earlier on the context's stream (a decode still reading
+  // a reused chunk buffer, or the caching allocator's previous user of the
+  // block) may touch it.
+  if (len && (hipEventRecord(sg.before, (hipStream_t)sb_ctx_stream(ctx)) != hipSuccess ||
+              hipStreamWaitEvent(sg.copy, sg.before, 0) != hipSuccess))
+    return file_fail(f, SB_E_DEVICE, "stream order");
   for (uint64_t done = 0, k = 0; done < len; k++) {
     const int b = (int)(k & 1);
     const uint64_t n = std::min(kStageChunk, len - done);

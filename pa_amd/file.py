@@ -121,6 +121,13 @@ class StrawboatFile:
         from .binary import BINARY, LARGE_BINARY, LARGE_UTF8, UTF8, BinaryColumnDecoder
         from .nested import ListColumnDecoder, NestedColumnDecoder
 
+        if len(self.leaves) != self.num_columns:
+            # leaves and column metas pair up one to one (to_leaves order); a
+            # mismatch would decode a column with another leaf's type
+            raise N.StrawboatError(N.E_OUT_OF_SPEC, f"schema has {len(self.leaves)} leaves but the footer "
+                                                    f"{self.num_columns} columns")
+        if not 0 <= col < self.num_columns:
+            raise N.StrawboatError(N.E_ARG, f"column {col} out of range")
         leaf = self.leaves[col]
         ctx = resolve_context(ctx, chunk)
         if chunk is None:

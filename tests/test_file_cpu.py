@@ -119,3 +119,48 @@ def test_file_open_errors(tmp_path):
     p.write_bytes(b"ARROW2\x00\x00" + b"\x00" * 8 + (1 << 30).to_bytes(4, "little") + b"\xff" * 4 + b"\x00" * 4)
     with pytest.raises(pa_amd.StrawboatError):
         pa_amd.StrawboatFile(p)
+
+
+def _fb_u32(b, p):
+    return int.from_bytes(b[p:p + 4], "little")
+
+
+def _fb_field(b, t, i):
+    vt = t - int.from_bytes(b[t:t + 4], "little", signed=True)
+    vsz = int.from_bytes(b[vt:vt + 2], "little")
+    if 4 + 2 * i + 2 > vsz:
+        return 0
+    o = int.from_bytes(b[vt + 4 + 2 * i:vt + 6 + 2 * i], "little")
+    return t + o if o else 0
+
+
+def test_parse_schema_aliased_children_bounded():
+    """A footer whose Struct child vectors point both entries at one table
+    (2^depth visits) is rejected after a bounded walk, not walked forever
+    (sb_file.cpp schema walk)."""
+    t = pa.int32()
+    for _ in range(40):
+        t = pa.struct([pa.field("a", t), pa.field("b", pa.int32())])
+    b = bytearray(pa.schema([pa.field("s", t)]).serialize().to_pybytes()[8:])
+    msg = _fb_u32(b, 0)
+    sch = _fb_field(b, msg, 2)
+    sch += _fb_u32(b, sch)
+    fv = _fb_field(b, sch, 1)
+    fv += _fb_u32(b, fv)
+    f = fv + 4 + _fb_u32(b, fv + 4)
+    patched = 0
+    while True:
+        cf = _fb_field(b, f, 5)
+        if not cf:
+            break
+        v = cf + _fb_u32(b, cf)
+        if _fb_u32(b, v) != 2:
+            break
+        e0, e1 = v + 4, v + 8
+        child0 = e0 + _fb_u32(b, e0)
+        b[e1:e1 + 4] = (child0 - e1).to_bytes(4, "little")  # entry 1 aliases entry 0
+        patched += 1
+        f = child0
+    assert patched == 40
+    with pytest.raises(N.StrawboatError):
+        pa_amd.parse_schema(bytes(b))

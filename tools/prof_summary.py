@@ -42,7 +42,8 @@ def pmc(fpath, wpath, out):
         fb = 2.0 * 1024 * sum(fv) / max(1, len(fv))
         wb = 1024 * sum(wv) / max(1, len(wv))
         res[k] = {"fetch_bytes_per_dispatch": int(fb), "write_bytes_per_dispatch": int(wb),
-                  "hbm_bytes_per_dispatch": int(fb + wb), "dispatches": [len(fv), len(wv)]}
+                  "hbm_bytes_per_dispatch": int(fb + wb), "dispatches": [len(fv), len(wv)],
+                  "raw_fetch_kib": round(sum(fv) / max(1, len(fv)), 1), "raw_write_kib": round(sum(wv) / max(1, len(wv)), 1)}
     res["_correction"] = "fetch = 2 x FETCH_SIZE x 1KiB (gfx950 16 B/lane read undercount), write = WRITE_SIZE x 1KiB"
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1)[:3000])
