@@ -68,6 +68,11 @@ struct sb_plan {
   uint32_t* d_defer = nullptr;  // [defer count x2 | inflate job count x2 | work list...]
   sb::InflateJob* d_jobs = nullptr;  // fixed: one per page; binary: two per page
   uint8_t* d_scratch = nullptr;      // binary: expanded offsets streams
+  uint8_t* d_region = nullptr;       // fixed width: the pages' HBM regions (PageDesc.reserved)
+  uint32_t* d_spill = nullptr;       // [2] spilled-leaf job counts (by decode parity)
+  sb::InflateJob* d_spill_jobs = nullptr;
+  uint32_t n_spill = 0;              // pages with a spill area (bounds the spill launches)
+  uint32_t n_big = 0;                // binary: big Extend pages (tables in d_region)
   uint32_t n_bin_jobs = 0;
   uint64_t decodes = 0;
   int deferred_state = -1;  // -1 unknown, 0 no deferred pages, 1 some
@@ -85,7 +90,7 @@ struct sb_plan {
   sb_plan* inner = nullptr;
   uint64_t n_leaves = 0;
   int offset_width = 0;
-  uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1 | LDS need 1] then BinLaunch::cls (u32)
+  uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1 | (unused) 1] then BinLaunch::cls (u32)
   uint32_t bin_grid = 0;      // staged-pass workgroups: the plan pass's staged page count
   uint32_t bin_lds = 0;       // dynamic LDS of the binary kernels (the largest page need, from the plan pass)
   uint64_t values_bytes = 0;
@@ -200,6 +205,9 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_defer) (void)hipFree(p->d_defer);
   if (p->d_jobs) (void)hipFree(p->d_jobs);
   if (p->d_scratch) (void)hipFree(p->d_scratch);
+  if (p->d_region) (void)hipFree(p->d_region);
+  if (p->d_spill) (void)hipFree(p->d_spill);
+  if (p->d_spill_jobs) (void)hipFree(p->d_spill_jobs);
   if (p->d_bin) (void)hipFree(p->d_bin);
   if (p->d_lc) (void)hipFree(p->d_lc);
   if (p->d_nest) (void)hipFree(p->d_nest);
@@ -216,11 +224,25 @@ uint64_t sb_plan_num_pages(const sb_plan* p) { return p ? p->n_pages : 0; }
 // rows [row_off, row_off + num_values) of the output (sb_plan_column: the
 // running sums of the PageMeta; nested leaves: each page's values stream at
 // its leaf base).
+// Fixed-width page regions (plan_regions): none, sized from a plan-time
+// probe of each large page's cascade, or sized conservatively from the page
+// table alone (List values streams, whose descriptors the levels pass writes
+// at decode time).
+enum RegionMode { kRegionsNone = 0, kRegionsProbe = 1, kRegionsBySize = 2 };
+
 static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
-                            std::vector<sb::PageDesc> pages, sb_plan** out);
+                            std::vector<sb::PageDesc> pages, sb_plan** out, int regions = kRegionsProbe);
+
+static sb_status plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                             const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out, int regions);
 
 sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
                          const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out) {
+  return plan_column(ctx, desc, d_chunk, chunk_len, h_metas, n_pages, out, kRegionsProbe);
+}
+
+static sb_status plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                             const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out, int regions) {
   if (!ctx || !desc || !out || (!h_metas && n_pages)) return fail(ctx, SB_E_ARG, "null argument");
   if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
   std::vector<sb::PageDesc> pages(n_pages);
@@ -233,11 +255,74 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
     off += m.length;
     rows += m.num_values;
   }
-  return plan_pages(ctx, desc, d_chunk, chunk_len, std::move(pages), out);
+  return plan_pages(ctx, desc, d_chunk, chunk_len, std::move(pages), out, regions);
+}
+
+// HBM regions of a fixed-width plan's large pages (PageDesc.reserved): the
+// roaring tables of a Freq page that can hold more containers than the LDS
+// tables (num_values > 4 bitmap containers' worth), and the area a Dict /
+// Freq cascade's general-codec leaf expands into when page + expansion
+// exceed the deferred pass's LDS.  Probed pages get only what their cascade
+// needs; by-size pages get both.
+static hipError_t plan_regions(sb_ctx* ctx, sb_plan* p, std::vector<sb::PageDesc>& pages, int mode) {
+  std::vector<uint32_t> cand;
+  const uint64_t W = (uint64_t)p->width;
+  auto roar_cand = [](const sb::PageDesc& pd) { return pd.num_values > 4u * 4096u; };
+  auto spill_cand = [&](const sb::PageDesc& pd) {
+    return sb::align16((uint64_t)pd.byte_len + 15 + sb::kStagePad) + sb::spill_area_bytes(pd.num_values, W) +
+               sb::kZTablesMax + 64 > sb::kDeferredLds;
+  };
+  for (uint32_t i = 0; i < (uint32_t)pages.size(); i++)
+    if (roar_cand(pages[i]) || spill_cand(pages[i])) cand.push_back(i);
+  if (cand.empty()) return hipSuccess;
+  std::vector<uint32_t> bits(cand.size(), 7u);
+  hipError_t e = hipSuccess;
+  if (mode == kRegionsProbe) {
+    uint32_t* d = nullptr;
+    e = hipMalloc(&d, 2 * cand.size() * sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(d, cand.data(), cand.size() * 4, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess && sb::launch_fix_probe(p->d_chunk, p->d_pages, d, (uint32_t)cand.size(), p->width,
+                                                p->desc.nullable, d + cand.size(), ctx->stream))
+      e = hipErrorLaunchFailure;
+    if (e == hipSuccess) e = hipMemcpyAsync(bits.data(), d + cand.size(), cand.size() * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return e;
+  }
+  uint64_t off = 0;
+  uint32_t n_spill = 0;
+  for (size_t j = 0; j < cand.size(); j++) {
+    sb::PageDesc& pd = pages[cand[j]];
+    uint64_t flags = 0, size = 0;
+    if (roar_cand(pd) && (bits[j] & 1)) {
+      flags |= sb::kRegionRoar;
+      size += sb::roar_area_bytes(pd.num_values);
+    }
+    if (spill_cand(pd) && (bits[j] & 2) && (bits[j] & 4)) {  // (a plain general leaf goes to k_inflate / k_zinflate)
+      flags |= sb::kRegionSpill;
+      size += sb::spill_area_bytes(pd.num_values, W);
+      n_spill++;
+    }
+    if (flags) {
+      pd.reserved = off | flags;
+      off += size;
+    }
+  }
+  if (!off) return hipSuccess;
+  e = hipMalloc(&p->d_region, off);
+  if (e == hipSuccess && n_spill) e = hipMalloc(&p->d_spill, 2 * sizeof(uint32_t));
+  if (e == hipSuccess && n_spill) e = hipMemsetAsync(p->d_spill, 0, 2 * sizeof(uint32_t), ctx->stream);
+  if (e == hipSuccess && n_spill) e = hipMalloc(&p->d_spill_jobs, n_spill * sizeof(sb::InflateJob));
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(p->d_pages, pages.data(), pages.size() * sizeof(sb::PageDesc), hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  p->n_spill = n_spill;
+  return e;
 }
 
 static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
-                            std::vector<sb::PageDesc> pages, sb_plan** out) {
+                            std::vector<sb::PageDesc> pages, sb_plan** out, int regions) {
   const uint64_t n_pages = pages.size();
   bool is_float;
   int width = type_width(desc->physical_type, &is_float);
@@ -314,6 +399,13 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
     sb_plan_destroy(p);
     return fail(ctx, SB_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
   }
+  if (regions != kRegionsNone && !owidth && !is_bool && n_pages) {
+    e = plan_regions(ctx, p, pages, regions);
+    if (e != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "plan regions: %s", hipGetErrorString(e));
+    }
+  }
   if (p->d_light && n_pages) {
     // Classify once: the per-decode classify pass (one thread per page) runs
     // only for chunks that hold header-only pages; the staged pass handles
@@ -345,16 +437,55 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
     }
   }
   if (p->binary && n_pages) {  // size every page's values once: they are fixed for the plan
-    e = hipMalloc(&p->d_bin, (2 * np + 2) * sizeof(uint64_t) + (3 * np + 2) * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemsetAsync(p->d_bin + 2 * np + 1, 0, sizeof(uint64_t), ctx->stream);
+    e = hipMalloc(&p->d_bin, (2 * np + 2) * sizeof(uint64_t) + (4 * np + 3) * sizeof(uint32_t));
     if (e != hipSuccess) {
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "plan alloc: %s", hipGetErrorString(e));
     }
+    uint32_t* cls = (uint32_t*)(p->d_bin + 2 * np + 2);
+    // Probe: the LDS each page's staged decode needs; Extend pages that need
+    // more than one workgroup's LDS become big pages with an HBM region
+    {
+      uint32_t* d_need = nullptr;
+      uint64_t* d_rneed = nullptr;
+      std::vector<uint32_t> need(n_pages);
+      std::vector<uint64_t> rneed(n_pages);
+      e = hipMalloc(&d_need, np * sizeof(uint32_t));
+      if (e == hipSuccess) e = hipMalloc(&d_rneed, np * sizeof(uint64_t));
+      if (e == hipSuccess) {
+        sb::BinLaunch P{d_chunk, p->d_pages, (uint32_t)n_pages, desc->nullable, nullptr, nullptr, nullptr, nullptr,
+                        nullptr, 0, nullptr, p->d_status, nullptr, nullptr, nullptr, 0, d_need, cls, 1, nullptr,
+                        d_rneed, 0};
+        if (sb::launch_binary(2, owidth, P, ctx->stream)) e = hipErrorLaunchFailure;
+      }
+      if (e == hipSuccess) e = hipMemcpyAsync(need.data(), d_need, n_pages * 4, hipMemcpyDeviceToHost, ctx->stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(rneed.data(), d_rneed, n_pages * 8, hipMemcpyDeviceToHost, ctx->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+      if (d_need) (void)hipFree(d_need);
+      if (d_rneed) (void)hipFree(d_rneed);
+      uint64_t off = 0;
+      uint32_t max_need = 0;
+      for (uint64_t i = 0; i < n_pages && e == hipSuccess; i++) {
+        if (need[i] > sb::kDeferredLds && rneed[i]) {
+          pages[i].reserved = off + 1;
+          off += sb::align16(rneed[i]);
+          p->n_big++;
+        } else {
+          max_need = std::max(max_need, need[i]);
+        }
+      }
+      p->bin_lds = std::min<uint32_t>(std::max<uint32_t>((max_need + 1023) & ~1023u, 4096), sb::kDeferredLds);
+      if (e == hipSuccess && off) e = hipMalloc(&p->d_region, off);
+      if (e == hipSuccess && off)
+        e = hipMemcpyAsync(p->d_pages, pages.data(), n_pages * sizeof(sb::PageDesc), hipMemcpyHostToDevice, ctx->stream);
+      if (e != hipSuccess) {
+        sb_plan_destroy(p);
+        return fail(ctx, SB_E_DEVICE, "binary plan probe: %s", hipGetErrorString(e));
+      }
+    }
     sb::BinLaunch L{d_chunk, p->d_pages, (uint32_t)n_pages, desc->nullable, p->d_bin, p->d_bin + np,
                     p->d_bin + 2 * np, nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr,
-                    sb::kDeferredLds, (uint32_t*)(p->d_bin + 2 * np + 1), (uint32_t*)(p->d_bin + 2 * np + 2),
-                    (uint32_t)std::min<size_t>(np, 65535)};
+                    p->bin_lds, nullptr, cls, (uint32_t)std::min<size_t>(np, 65535), p->d_region, nullptr, p->n_big};
     if (sb::launch_binary(0, owidth, L, ctx->stream) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "binary sizing failed: %s", hipGetErrorString(hipGetLastError()));
@@ -368,11 +499,8 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
       if (hipMemcpy(jobs.data(), p->d_jobs, jobs.size() * sizeof(sb::InflateJob), hipMemcpyDeviceToHost) == hipSuccess)
         for (const auto& j : jobs) p->has_zstd_big |= j.codec == 2;
     }
-    uint32_t need = sb::kDeferredLds;
-    (void)hipMemcpy(&need, p->d_bin + 2 * np + 1, 4, hipMemcpyDeviceToHost);
-    p->bin_lds = std::min<uint32_t>(std::max<uint32_t>((need + 1023) & ~1023u, 4096), sb::kDeferredLds);
     uint32_t n_staged = 0;
-    (void)hipMemcpy(&n_staged, (uint32_t*)(p->d_bin + 2 * np + 2) + 3 * np, 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&n_staged, cls + 4 * np, 4, hipMemcpyDeviceToHost);
     p->bin_grid = std::max<uint32_t>(1, std::min<uint32_t>(n_staged, 65535));
     for (uint64_t i = 0; i < n_pages; i++) {
       if (st[i]) {
@@ -409,13 +537,13 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   HIP_TRY(ctx, hipMemsetAsync(p->d_defer + 2, 0, sizeof(uint32_t), ctx->stream));
   sb::BinLaunch S{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
                   nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr, p->bin_lds, nullptr,
-                  (uint32_t*)(p->d_bin + 2 * np + 2), p->bin_grid};
+                  (uint32_t*)(p->d_bin + 2 * np + 2), p->bin_grid, p->d_region, nullptr, p->n_big};
   if (sb::launch_binary(0, p->offset_width, S, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "binary sizing launch failed: %s", hipGetErrorString(hipGetLastError()));
   sb::BinLaunch L{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
                   (uint8_t*)out->d_offsets, out->d_values, out->values_capacity, (uint32_t*)out->d_validity,
                   p->d_status, p->d_jobs, nullptr, p->d_scratch, p->bin_lds, nullptr, (uint32_t*)(p->d_bin + 2 * np + 2),
-                  p->bin_grid};
+                  p->bin_grid, p->d_region, nullptr, p->n_big};
   if (p->n_bin_jobs) {  // Basic LZ4 / Snappy pages: streams expanded first, one wave each
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2, p->n_bin_jobs, out->d_values, p->d_scratch,
                         p->d_bin + np, p->d_status, (uint8_t*)out->d_offsets};
@@ -456,6 +584,9 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   a.job_count = p->d_defer + 2;
   a.defer_list = p->d_defer + 4;
   a.jobs = p->d_jobs;
+  a.region = p->d_region;
+  a.spill_count = p->d_spill;
+  a.spill_jobs = p->d_spill_jobs;
   a.parity = (uint32_t)(p->decodes & 1);
   p->decodes++;
   if (p->boolean) {
@@ -498,6 +629,17 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
     a.stage_bytes = sb::kDeferredLds;
     if (sb::launch_decode_fixed(p->width, p->is_float, 2, a, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "deferred decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (p->n_spill) {
+      // leaves the deferred pass could not hold in LDS: expanded into the
+      // pages' regions (one wave per stream), then the pages decoded from there
+      sb::InflateLaunch I{p->d_chunk, p->d_spill_jobs, p->d_spill + a.parity, p->n_spill, nullptr, p->d_region,
+                          nullptr, p->d_status};
+      if (sb::launch_inflate(I, ctx->stream) || sb::launch_zinflate(I, ctx->stream))
+        return fail(ctx, SB_E_DEVICE, "spill inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
+      a.n_list = p->n_spill;
+      if (sb::launch_decode_fixed(p->width, p->is_float, 3, a, ctx->stream))
+        return fail(ctx, SB_E_DEVICE, "spilled decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    }
   }
   if (p->timing) {
     HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
@@ -570,7 +712,7 @@ sb_status sb_plan_list_column(sb_ctx* ctx, const sb_list_desc* d, const uint8_t*
   if (d->offset_width != 4 && d->offset_width != 8) return fail(ctx, SB_E_ARG, "offset width must be 4 or 8");
   sb_column_desc cd{d->physical_type, 0};
   sb_plan* inner = nullptr;
-  sb_status st = sb_plan_column(ctx, &cd, d_chunk, chunk_len, h_metas, n_pages, &inner);
+  sb_status st = plan_column(ctx, &cd, d_chunk, chunk_len, h_metas, n_pages, &inner, kRegionsBySize);
   if (st) return st;
   sb_plan* p = new sb_plan();
   p->desc = cd;

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "sb_internal.h"
 
@@ -154,14 +155,21 @@ struct Shared {
   uint32_t defer;
   // Dict
   uint32_t dict_k, dict_off;
-  // Freq
+  // Freq: the roaring bitmap's container tables (roaring_build), in the LDS
+  // arrays below when they fit, else in the page's HBM region
   uint64_t freq_top;
   uint32_t n_conts;
+  uint32_t roar_r, roar_bm, roar_pending;  // position and size of the portable bitmap; tables still to build
+  uint32_t* rkey;                         // container keys
+  uint32_t* rdata;                        // source position of each container's data
+  uint32_t* rpre;                         // exceptions before each container (n_conts + 1)
+  uint32_t* rbm;                          // bitmap container index into rcp, or ~0u for array containers
+  uint16_t* rcp;                          // per bitmap container: set bits before each 16-word group (64)
   uint32_t cont_key[kMaxConts];
   uint32_t cont_data[kMaxConts];
   uint32_t cont_prefix[kMaxConts + 1];
-  uint32_t cont_bm[kMaxConts];            // index into cont_cp, or ~0u for array containers
-  uint16_t cont_cp[kMaxBitmapConts][64];  // set bits before each 16-word group
+  uint32_t cont_bm[kMaxConts];
+  uint16_t cont_cp[kMaxBitmapConts][64];
 };
 
 __device__ __forceinline__ void set_err(Shared& sh, uint32_t code) { atomicMax(&sh.err, code); }
@@ -516,26 +524,32 @@ __device__ bool parse_stream(const Src& s, uint32_t p, uint32_t end, uint32_t n,
 
 // Roaring select: row of exception i.  Array containers index directly;
 // bitmap containers find the 16-word group by its checkpoint, then the word by
-// popcounts, then the bit.
+// popcounts, then the bit.  The container is found by binary search over the
+// exception prefix (a 1M-row page has 16 containers, a 100M-row one 1526).
 template <class Src>
 __device__ __forceinline__ uint32_t roaring_select(const Src& s, const Shared& sh, uint32_t i) {
-  uint32_t c = 0;
-  while (c + 1 < sh.n_conts && sh.cont_prefix[c + 1] <= i) c++;
-  uint32_t j = i - sh.cont_prefix[c];
-  const uint32_t bmi = sh.cont_bm[c];
-  if (bmi == ~0u) return (sh.cont_key[c] << 16) | (s.u32(sh.cont_data[c] + 2 * j) & 0xFFFFu);
+  const uint32_t* pre = sh.rpre;
+  uint32_t c = 0, hi = sh.n_conts;
+  while (hi - c > 1) {
+    const uint32_t mid = (c + hi) >> 1;
+    if (pre[mid] <= i) c = mid; else hi = mid;
+  }
+  uint32_t j = i - pre[c];
+  const uint32_t bmi = sh.rbm[c], key = sh.rkey[c], data = sh.rdata[c];
+  if (bmi == ~0u) return (key << 16) | (s.u32(data + 2 * j) & 0xFFFFu);
+  const uint16_t* cp = sh.rcp + 64 * bmi;
   uint32_t g = 0;
   for (uint32_t step = 32; step; step >>= 1)
-    if (g + step < 64 && sh.cont_cp[bmi][g + step] <= j) g += step;
-  j -= sh.cont_cp[bmi][g];
+    if (g + step < 64 && cp[g + step] <= j) g += step;
+  j -= cp[g];
   uint32_t w = 16 * g;
-  uint64_t word = s.u64(sh.cont_data[c] + 8 * w);
+  uint64_t word = s.u64(data + 8 * w);
   for (uint32_t pc = __popcll(word); pc <= j && w + 1 < 1024; pc = __popcll(word)) {
     j -= pc;
-    word = s.u64(sh.cont_data[c] + 8 * (++w));
+    word = s.u64(data + 8 * (++w));
   }
   for (uint32_t t = 0; t < j; t++) word &= word - 1;  // drop the j lowest set bits
-  return (sh.cont_key[c] << 16) | (w * 64 + (uint32_t)__builtin_ctzll(word));
+  return (key << 16) | (w * 64 + (uint32_t)__builtin_ctzll(word));
 }
 
 // ---------------------------------------------------------------------------
@@ -563,42 +577,113 @@ __device__ void write_validity(const Src& s, uint32_t vb, uint32_t n, uint64_t r
 // ---------------------------------------------------------------------------
 // the page kernel
 // ---------------------------------------------------------------------------
-// Parses a roaring portable bitmap of bm bytes at r into the container table
-// (array and bitmap containers; cookie 12347 run containers are not written
-// by roaring 0.10.1 and report NYI).  Thread 0 only; total = cardinality.
+// Parses the header of a roaring portable bitmap of bm bytes at r (roaring
+// 0.10.1 serialize_into: cookie 12346, container count, per container
+// (key, card - 1), then per container its data offset; array containers of
+// u16 values, bitmap containers of 1024 u64 words; cookie 12347 run
+// containers are not written by 0.10.1 and report NYI).  Thread 0; *total =
+// cardinality.  The container tables are built afterwards by the whole
+// workgroup (roaring_build).
 template <class Src>
 __device__ bool parse_roaring(const Src& s, Shared& sh, uint32_t r, uint32_t bm, uint32_t* total) {
   if (bm < 8) { set_err(sh, ST_IO); return false; }
   if (s.u32(r) != 12346) { set_err(sh, ST_NYI); return false; }
   const uint32_t nc = s.u32(r + 4);
-  if (nc > kMaxConts || 8 + 8 * (uint64_t)nc > bm) { set_err(sh, ST_NYI); return false; }
-  uint32_t tot = 0, nbm = 0;
+  if (8 + 8 * (uint64_t)nc > bm) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+  uint64_t tot = 0;
+  for (uint32_t c = 0; c < nc; c++) tot += (s.u32(r + 8 + 4 * c) >> 16) + 1;
+  if (tot > 0xFFFFFFFFull) { set_err(sh, ST_OUT_OF_SPEC); return false; }
   sh.n_conts = nc;
-  for (uint32_t c = 0; c < nc; c++) {
-    const uint32_t kc = s.u32(r + 8 + 4 * c);
-    const uint32_t card = (kc >> 16) + 1;
-    const uint32_t off = s.u32(r + 8 + 4 * nc + 4 * c);
-    const uint32_t dbytes = card > 4096 ? 8192u : 2 * card;  // bitmap : array container
-    if (off > bm || dbytes > bm - off) { set_err(sh, ST_OUT_OF_SPEC); return false; }
-    sh.cont_key[c] = kc & 0xFFFF;
-    sh.cont_data[c] = r + off;
-    sh.cont_prefix[c] = tot;
-    sh.cont_bm[c] = ~0u;
-    if (card > 4096) {
-      if (nbm == kMaxBitmapConts) { set_err(sh, ST_NYI); return false; }
-      uint32_t acc = 0;
-      for (uint32_t g = 0; g < 64; g++) {
-        sh.cont_cp[nbm][g] = (uint16_t)acc;
-        for (uint32_t w = 0; w < 16; w++) acc += __popcll(s.u64(r + off + 8 * (16 * g + w)));
-      }
-      if (acc != card) { set_err(sh, ST_OUT_OF_SPEC); return false; }
-      sh.cont_bm[c] = nbm++;
-    }
-    tot += card;
-  }
-  sh.cont_prefix[nc] = tot;
-  *total = tot;
+  sh.roar_r = r;
+  sh.roar_bm = bm;
+  sh.roar_pending = 1;
+  *total = (uint32_t)tot;
   return true;
+}
+
+// Container tables of the bitmap parse_roaring found (all NT threads, after
+// a barrier): keys, data positions, exception prefix and the bitmap
+// checkpoints, one wave per bitmap container (lane g popcounts words
+// 16g..16g+15, a wave scan turns the counts into checkpoints).  In the LDS
+// arrays of Shared when nc <= kMaxConts and at most kMaxBitmapConts bitmap
+// containers, else in the page's HBM region (`tabs`, room for `cap`
+// containers: roar_area_bytes); NYI when neither holds them.
+template <class Src>
+__device__ void roaring_build(const Src& s, Shared& sh, uint8_t* tabs, uint32_t cap) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t nc = sh.n_conts, r = sh.roar_r;
+  __syncthreads();
+  const bool lds = nc <= kMaxConts;
+  if (!lds && (!tabs || nc > cap)) {
+    if (tid == 0) { set_err(sh, ST_NYI); sh.roar_pending = 0; }
+    __syncthreads();
+    return;
+  }
+  uint32_t* key = lds ? sh.cont_key : (uint32_t*)tabs;
+  uint32_t* data = lds ? sh.cont_data : key + cap;
+  uint32_t* pre = lds ? sh.cont_prefix : data + cap;
+  uint32_t* bmx = lds ? sh.cont_bm : pre + cap + 1;
+  uint64_t carry = 0;
+  uint32_t bcarry = 0;
+  for (uint32_t c0 = 0; c0 < nc; c0 += NT) {
+    const uint32_t c = c0 + tid;
+    uint32_t card = 0, isbm = 0;
+    if (c < nc) {
+      const uint32_t kc = s.u32(r + 8 + 4 * c);
+      card = (kc >> 16) + 1;
+      const uint32_t off = s.u32(r + 8 + 4 * nc + 4 * c);
+      const uint32_t dbytes = card > 4096 ? 8192u : 2 * card;  // bitmap : array container
+      const uint32_t bm = sh.roar_bm;
+      if (off > bm || dbytes > bm - off) set_err(sh, ST_OUT_OF_SPEC);
+      key[c] = kc & 0xFFFF;
+      data[c] = r + off;
+      isbm = card > 4096;
+    }
+    uint64_t t64;
+    const uint64_t p = block_excl_scan<uint64_t>(card, sh, &t64) + carry;
+    uint32_t bt;
+    const uint32_t bp = block_excl_scan<uint32_t>(isbm, sh, &bt) + bcarry;
+    if (c < nc) {
+      pre[c] = (uint32_t)p;
+      bmx[c] = isbm ? bp : ~0u;
+    }
+    carry += t64;
+    bcarry += bt;
+  }
+  if (tid == 0) pre[nc] = (uint32_t)carry;
+  const uint32_t nbm = bcarry;
+  const bool cp_lds = nbm <= kMaxBitmapConts;
+  uint16_t* cp = cp_lds ? &sh.cont_cp[0][0] : (tabs ? (uint16_t*)(tabs + align16(4 * (4 * (uint64_t)cap + 1))) : nullptr);
+  __syncthreads();  // pre / bmx of every container (and any bounds error) visible
+  if (!cp || (!cp_lds && nbm > cap)) {
+    if (tid == 0) set_err(sh, ST_NYI);
+  } else if (!sh.err) {
+    // bitmap containers in container order: wave wv takes containers wv, wv + NW, ...
+    for (uint32_t c = wv; c < nc; c += NW) {
+      const uint32_t bi = bmx[c];
+      if (bi == ~0u) continue;
+      uint32_t cnt = 0;
+#pragma unroll 4
+      for (uint32_t w = 0; w < 16; w++) cnt += __popcll(s.u64(data[c] + 8 * (16 * lane + w)));
+      uint32_t x = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+      }
+      cp[64 * bi + lane] = (uint16_t)(x - cnt);
+      if (lane == 63 && x != pre[c + 1] - pre[c]) set_err(sh, ST_OUT_OF_SPEC);
+    }
+  }
+  if (tid == 0) {
+    sh.rkey = key;
+    sh.rdata = data;
+    sh.rpre = pre;
+    sh.rbm = bmx;
+    sh.rcp = cp;
+    sh.roar_pending = 0;
+  }
+  __syncthreads();
 }
 
 // Parses a Freq body [T top][u32 bm][roaring][exceptions stream] whose value
@@ -657,6 +742,14 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 constexpr uint32_t kRing = 4096, kChunk = 1024;
 constexpr uint32_t kInfWaves = SB_INF_WPB;  // waves (jobs in flight) per k_inflate workgroup
 
+// Far-history reads re-read bytes this wave stored and waited for (vmcnt(0))
+// earlier in the same kernel, so workgroup scope suffices: the CU's L1 and
+// its XCD's L2 see their own stores (the gfx942/950 memory model needs no
+// invalidate for same-CU store -> load).  sc1 (16, device scope) made every
+// such read a fabric request of a whole line (FETCH_SIZE, round 3).
+#ifndef SB_FAR_AUX
+#define SB_FAR_AUX 0
+#endif
 typedef const __attribute__((address_space(1))) uint32_t gmem_u32;
 typedef const __attribute__((address_space(1))) uint8_t gmem_u8;
 
@@ -704,6 +797,14 @@ struct WaveWin {
     else return ((gmem_u8*)g)[pos];  // past the window (long length runs)
     return (d >> ((r & 3) * 8)) & 0xFFu;
   }
+  // uniform dword at pos (any alignment), for pos - lo < 504
+  __device__ __forceinline__ uint32_t dw(uint32_t i) const {  // window dword i < 128
+    return i < 64 ? __builtin_amdgcn_readlane(w0, i) : __builtin_amdgcn_readlane(w1, i - 64);
+  }
+  __device__ __forceinline__ uint32_t u32at(uint32_t pos) const {
+    const uint32_t r = pos - lo, i = r >> 2;
+    return __builtin_amdgcn_alignbyte(dw(i + 1), dw(i), r & 3);
+  }
   // byte at pos + lane, for pos - lo < 256
   __device__ __forceinline__ uint32_t lane_byte(uint32_t pos) const {
     const uint32_t r = pos - lo + (threadIdx.x & 63);
@@ -731,12 +832,12 @@ struct WaveOut {
 
   __device__ __forceinline__ uint32_t slot(uint32_t q) const { return RING ? (q & (kRing - 1)) : q; }
   __device__ __forceinline__ uint32_t far8(uint32_t q) const {  // stream byte q < far_limit(), from HBM
-    if (!xf) return __builtin_amdgcn_raw_buffer_load_b8(rs, q, 0, 16);  // sc1: device scope, misses L1
-    const uint32_t w = q < 4 ? w0 : __builtin_amdgcn_raw_buffer_load_b32(rsa, q & ~3u, 0, 16) - xadd;
+    if (!xf) return __builtin_amdgcn_raw_buffer_load_b8(rs, q, 0, SB_FAR_AUX);
+    const uint32_t w = q < 4 ? w0 : __builtin_amdgcn_raw_buffer_load_b32(rsa, q & ~3u, 0, SB_FAR_AUX) - xadd;
     return (w >> (8 * (q & 3))) & 0xFFu;
   }
   __device__ __forceinline__ uint32_t far32(uint32_t a, bool on) const {  // dword at dst-aligned byte a (0 if !on)
-    const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(rsa, on ? a : 0x80000000u, 0, 16);
+    const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(rsa, on ? a : 0x80000000u, 0, SB_FAR_AUX);
     return !xf ? g : a == 0 ? w0 : g - xadd;
   }
   // History below this position is read from HBM: writes of up to one chunk
@@ -1766,13 +1867,111 @@ __device__ bool parse_validity(const Src& s, Shared& sh, uint32_t len, uint32_t 
 // Freq: dict.rs:60-62, freq.rs:79-83).
 enum : uint32_t { CH_LEAF = 0, CH_DICT = 1, CH_FREQ = 2, CH_DICT_FREQ = 3, CH_FREQ_DICT = 4 };
 
+// A page's HBM region (PageDesc.reserved, planned by sb_api's fixed-width
+// plan): the roaring container tables of a Freq page with many containers,
+// then the area a spilled leaf stream expands into.
+__device__ __forceinline__ uint8_t* region_roar(const LaunchArgs& a, const PageDesc& pd, uint32_t* cap) {
+  *cap = 0;
+  if (!a.region || !(pd.reserved & kRegionRoar)) return nullptr;
+  *cap = (uint32_t)roar_cap(pd.num_values);
+  return a.region + (pd.reserved & kRegionOffMask);
+}
+__device__ __forceinline__ uint8_t* region_spill(const LaunchArgs& a, const PageDesc& pd) {
+  if (!a.region || !(pd.reserved & kRegionSpill)) return nullptr;
+  return a.region + (pd.reserved & kRegionOffMask) + ((pd.reserved & kRegionRoar) ? roar_area_bytes(pd.num_values) : 0);
+}
+
+// Values of a parsed page (sh.chain / sh.sub / Dict / Freq state): the leaf
+// stream is read from `ls`, the page's dictionary and roaring bitmap from `s`.
+template <int W, class Src, class LSrc>
+__device__ void decode_values(const Src& s, const LSrc& ls, Shared& sh, const PageDesc& pd, const LaunchArgs& a) {
+  using T = typename VT<W>::T;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = pd.num_values;
+  uint8_t* obase = a.out_values + pd.row_off * W;
+  GSink<W> out{obase, ((uintptr_t)obase & (uintptr_t)(W == 8 ? 15 : 4 * W - 1)) == 0};
+  const uint32_t chain = sh.chain;
+  const Stream leaf = sh.sub;
+  const uint32_t k = sh.dict_k, doff = sh.dict_off;
+
+  if (chain == CH_LEAF) {
+    run_leaf<W>(ls, sh, leaf, [&](uint32_t row, const T* v, uint32_t nv) { out.put4(row, v, nv); });
+    return;
+  }
+  if (chain == CH_DICT) {
+    // Dict: u32 index leaf stream -> gather from the plain dictionary
+    run_leaf<4>(ls, sh, leaf, [&](uint32_t row, const uint32_t* idx, uint32_t nv) {
+      T v[4];
+      bool bad = false;
+#pragma unroll
+      for (uint32_t l = 0; l < 4; l++) {
+        const bool ok = l < nv && idx[l] < k;
+        bad |= (l < nv && !ok);
+        v[l] = ok ? ldv<W>(s, doff + idx[l] * W) : (T)0;
+      }
+      if (bad) set_err(sh, ST_OUT_OF_SPEC);  // data[i] out of range panics
+      out.put4(row, v, nv);
+    });
+    return;
+  }
+  // Freq at the top (CH_FREQ, CH_FREQ_DICT) or under the Dict (CH_DICT_FREQ):
+  // fill every row, then scatter the exceptions at their roaring rows.
+  if (sh.roar_pending) {
+    uint32_t cap;
+    uint8_t* tabs = region_roar(a, pd, &cap);
+    roaring_build(s, sh, tabs, cap);
+    if (sh.err) return;
+  }
+  T fill;
+  if (chain == CH_DICT_FREQ) {
+    const uint32_t ti = (uint32_t)sh.freq_top;
+    if (ti >= k && leaf.n < n) { if (tid == 0) set_err(sh, ST_OUT_OF_SPEC); return; }
+    fill = ti < k ? ldv<W>(s, doff + ti * W) : (T)0;
+  } else {
+    fill = (T)sh.freq_top;
+  }
+  for (uint32_t q = tid; q < (n + 3) / 4; q += NT) {
+    T v[4] = {fill, fill, fill, fill};
+    out.put4(4 * q, v, min(4u, n - 4 * q));
+  }
+  __syncthreads();  // the scatter below overwrites rows of the fill
+  auto scatter = [&](uint32_t i0, const T* x, uint32_t nv) {
+    for (uint32_t l = 0; l < nv; l++) {
+      const uint32_t row = roaring_select(s, sh, i0 + l);
+      if (row < n) out.put(row, x[l]);
+      else set_err(sh, ST_OUT_OF_SPEC);  // output[begin + val] out of range panics
+    }
+  };
+  if (chain == CH_FREQ) {
+    run_leaf<W>(ls, sh, leaf, scatter);
+  } else {
+    run_leaf<4>(ls, sh, leaf, [&](uint32_t i0, const uint32_t* idx, uint32_t nv) {
+      T v[4];
+      bool bad = false;
+#pragma unroll
+      for (uint32_t l = 0; l < 4; l++) {
+        const bool ok = l < nv && idx[l] < k;
+        bad |= (l < nv && !ok);
+        v[l] = ok ? ldv<W>(s, doff + idx[l] * W) : (T)0;
+      }
+      if (bad) set_err(sh, ST_OUT_OF_SPEC);
+      scatter(i0, v, nv);
+    });
+  }
+}
+
+__device__ __forceinline__ bool general_codec(uint32_t c) { return c == 1 || c == 2 || c == 3 || c == 16; }
+
 // MODE 0: main pass (general-codec / Patas leaves are deferred to a work
 // list); MODE 1: deferred pass (the leaf is expanded into LDS at `xpos`,
-// xcap bytes available, then decoded as a plain stream).
+// xcap bytes available, then decoded as a plain stream; a leaf that does not
+// fit -- or any leaf of a page too large to stage (xcap 0) -- is queued for
+// k_inflate / k_zinflate to expand into the page's HBM region, sh.defer = 3);
+// MODE 2: spilled pass (that expanded leaf, read from `lsrc` as a None stream).
 template <int W, bool FLT, int MODE, class Src>
 __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const LaunchArgs& a, uint32_t page,
-                            uint8_t* xbuf = nullptr, uint32_t xpos = 0, uint32_t xcap = 0) {
-  using T = typename VT<W>::T;
+                            uint8_t* xbuf = nullptr, uint32_t xpos = 0, uint32_t xcap = 0,
+                            const GlbSrc* lsrc = nullptr) {
   const uint32_t tid = threadIdx.x;
   const uint32_t len = pd.byte_len, n = pd.num_values;
 
@@ -1780,6 +1979,7 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
     uint32_t p = 0;
     sh.has_valid = 0;
     sh.defer = 0;
+    sh.roar_pending = 0;
     do {
       if (a.nullable && !parse_validity(s, sh, len, n, &p)) break;
       Stream st;
@@ -1815,8 +2015,7 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
       sh.top = st;
       sh.sub = inner;
       sh.chain = chain;
-      sh.defer = 0;
-      if (inner.codec == 1 || inner.codec == 2 || inner.codec == 3 || inner.codec == 16) {
+      if (general_codec(inner.codec)) {
         if (MODE == 0) {
           if (chain == CH_LEAF && (inner.codec == 1 || inner.codec == 3 || (FLT && inner.codec == 16))) {
             // plain values under LZ4 / Snappy, or a Patas stream: k_inflate
@@ -1830,7 +2029,13 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
             const uint32_t slot = atomicAdd(a.defer_count + a.parity, 1u);
             a.defer_list[slot] = page;
           }
+        } else if (MODE == 2) {
+          // expanded by k_inflate / k_zinflate into the region: a None stream there
+          const bool idx_stream = chain == CH_DICT || chain == CH_FREQ_DICT || chain == CH_DICT_FREQ;
+          sh.sub = Stream{0u, 0u, inner.n * (idx_stream ? 4u : (uint32_t)W), inner.n};
         }
+      } else if (MODE == 2) {
+        set_err(sh, ST_OUT_OF_SPEC);  // (the page changed under the plan)
       }
     } while (0);
   }
@@ -1842,101 +2047,57 @@ __device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const 
 
   if constexpr (MODE == 1) {
     Stream lf = sh.sub;
-    if (lf.codec == 1 || lf.codec == 2 || lf.codec == 3 || lf.codec == 16) {
+    if (general_codec(lf.codec)) {
       const bool idx_stream = sh.chain == CH_DICT || sh.chain == CH_FREQ_DICT || sh.chain == CH_DICT_FREQ;
       const uint32_t sw = idx_stream ? 4u : (uint32_t)W;
       const uint64_t bytes = (uint64_t)lf.n * sw;
       const uint64_t zt = (bytes + 15) & ~15ull;  // Zstd: its tables after the expanded stream
       if ((lf.codec == 2 ? zt + kZTablesBytes : bytes) > xcap) {
-        if (tid == 0) set_err(sh, ST_NYI);  // decompressed stream larger than the LDS budget
-      } else if (lf.codec == 16) {  // Patas: every thread of the workgroup
-        const lds_u8* in = (const lds_u8*)((const uint8_t*)s.w + s.base + lf.body);
-        uint32_t st;
-        if (!FLT || idx_stream) st = ST_OUT_OF_SPEC;  // Patas only in decompress_double
-        else st = patas_expand<W>(in, lf.csize, (lds_u8*)xbuf, lf.n, sh);
-        if (st && tid == 0) set_err(sh, st);
-      } else if (tid < 64) {
-        lds_u8* xo = (lds_u8*)xbuf;
-        uint32_t st = ST_OK;
-        if (lf.codec == 1 || lf.codec == 3)
-          st = expand_to_lds(lf.codec, a.chunk + pd.byte_off + lf.body, lf.csize, xo, (uint32_t)bytes);
-        else {
-          st = zs::zstd_to_lds(LdsSrc{s.w, s.base + lf.body}, lf.csize, xo, (uint32_t)bytes, xo + zt,
-                               (uint32_t)(xcap - zt));
+        // the expansion does not fit the LDS: spill it into the page's HBM region
+        if (tid == 0) {
+          uint8_t* sp = region_spill(a, pd);
+          if (lf.codec == 16 && (!FLT || idx_stream)) {
+            set_err(sh, ST_OUT_OF_SPEC);  // Patas only in decompress_double
+          } else if (!sp || bytes > spill_area_bytes(n, W)) {
+            set_err(sh, ST_NYI);
+          } else {
+            const uint32_t slot = atomicAdd(a.spill_count + a.parity, 1u);
+            a.spill_jobs[slot] = InflateJob{pd.byte_off + lf.body, kDstScratch | (uint64_t)(sp - a.region), lf.csize,
+                                            (uint32_t)bytes, lf.codec == 16 ? 16u | (sw << 8) : lf.codec, page};
+            sh.defer = 3;
+          }
         }
-        if (st) set_err(sh, st);
+        __syncthreads();
+        return;
       }
-      __syncthreads();
-      if (sh.err) return;
-      if (tid == 0) sh.sub = Stream{0u, xpos - s.base, (uint32_t)bytes, lf.n};
-      __syncthreads();
+      if constexpr (std::is_same<Src, LdsSrc>::value) {
+        if (lf.codec == 16) {  // Patas: every thread of the workgroup
+          const lds_u8* in = (const lds_u8*)((const uint8_t*)s.w + s.base + lf.body);
+          uint32_t st;
+          if (!FLT || idx_stream) st = ST_OUT_OF_SPEC;  // Patas only in decompress_double
+          else st = patas_expand<W>(in, lf.csize, (lds_u8*)xbuf, lf.n, sh);
+          if (st && tid == 0) set_err(sh, st);
+        } else if (tid < 64) {
+          lds_u8* xo = (lds_u8*)xbuf;
+          uint32_t st = ST_OK;
+          if (lf.codec == 1 || lf.codec == 3)
+            st = expand_to_lds(lf.codec, a.chunk + pd.byte_off + lf.body, lf.csize, xo, (uint32_t)bytes);
+          else {
+            st = zs::zstd_to_lds(LdsSrc{s.w, s.base + lf.body}, lf.csize, xo, (uint32_t)bytes, xo + zt,
+                                 (uint32_t)(xcap - zt));
+          }
+          if (st) set_err(sh, st);
+        }
+        __syncthreads();
+        if (sh.err) return;
+        if (tid == 0) sh.sub = Stream{0u, xpos - s.base, (uint32_t)bytes, lf.n};
+        __syncthreads();
+      }
     }
   }
 
-  uint8_t* obase = a.out_values + pd.row_off * W;
-  GSink<W> out{obase, ((uintptr_t)obase & (uintptr_t)(W == 8 ? 15 : 4 * W - 1)) == 0};
-  const uint32_t chain = sh.chain;
-  const Stream leaf = sh.sub;
-  const uint32_t k = sh.dict_k, doff = sh.dict_off;
-
-  if (chain == CH_LEAF) {
-    run_leaf<W>(s, sh, leaf, [&](uint32_t row, const T* v, uint32_t nv) { out.put4(row, v, nv); });
-    return;
-  }
-  if (chain == CH_DICT) {
-    // Dict: u32 index leaf stream -> gather from the plain dictionary
-    run_leaf<4>(s, sh, leaf, [&](uint32_t row, const uint32_t* idx, uint32_t nv) {
-      T v[4];
-      bool bad = false;
-#pragma unroll
-      for (uint32_t l = 0; l < 4; l++) {
-        const bool ok = l < nv && idx[l] < k;
-        bad |= (l < nv && !ok);
-        v[l] = ok ? ldv<W>(s, doff + idx[l] * W) : (T)0;
-      }
-      if (bad) set_err(sh, ST_OUT_OF_SPEC);  // data[i] out of range panics
-      out.put4(row, v, nv);
-    });
-    return;
-  }
-  // Freq at the top (CH_FREQ, CH_FREQ_DICT) or under the Dict (CH_DICT_FREQ):
-  // fill every row, then scatter the exceptions at their roaring rows.
-  T fill;
-  if (chain == CH_DICT_FREQ) {
-    const uint32_t ti = (uint32_t)sh.freq_top;
-    if (ti >= k && leaf.n < n) { if (tid == 0) set_err(sh, ST_OUT_OF_SPEC); return; }
-    fill = ti < k ? ldv<W>(s, doff + ti * W) : (T)0;
-  } else {
-    fill = (T)sh.freq_top;
-  }
-  for (uint32_t q = tid; q < (n + 3) / 4; q += NT) {
-    T v[4] = {fill, fill, fill, fill};
-    out.put4(4 * q, v, min(4u, n - 4 * q));
-  }
-  __syncthreads();  // the scatter below overwrites rows of the fill
-  auto scatter = [&](uint32_t i0, const T* x, uint32_t nv) {
-    for (uint32_t l = 0; l < nv; l++) {
-      const uint32_t row = roaring_select(s, sh, i0 + l);
-      if (row < n) out.put(row, x[l]);
-      else set_err(sh, ST_OUT_OF_SPEC);  // output[begin + val] out of range panics
-    }
-  };
-  if (chain == CH_FREQ) {
-    run_leaf<W>(s, sh, leaf, scatter);
-  } else {
-    run_leaf<4>(s, sh, leaf, [&](uint32_t i0, const uint32_t* idx, uint32_t nv) {
-      T v[4];
-      bool bad = false;
-#pragma unroll
-      for (uint32_t l = 0; l < 4; l++) {
-        const bool ok = l < nv && idx[l] < k;
-        bad |= (l < nv && !ok);
-        v[l] = ok ? ldv<W>(s, doff + idx[l] * W) : (T)0;
-      }
-      if (bad) set_err(sh, ST_OUT_OF_SPEC);
-      scatter(i0, v, nv);
-    });
-  }
+  if constexpr (MODE == 2) decode_values<W>(s, *lsrc, sh, pd, a);
+  else decode_values<W>(s, s, sh, pd, a);
 }
 
 // Stage [pg, pg + len) into LDS with aligned 16-byte pieces.
@@ -2058,6 +2219,7 @@ __global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
     if (blockIdx.x == 0) {  // the next decode's work lists
       a.defer_count[a.parity ^ 1] = 0;
       a.job_count[a.parity ^ 1] = 0;
+      if (a.spill_count) a.spill_count[a.parity ^ 1] = 0;
     }
   }
   if (light_page(a, pd, page)) return;
@@ -2078,6 +2240,7 @@ __global__ __launch_bounds__(NT) void k_decode_global(LaunchArgs a) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     a.defer_count[a.parity ^ 1] = 0;
     a.job_count[a.parity ^ 1] = 0;
+    if (a.spill_count) a.spill_count[a.parity ^ 1] = 0;
   }
   if (light_page(a, pd, page)) return;
   GlbSrc s{a.chunk + pd.byte_off};
@@ -2097,25 +2260,113 @@ __global__ __launch_bounds__(NT) void k_decode_deferred(LaunchArgs a) {
     const uint32_t page = a.defer_list[i];
     const PageDesc pd = a.pages[page];
     if (threadIdx.x == 0) sh.err = 0;
-    const uint32_t need = ((pd.byte_len + 15 + kStagePad + 15) & ~15u);
-    if (need + 64 > a.stage_bytes) {  // page too large for the deferred LDS budget
+    const uint64_t need = align16((uint64_t)pd.byte_len + 15 + kStagePad);
+    if (need + 64 > a.stage_bytes) {
+      // page too large to stage: parsed from HBM, its leaf spills into the
+      // page's region (NYI when the plan reserved none)
+      decode_page<W, FLT, 1>(GlbSrc{a.chunk + pd.byte_off}, sh, pd, a, page);
       __syncthreads();
-      if (threadIdx.x == 0) a.status[page] = ST_NYI;
+      if (threadIdx.x == 0) a.status[page] = sh.err;
+      __syncthreads();
       continue;
     }
     const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
     LdsSrc s{(const uint32_t*)stage, base};
     uint8_t* xbuf = (uint8_t*)stage + need;
-    decode_page<W, FLT, 1>(s, sh, pd, a, page, xbuf, need, a.stage_bytes - need - kStagePad);
+    decode_page<W, FLT, 1>(s, sh, pd, a, page, xbuf, (uint32_t)need, a.stage_bytes - (uint32_t)need - kStagePad);
     __syncthreads();
     if (threadIdx.x == 0) a.status[page] = sh.err;
     __syncthreads();
   }
 }
 
+// Spilled pages: their leaf was expanded into the page's HBM region by
+// k_inflate / k_zinflate (an error there stands); the page is parsed again
+// from HBM and decoded with that expansion as a None leaf stream.
+template <int W, bool FLT>
+__global__ __launch_bounds__(NT) void k_decode_spilled(LaunchArgs a) {
+  __shared__ Shared sh;
+  const uint32_t count = a.spill_count[a.parity];
+  for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+    const InflateJob jb = a.spill_jobs[i];
+    const uint32_t page = jb.page;
+    if (a.status[page]) continue;
+    const PageDesc pd = a.pages[page];
+    if (threadIdx.x == 0) sh.err = 0;
+    const GlbSrc ls{a.region + (jb.dst & kDstMask)};
+    decode_page<W, FLT, 2>(GlbSrc{a.chunk + pd.byte_off}, sh, pd, a, page, nullptr, 0, 0, &ls);
+    __syncthreads();
+    if (threadIdx.x == 0) a.status[page] = sh.err;
+    __syncthreads();
+  }
+}
+
+// Plan-time cascade probe of a fixed-width page, one thread per page from
+// HBM (the header walk of decode_page without the tables): bit 0 a Freq in
+// the cascade, bit 1 a general-codec / Patas leaf, bit 2 under a Dict / Freq.
+__global__ __launch_bounds__(NT) void k_fix_probe(const uint8_t* chunk, const PageDesc* pages, const uint32_t* list,
+                                                  uint32_t n_list, uint32_t W, int nullable, uint32_t* probe) {
+  const uint32_t i = blockIdx.x * NT + threadIdx.x;
+  if (i >= n_list) return;
+  const PageDesc pd = pages[list[i]];
+  const GlbSrc s{chunk + pd.byte_off};
+  const uint32_t len = pd.byte_len;
+  uint32_t p = 0, bits = 0;
+  auto hdr = [&](uint32_t q, uint32_t* codec, uint32_t* body, uint32_t* cs) {
+    if (q + 9 > len) return false;
+    *codec = s.u8(q);
+    *cs = s.u32(q + 1);
+    *body = q + 9;
+    return *cs <= len - *body;
+  };
+  do {
+    if (nullable) {
+      if (len < 4) break;
+      const uint32_t dl = s.u32(0);
+      if (dl > len - 4) break;
+      p = 4 + dl;
+    }
+    uint32_t c0, b0, cs0, c1, b1, cs1;
+    if (!hdr(p, &c0, &b0, &cs0)) break;
+    uint32_t leaf = c0;
+    if (c0 == 11 || c0 == 13) {
+      bits |= 4;
+      uint32_t q;
+      if (c0 == 11) {
+        q = b0;  // the index stream
+      } else {
+        bits |= 1;
+        if (b0 + W + 4 > len) break;
+        q = b0 + W + 4 + s.u32(b0 + W);  // past top value and bitmap: the exceptions stream
+      }
+      if (!hdr(q, &c1, &b1, &cs1)) break;
+      leaf = c1;
+      if (c1 == 11 || c1 == 13) {  // Dict -> Freq or Freq -> Dict
+        uint32_t c2, b2, cs2;
+        if (c1 == 11) {
+          q = b1;
+        } else {
+          bits |= 1;
+          if (b1 + 8 > len) break;
+          q = b1 + 8 + s.u32(b1 + 4);  // Freq of u32 indices: u32 top, u32 bitmap size
+        }
+        if (!hdr(q, &c2, &b2, &cs2)) break;
+        leaf = c2;
+      }
+    }
+    if (general_codec(leaf)) bits |= 2;
+  } while (0);
+  probe[i] = bits;
+}
+
 template <int W, bool FLT>
 static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
   dim3 block(NT);
+  if (kind == 3) {
+    if (a.n_list == 0) return 0;
+    hipLaunchKernelGGL((k_decode_spilled<W, FLT>), dim3(a.n_list), block, 0, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   if (kind == 2) {
     ensure_lds_attr(k_decode_deferred<W, FLT>, (int)kDeferredLds);
     hipLaunchKernelGGL((k_decode_deferred<W, FLT>), dim3(a.n_list), block, a.stage_bytes, stream, a);
@@ -2243,11 +2494,21 @@ struct BinArgs {
   InflateJob* jobs;
   uint32_t* job_count;
   uint8_t* scratch;
-  uint32_t* lds_need;
-  uint32_t* cls;  // staged list [n] | header-only list [n] | validity bitmap positions [n] | the 2 list lengths
+  uint32_t* lds_need;  // plan time (k_bin_probe): LDS bytes per page
+  uint32_t* cls;  // staged list [n] | header-only list [n] | validity bitmap positions [n] | big list [n] | 3 lengths
+  uint8_t* region;     // big pages' tables (PageDesc.reserved = region offset + 1)
+  uint64_t* rneed;     // plan time (k_bin_probe): region bytes per page
 };
 
 enum : uint32_t { BIN_BASIC = 0, BIN_ONE = 12, BIN_DICT = 11, BIN_FREQ = 13 };
+
+// Rows per emission tile (bin_emit) and the LDS its row tables take.
+constexpr uint32_t kEmitRows = 4 * NT;
+constexpr uint32_t kEmitBytes = (4 * (2 * kEmitRows + 1) + 15) & ~15u;
+// Dynamic LDS of the big-page kernels: Zstd tables, one wave's inflate
+// buffers (ring, input ring, chain tables), the emission tables.
+constexpr uint32_t kBigZt = 0, kBigRing = kZTablesMax, kBigIb = kBigRing + kRing, kBigCt = kBigIb + kIb,
+                   kBigEmit = kBigCt + 2048, kBigLds = kBigEmit + kEmitBytes;
 
 struct BinInfo {
   uint32_t codec;      // leading codec byte
@@ -2255,20 +2516,72 @@ struct BinInfo {
   uint32_t vb, vcs;    // Basic: values stream body / csize
   uint64_t S;          // values bytes of the page
   uint32_t L, top;     // OneValue / Freq top: length and position
-  uint32_t k;          // Dict entries / Freq exceptions consumed (positions < n)
-  uint32_t tab;        // LDS byte offset of the (pos, len) entry table
-  uint32_t xoff, yoff; // LDS byte offsets of the X (offsets / indices) and Y (values) regions
-  uint32_t ztab;       // Zstd: LDS byte offset of the decoder's tables
+  uint32_t k;          // Dict entries / Freq exceptions consumed (rows < n)
+  uint32_t q, end;     // Dict / Freq: first entry record, body end
+  uint32_t tot;        // roaring cardinality (a Freq page, or a Dict's Freq index stream)
+  uint32_t xcodec;     // a Dict's Freq index stream: its exceptions stream's codec
+  uint32_t xoff, yoff; // Basic Zstd: LDS byte offsets of the expanded offsets / values
+  uint32_t ztab;       // LDS byte offset of the Zstd decoder's tables
+  uint32_t emit;       // LDS byte offset of the emission tables
+  uint32_t need;       // LDS bytes the page needs
+  // Extend tables, in LDS or in the page's HBM region: Dict indices (u32 per
+  // row) or the Freq exception-row bitmap + its prefix (u32 per 32 rows each),
+  // the (position, length) entry table, a Dict's expanded Freq exceptions,
+  // the roaring container tables (region only)
+  uint32_t* x;
+  uint2* tab;
+  uint32_t* xex;
+  uint8_t* roar;
 };
 
-// Thread 0: parse validity prefix + binary header; walk Dict entries / Freq
-// exception records into the LDS table (pos, len).  Returns false on error.
+// Table layout of an Extend page from its header counts (offsets from the
+// tables' base; x at 0).  Shared by the plan-time probe and the parse.
+struct BinLayout {
+  uint64_t tab, xex, roar, end;
+};
+__device__ __forceinline__ BinLayout bin_layout(uint32_t codec, uint32_t n, uint32_t k, uint32_t tot, bool xex,
+                                                bool roar) {
+  BinLayout L;
+  uint64_t p = codec == BIN_DICT ? align16(4ull * n) : codec == BIN_FREQ ? align16(8ull * ((n + 31) / 32)) : 0;
+  L.tab = p;
+  const uint64_t ent = codec == BIN_DICT ? k : codec == BIN_FREQ ? min(tot, n) : 0;
+  p = align16(p + 8 * ent);
+  L.xex = p;
+  if (xex) p = align16(p + 4ull * tot);
+  L.roar = p;
+  if (roar) p += roar_area_bytes(n);
+  L.end = p;
+  return L;
+}
+
+// The Freq header of a u32 index stream [u32 top][u32 bm][roaring][exceptions]
+// at body (thread 0): roaring cardinality and the exceptions' codec.
+template <class Src>
+__device__ bool idx_freq_header(const Src& s, uint32_t body, uint32_t end, uint32_t* tot, uint32_t* xcodec) {
+  if (body + 8 > end) return false;
+  const uint32_t bm = s.u32(body + 4), r = body + 8;
+  if (bm > end - r || bm < 8) return false;
+  const uint32_t nc = s.u32(r + 4);
+  if (8 + 8 * (uint64_t)nc > bm) return false;
+  uint64_t t = 0;
+  for (uint32_t c = 0; c < nc; c++) t += (s.u32(r + 8 + 4 * c) >> 16) + 1;
+  if (t > 0xFFFFFFFFull || r + bm + 9 > end) return false;
+  *tot = (uint32_t)t;
+  *xcodec = s.u8(r + bm);
+  return true;
+}
+
+// Thread 0: validity prefix, binary header, and for Extend pages the counts
+// that size the tables and where they go: LDS after the staged page
+// (`lds` non-null: stage_end..lds_bytes) or the page's HBM region (`rgn`).
+// Records are not walked here (walk_records).  Returns false on error.
 template <int OW, class Src>
 __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc& pd, int nullable, uint8_t* lds,
-                          uint32_t stage_end, uint32_t lds_bytes, Stream* idx) {
+                          uint32_t stage_end, uint32_t lds_bytes, uint8_t* rgn, Stream* idx) {
   const uint32_t len = pd.byte_len, n = pd.num_values;
   uint32_t p = 0;
   sh.has_valid = 0;
+  sh.roar_pending = 0;
   if (nullable && !parse_validity(s, sh, len, n, &p)) return false;
   if (p + 9 > len) { set_err(sh, ST_IO); return false; }
   bi.codec = s.u8(p);
@@ -2278,6 +2591,11 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
   bi.xoff = stage_end;
   bi.S = 0;
   bi.k = 0;
+  bi.tot = 0;
+  bi.xcodec = 0;
+  bi.need = stage_end + 64;
+  bi.ztab = 0;
+  bi.end = end;
   if (bi.codec <= 3) {  // Basic: offsets stream then values stream (same codec)
     bi.ob = body;
     bi.ocs = cs;
@@ -2289,58 +2607,41 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     if (bi.vcs > len - bi.vb) { set_err(sh, ST_IO); return false; }
     const uint32_t xb = ((n + 1) * OW + 15) & ~15u;
     bi.yoff = bi.xoff + xb;
-    bi.tab = bi.yoff;
     if (bi.codec == 2) {  // Zstd: offsets into X, values into Y, the decoder's tables after Y
       const uint64_t zt = ((uint64_t)bi.yoff + bi.S + 15) & ~15ull;
-      if (zt + kZTablesBytes + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
+      bi.need = kDeferredLds;  // (the tables take the rest)
+      if (lds && zt + kZTablesBytes + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
       bi.ztab = (uint32_t)zt;
     }
     return true;
   }
+  bool zstd = false, xex = false, roar = false;
+  uint32_t k = 0;
   if (bi.codec == BIN_ONE) {
     if (cs < 4) { set_err(sh, ST_IO); return false; }
     bi.L = s.u32(body);
     if (bi.L > cs - 4) { set_err(sh, ST_OUT_OF_SPEC); return false; }
     bi.top = body + 4;
     bi.S = (uint64_t)n * bi.L;
-    return true;
-  }
-  uint2* tab = nullptr;
-  if (bi.codec == BIN_DICT) {
+  } else if (bi.codec == BIN_DICT) {
     Stream ix;
     if (!parse_stream(s, body, end, n, &ix)) { set_err(sh, ST_IO); return false; }
     if (ix.codec == 11) { set_err(sh, ST_OUT_OF_SPEC); return false; }
     *idx = ix;
     uint32_t q = ix.body + ix.csize;
     if (q + 4 > end) { set_err(sh, ST_IO); return false; }
-    const uint32_t k = s.u32(q);
-    q += 4;
-    bi.tab = bi.xoff + ((n * 4 + 15) & ~15u);  // X = indices
-    bi.ztab = (uint32_t)((bi.tab + 8 * (uint64_t)k + 15) & ~15ull);  // a Zstd index stream's tables
-    if (bi.tab + 8 * (uint64_t)k + kStagePad > lds_bytes ||
-        (ix.codec == 2 && (uint64_t)bi.ztab + kZTablesBytes + kStagePad > lds_bytes)) {
-      set_err(sh, ST_NYI);
-      return false;
-    }
-    tab = (uint2*)(lds + bi.tab);
-#ifdef SB_V_BIN_NOWALK  // timing only: every entry is the first (wrong bytes, consistent sizes)
-    if (k && q + 8 <= end && s.u64(q) <= end - q - 8)
-      for (uint32_t e = 0; e < k; e++) tab[e] = make_uint2(q + 8, (uint32_t)s.u64(q));
-    q = end;
-    if (false)
-#endif
-    for (uint32_t e = 0; e < k; e++) {  // u64 len + bytes per entry
-      if (q + 8 > end) { set_err(sh, ST_IO); return false; }
-      const uint64_t l = s.u64(q);
-      q += 8;
-      if (l > end - q) { set_err(sh, ST_OUT_OF_SPEC); return false; }
-      tab[e] = make_uint2(q, (uint32_t)l);
-      q += (uint32_t)l;
+    k = s.u32(q);
+    bi.q = q + 4;
+    zstd = ix.codec == 2;
+    if (ix.codec == 13) {
+      if (!idx_freq_header(s, ix.body, ix.body + ix.csize, &bi.tot, &bi.xcodec)) { set_err(sh, ST_IO); return false; }
+      if (bi.xcodec == 11 || bi.xcodec == 13) { set_err(sh, ST_OUT_OF_SPEC); return false; }
+      xex = bi.xcodec == 1 || bi.xcodec == 2 || bi.xcodec == 3;
+      zstd = bi.xcodec == 2;
+      roar = true;
     }
     bi.k = k;
-    return true;
-  }
-  if (bi.codec == BIN_FREQ) {
+  } else if (bi.codec == BIN_FREQ) {
     if (cs < 8) { set_err(sh, ST_IO); return false; }
     const uint64_t tl = s.u64(body);
     uint32_t q = body + 8;
@@ -2352,41 +2653,34 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     const uint32_t bm = s.u32(q);
     q += 4;
     if (bm > end - q) { set_err(sh, ST_IO); return false; }
-    uint32_t tot;
-    if (!parse_roaring(s, sh, q, bm, &tot)) return false;
-    q += bm;
-    // exceptions at rows < n are consumed in row order (freq.rs:127-141);
-    // select is increasing: binary search for the first row >= n
-    uint32_t ep = 0, hi_e = tot;
-    while (ep < hi_e) {
-      const uint32_t mid = (ep + hi_e) / 2;
-      if (roaring_select(s, sh, mid) < n) ep = mid + 1;
-      else hi_e = mid;
-    }
-    bi.tab = bi.xoff + ((((n + 31) / 32) * 8 + 15) & ~15u);  // X = row bitmap + prefix
-    if (bi.tab + 8 * (uint64_t)ep + kStagePad > lds_bytes) { set_err(sh, ST_NYI); return false; }
-    tab = (uint2*)(lds + bi.tab);
-    uint64_t sum = 0;
-#ifdef SB_V_BIN_NOWALK
-    if (ep && q + 8 <= end && s.u64(q) <= end - q - 8)
-      for (uint32_t e = 0; e < ep; e++) { tab[e] = make_uint2(q + 8, (uint32_t)s.u64(q)); sum += s.u64(q); }
-    if (false)
-#endif
-    for (uint32_t e = 0; e < ep; e++) {
-      if (q + 8 > end) { set_err(sh, ST_IO); return false; }
-      const uint64_t l = s.u64(q);
-      q += 8;
-      if (l > end - q) { set_err(sh, ST_OUT_OF_SPEC); return false; }
-      tab[e] = make_uint2(q, (uint32_t)l);
-      sum += l;
-      q += (uint32_t)l;
-    }
-    bi.k = ep;
-    bi.S = (uint64_t)(n - ep) * bi.L + sum;
-    return true;
+    if (!parse_roaring(s, sh, q, bm, &bi.tot)) return false;
+    bi.q = q + bm;
+    roar = true;
+  } else {
+    set_err(sh, ST_OUT_OF_SPEC);
+    return false;
   }
-  set_err(sh, ST_OUT_OF_SPEC);
-  return false;
+  const BinLayout L = bin_layout(bi.codec, n, k, bi.tot, xex, roar && !lds);
+  if (lds) {
+    const uint64_t zt = align16(stage_end + L.end);
+    const uint64_t em = zt + (zstd ? kZTablesBytes : 0);
+    const uint64_t need = em + kEmitBytes + kStagePad;
+    if (need > lds_bytes) { set_err(sh, ST_NYI); return false; }  // (the plan made it a big page)
+    bi.ztab = (uint32_t)zt;
+    bi.emit = (uint32_t)em;
+    bi.need = (uint32_t)need;
+    uint8_t* t = lds + stage_end;
+    bi.x = (uint32_t*)t;
+    bi.tab = (uint2*)(t + L.tab);
+    bi.xex = (uint32_t*)(t + L.xex);
+    bi.roar = nullptr;
+  } else {
+    bi.x = (uint32_t*)rgn;
+    bi.tab = (uint2*)(rgn + L.tab);
+    bi.xex = (uint32_t*)(rgn + L.xex);
+    bi.roar = roar ? rgn + L.roar : nullptr;
+  }
+  return true;
 }
 
 template <int OW, class Src>
@@ -2416,17 +2710,103 @@ __device__ void copy_lds_to_global(const uint8_t* lds, uint32_t src, uint8_t* ds
   if (tid < len - done) dst[done + tid] = lds[src + done + tid];
 }
 
-// Materializes a binary Dict's u32 index stream (n values) into LDS xi: leaf
-// codecs via run_leaf, LZ4 / Snappy expanded straight into xi, Freq (top +
-// roaring-placed exceptions of a leaf stream) filled then scattered.
-__device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, uint32_t* xi, const uint8_t* gpage,
-                                uint8_t* ztab, uint32_t ztcap) {
+// One wave walks `count` records [u64 len][len bytes] from page position q
+// (bounded by end) of the page at `pg` in HBM: the chase runs in scalar
+// registers over a register window of the page (WaveWin, readlane), each
+// record's (position, length) goes to lane e % 64 and 64 records at a time
+// to tab (one coalesced store).  binary/dict.rs:95-141 / freq.rs:127-142
+// read the same records one by one.  Returns the status; *sum = the lengths'
+// total.
+__device__ uint32_t walk_records(const uint8_t* pg, uint32_t q, uint32_t end, uint32_t count, uint2* tab,
+                                 uint64_t* sum) {
+  const uint32_t lane = threadIdx.x & 63;
+  *sum = 0;
+  if (!count) return ST_OK;
+  const uint32_t al = (uint32_t)((uintptr_t)pg & 3);
+  WaveWin w;
+  w.init(pg, end);
+  uint32_t pos = q, mp = 0, ml = 0, st = ST_OK;
+  uint64_t s = 0;
+  uint32_t e = 0;
+  for (; e < count; e++) {
+    if (pos + 8 > end) { st = ST_IO; break; }
+    w.slide(pos + al);
+    const uint32_t lo32 = w.u32at(pos + al), hi32 = w.u32at(pos + al + 4);
+    const uint32_t p = pos + 8;
+    if (hi32 || lo32 > end - p) { st = ST_OUT_OF_SPEC; break; }
+    if (lane == (e & 63)) {
+      mp = p;
+      ml = lo32;
+    }
+    s += lo32;
+    pos = p + lo32;
+    if ((e & 63) == 63) tab[e - 63 + lane] = make_uint2(mp, ml);
+  }
+  if (lane < (e & 63)) tab[(e & ~63u) + lane] = make_uint2(mp, ml);
+  *sum = s;
+  return st;
+}
+
+// One wave expands a general-codec stream (LZ4 / Snappy / Zstd) from HBM
+// into HBM, with k_inflate's per-wave LDS (output ring, input ring, chain
+// tables) or the Zstd decoder's tables.
+__device__ uint32_t expand_to_hbm(uint32_t codec, const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t usize,
+                                  uint8_t* lds) {
+  if (codec == 2) return zs::zstd_decode(GlbSrc{src}, csize, dst, usize, (lds_u8*)(lds + kBigZt), kZTablesMax);
+  WaveOut<true> o;
+  o.xf = false;
+  o.xadd = 0;
+  o.skip0 = false;
+  o.w0 = 0;
+  o.ring = (lds_u8*)(lds + kBigRing);
+  o.dst = dst;
+  o.rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)usize, 0x00020000);
+  o.dal = (uint32_t)((uintptr_t)dst & 3);
+  o.rsa = __builtin_amdgcn_make_buffer_rsrc(dst - o.dal, 0, (int)(usize + o.dal), 0x00020000);
+  o.olen = usize;
+  o.op = 0;
+  const uint32_t p0 = (uint32_t)((uintptr_t)src & 3);
+  if (codec == 1) {
+    InRing in;
+    in.g = (gmem_u32*)((uintptr_t)src & ~(uintptr_t)3);
+    in.nd = (p0 + csize + 3) >> 2;
+    in.ib = (lds_u8*)(lds + kBigIb);
+    in.ct = (lds_u8*)(lds + kBigCt);
+    in.seek(p0);
+    return lz4_inflate(in, p0, p0 + csize, o);
+  }
+  if (codec == 3) {
+    WaveWin w;
+    w.init(src, csize);
+    return snappy_wave<true>(w, p0, p0 + csize, o);
+  }
+  return ST_NYI;
+}
+
+// A binary Dict's u32 index stream (n values) into bi.x: leaf codecs via
+// run_leaf; LZ4 / Snappy / Zstd expanded by wave 0 (into LDS for a staged
+// page, straight into the region for a big page); Freq: the top index filled,
+// then the exceptions (a leaf stream, or a general-codec stream expanded
+// into bi.xex first) scattered at their roaring rows.  All NT threads.
+template <class Src>
+__device__ void materialize_idx(const Src& s, Shared& sh, const BinInfo& bi, const Stream ix, const uint8_t* gpage,
+                                uint8_t* lds, uint32_t lds_bytes, uint8_t* biglds) {
+  constexpr bool kLds = std::is_same<Src, LdsSrc>::value;
   const uint32_t tid = threadIdx.x, n = ix.n;
+  uint32_t* xi = bi.x;
+  auto expand = [&](uint32_t codec, uint32_t body, uint32_t csize, uint32_t* dst, uint32_t bytes) -> uint32_t {
+    if constexpr (kLds) {
+      if (codec == 2)
+        return zs::zstd_to_lds(LdsSrc{s.w, s.base + body}, csize, (lds_u8*)dst, bytes, (lds_u8*)(lds + bi.ztab),
+                               lds_bytes - bi.ztab - kStagePad);
+      return expand_to_lds(codec, gpage + body, csize, (lds_u8*)dst, bytes);
+    } else {
+      return expand_to_hbm(codec, gpage + body, csize, (uint8_t*)dst, bytes, biglds);
+    }
+  };
   if (ix.codec == 1 || ix.codec == 2 || ix.codec == 3) {
     if (tid < 64) {
-      const uint32_t st =
-          ix.codec == 2 ? zs::zstd_to_lds(LdsSrc{s.w, s.base + ix.body}, ix.csize, (lds_u8*)xi, 4 * n, (lds_u8*)ztab, ztcap)
-                        : expand_to_lds(ix.codec, gpage + ix.body, ix.csize, (lds_u8*)xi, 4 * n);
+      const uint32_t st = expand(ix.codec, ix.body, ix.csize, xi, 4 * n);
       if (st) set_err(sh, st);
     }
     __syncthreads();
@@ -2434,21 +2814,38 @@ __device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, ui
   }
   if (ix.codec == 13) {
     __shared__ Stream ex;
-    if (tid == 0 && parse_freq(s, sh, ix, 4, &ex)) {
-      if (ex.codec == 11 || ex.codec == 13 || ex.codec == 1 || ex.codec == 2 || ex.codec == 3) set_err(sh, ST_NYI);
+    if (tid == 0) {
+      sh.roar_pending = 0;
+      parse_freq(s, sh, ix, 4, &ex);
     }
     __syncthreads();
     if (sh.err) return;
+    roaring_build(s, sh, bi.roar, bi.roar ? (uint32_t)roar_cap(n) : 0u);
+    if (sh.err) return;
     const uint32_t top = (uint32_t)sh.freq_top;
     for (uint32_t i = tid; i < n; i += NT) xi[i] = top;
+    const bool gen = ex.codec == 1 || ex.codec == 2 || ex.codec == 3;
+    if (gen && tid < 64) {
+      const uint32_t st = expand(ex.codec, ex.body, ex.csize, bi.xex, 4 * ex.n);
+      if (st) set_err(sh, st);
+    }
     __syncthreads();
-    run_leaf<4>(s, sh, ex, [&](uint32_t i0, const uint32_t* v, uint32_t nv) {
+    if (sh.err) return;
+    auto scatter = [&](uint32_t i0, const uint32_t* v, uint32_t nv) {
       for (uint32_t l = 0; l < nv; l++) {
         const uint32_t row = roaring_select(s, sh, i0 + l);
         if (row < n) xi[row] = v[l];
         else set_err(sh, ST_OUT_OF_SPEC);
       }
-    });
+    };
+    if (!gen) {
+      run_leaf<4>(s, sh, ex, scatter);
+    } else if constexpr (kLds) {
+      run_leaf<4>(LdsSrc{s.w, (uint32_t)((const uint8_t*)bi.xex - (const uint8_t*)s.w)}, sh, Stream{0u, 0u, 4 * ex.n, ex.n},
+                  scatter);
+    } else {
+      run_leaf<4>(GlbSrc{(const uint8_t*)bi.xex}, sh, Stream{0u, 0u, 4 * ex.n, ex.n}, scatter);
+    }
     __syncthreads();
     return;
   }
@@ -2456,6 +2853,169 @@ __device__ void materialize_idx(const LdsSrc& s, Shared& sh, const Stream ix, ui
     for (uint32_t l = 0; l < nv; l++) xi[row + l] = v[l];
   });
   __syncthreads();
+}
+
+// A binary Freq page's exceptions (all NT threads, after bin_parse): the
+// roaring tables, the exceptions at rows < n (freq.rs:127-141 consumes them
+// in row order; select is increasing, so a binary search finds the first
+// row >= n), and wave 0's walk of their records.  S = (n - ep) * L + sum.
+template <class Src>
+__device__ void freq_tables(const Src& s, Shared& sh, BinInfo& bi, const PageDesc& pd, const uint8_t* gpage) {
+  const uint32_t n = pd.num_values;
+  roaring_build(s, sh, bi.roar, bi.roar ? (uint32_t)roar_cap(n) : 0u);
+  if (sh.err) return;
+  if (threadIdx.x == 0) {
+    uint32_t ep = 0, hi_e = bi.tot;
+    while (ep < hi_e) {
+      const uint32_t mid = (ep + hi_e) / 2;
+      if (roaring_select(s, sh, mid) < n) ep = mid + 1;
+      else hi_e = mid;
+    }
+    bi.k = ep;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    uint64_t sum;
+    const uint32_t st = walk_records(gpage, bi.q, bi.end, bi.k, bi.tab, &sum);
+    if (st) set_err(sh, st);
+    if (threadIdx.x == 0) bi.S = (uint64_t)(n - bi.k) * bi.L + sum;
+  }
+  __syncthreads();
+}
+
+// A binary Dict page's tables (all NT threads, after bin_parse): wave 0
+// walks the k entry records, then the index stream is materialized; S = the
+// page's values bytes, sum of its rows' entry lengths (an index >= k is
+// out of range, dict.rs:131-139 panics).
+template <class Src>
+__device__ void dict_tables(const Src& s, Shared& sh, BinInfo& bi, const Stream& ix, const PageDesc& pd,
+                            const uint8_t* gpage, uint8_t* lds, uint32_t lds_bytes, uint8_t* biglds, bool sized) {
+  if (threadIdx.x < 64) {
+    uint64_t sum;
+    const uint32_t st = walk_records(gpage, bi.q, bi.end, bi.k, bi.tab, &sum);
+    if (st) set_err(sh, st);
+  }
+  __syncthreads();
+  if (sh.err) return;
+  materialize_idx(s, sh, bi, ix, gpage, lds, lds_bytes, biglds);
+  if (sh.err || !sized) return;
+  const uint32_t k = bi.k;
+  uint64_t part = 0;
+  for (uint32_t i = threadIdx.x; i < pd.num_values; i += NT) {
+    const uint32_t x = bi.x[i];
+    if (x < k) part += bi.tab[x].y;
+    else set_err(sh, ST_OUT_OF_SPEC);
+  }
+  uint64_t tot;
+  block_excl_scan<uint64_t>(part, sh, &tot);
+  if (threadIdx.x == 0) bi.S = tot;
+  __syncthreads();
+}
+
+// A binary Freq page's exception-row bitmap and its prefix popcounts (in
+// bi.x: ceil(n/32) words, then as many prefixes), after freq_tables; all NT
+// threads.  A row's exception rank is then pref[w] + popc(bits[w] & below).
+template <class Src>
+__device__ void freq_rows(const Src& s, Shared& sh, const BinInfo& bi, uint32_t n) {
+  const uint32_t tid = threadIdx.x, nw = (n + 31) / 32;
+  uint32_t* bits = bi.x;
+  uint32_t* pref = bits + nw;
+  for (uint32_t w = tid; w < nw; w += NT) bits[w] = 0;
+  __syncthreads();
+  for (uint32_t e = tid; e < bi.k; e += NT) {
+    const uint32_t row = roaring_select(s, sh, e);
+    atomicOr(&bits[row >> 5], 1u << (row & 31));
+  }
+  __syncthreads();
+  uint32_t carry = 0;
+  for (uint32_t w0 = 0; w0 < nw; w0 += NT) {
+    const uint32_t w = w0 + tid;
+    const uint32_t pc = w < nw ? __popc(bits[w]) : 0u;
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<uint32_t>(pc, sh, &tot);
+    if (w < nw) pref[w] = carry + pre;
+    carry += tot;
+  }
+  __syncthreads();
+}
+
+// Arrow offsets and values bytes of rows [0, n): row i has len_of(i) bytes at
+// page position src_of(i) of `src`.  Offsets[R + i + 1] = V + running length
+// (read_binary's rebase, binary/mod.rs:136-144).  The values go out in
+// 16-byte units aligned to the destination: one binary search over the
+// tile's row starts finds a unit's first row, its bytes are then read in row
+// order; units cut by the page's edges are stored byte by byte.  `ea` is
+// kEmitBytes of LDS for the tile's row starts and source positions.
+template <int OW, class Src, class LenF, class SrcF>
+__device__ void bin_emit(Shared& sh, const Src& src, uint32_t* ea, uint32_t n, uint64_t R, uint64_t V,
+                         const BinArgs& a, LenF len_of, SrcF src_of) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t* rs = ea;                  // kEmitRows + 1 tile-relative row starts
+  uint32_t* rp = ea + kEmitRows + 1;  // kEmitRows source positions
+  uint64_t carry = 0;
+  for (uint32_t r0 = 0; r0 < n; r0 += kEmitRows) {
+    const uint32_t m = min(kEmitRows, n - r0);
+    uint32_t l[4], sp[4];
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t i = 4 * tid + j;
+      l[j] = i < m ? len_of(r0 + i) : 0u;
+      sp[j] = i < m ? src_of(r0 + i) : 0u;
+      tsum += l[j];
+    }
+    uint32_t tot;
+    uint32_t pre = block_excl_scan<uint32_t>(tsum, sh, &tot);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t i = 4 * tid + j;
+      if (i < m) {
+        rs[i] = pre;
+        rp[i] = sp[j] - pre;  // page position of tile byte x of row i = rp[i] + x
+        pre += l[j];
+        bin_put_off(a.out_offsets, R + r0 + i + 1, V + carry + pre, OW);
+      }
+    }
+    if (tid == 0) rs[m] = tot;
+    __syncthreads();
+    uint8_t* d0 = a.out_values + V + carry;
+    const uint32_t head = (uint32_t)((uintptr_t)d0 & 15);
+    const uint32_t nunits = (head + tot + 15) / 16;
+    for (uint32_t u = tid; u < nunits; u += NT) {
+      const int32_t x0 = (int32_t)(16 * u) - (int32_t)head;  // tile byte of the unit's first byte
+      const uint32_t xs = x0 < 0 ? 0u : (uint32_t)x0;
+      uint32_t lo = 0, hi = m;  // the last row starting at or before xs
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rs[mid] <= xs) lo = mid; else hi = mid;
+      }
+      uint32_t row = lo, re = rs[row + 1], base = rp[row];
+      uint32_t wv[4] = {0, 0, 0, 0};
+      bool full = x0 >= 0 && (uint32_t)x0 + 16 <= tot;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int32_t x = x0 + k;
+        if (x < 0 || (uint32_t)x >= tot) continue;
+        while ((uint32_t)x >= re) {
+          row++;
+          re = rs[row + 1];
+          base = rp[row];
+        }
+        wv[k >> 2] |= src.u8(base + (uint32_t)x) << (8 * (k & 3));
+      }
+      uint8_t* d = d0 - head + 16 * u;
+      if (full) {
+        *(u32x4*)d = u32x4{wv[0], wv[1], wv[2], wv[3]};
+      } else {
+        for (int k = 0; k < 16; k++) {
+          const int32_t x = x0 + k;
+          if (x >= 0 && (uint32_t)x < tot) d[k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+        }
+      }
+    }
+    carry += tot;
+    __syncthreads();
+  }
 }
 
 // Header-only pages: Basic pages under LZ4 / Snappy need no staging.  Their
@@ -2497,7 +3057,7 @@ __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int n
 template <int OW>
 __global__ __launch_bounds__(NT) void k_bin_light(BinArgs a) {
   const uint32_t np = a.n_pages;
-  uint32_t *staged = a.cls, *light = a.cls + np, *vbpos = a.cls + 2 * np, *cnt = a.cls + 3 * np;
+  uint32_t *staged = a.cls, *light = a.cls + np, *vbpos = a.cls + 2 * np, *cnt = a.cls + 4 * np;
   for (uint32_t page = blockIdx.x * NT + threadIdx.x; page < np; page += gridDim.x * NT) {
     const PageDesc pd = a.pages[page];
     LightPage lp;
@@ -2550,7 +3110,7 @@ __device__ void copy_glb(uint64_t src, const uint8_t* chunk, uint8_t* dst, uint6
 template <int OW>
 __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
   __shared__ uint32_t bad;
-  const uint32_t np = a.n_pages, nl = a.cls[3 * np + 1], tid = threadIdx.x;
+  const uint32_t np = a.n_pages, nl = a.cls[4 * np + 1], tid = threadIdx.x;
   for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
     const uint32_t page = a.cls[np + i];
     const PageDesc pd = a.pages[page];
@@ -2608,6 +3168,73 @@ __global__ __launch_bounds__(NT) void k_bin_light_out(BinArgs a) {
   }
 }
 
+// Plan time, one thread per page from HBM: the LDS a staged decode of the
+// page needs (bin_parse's layout) and the HBM region its tables need when
+// that exceeds one workgroup's LDS (an Extend page: OneValue / Dict / Freq).
+// Header-only (light) pages need neither.
+template <int OW>
+__global__ __launch_bounds__(NT) void k_bin_probe(BinArgs a) {
+  for (uint32_t page = blockIdx.x * NT + threadIdx.x; page < a.n_pages; page += gridDim.x * NT) {
+    const PageDesc pd = a.pages[page];
+    const GlbSrc s{a.chunk + pd.byte_off};
+    const uint32_t len = pd.byte_len, n = pd.num_values;
+    uint32_t need = 0;
+    uint64_t rneed = 0;
+    LightPage lp;
+    if (!bin_light_parse<OW>(s, len, n, a.nullable, lp)) {
+      const uint64_t stage_end = align16((uint64_t)len + 15 + kStagePad);
+      uint64_t nd = stage_end + 64;
+      uint32_t p = 0;
+      bool ok = true;
+      if (a.nullable) {
+        ok = len >= 4 && s.u32(0) <= len - 4;
+        p = ok ? 4 + s.u32(0) : 0;
+      }
+      ok = ok && p + 9 <= len;
+      const uint32_t codec = ok ? s.u8(p) : 0u, cs = ok ? s.u32(p + 1) : 0u, body = p + 9;
+      ok = ok && cs <= len - body;
+      const uint32_t end = body + cs;
+      if (ok && codec == 2) {
+        nd = kDeferredLds;
+      } else if (ok && (codec == BIN_ONE || codec == BIN_DICT || codec == BIN_FREQ)) {
+        uint32_t k = 0, tot = 0, xcodec = 0;
+        bool zstd = false, xex = false, roar = false;
+        if (codec == BIN_DICT && body + 9 <= end) {
+          const uint32_t ic = s.u8(body), ics = s.u32(body + 1);
+          if (ics <= end - body - 9 && body + 9 + ics + 4 <= end) {
+            k = s.u32(body + 9 + ics);
+            zstd = ic == 2;
+            if (ic == 13 && idx_freq_header(s, body + 9, body + 9 + ics, &tot, &xcodec)) {
+              xex = xcodec == 1 || xcodec == 2 || xcodec == 3;
+              zstd = xcodec == 2;
+              roar = true;
+            }
+          }
+        } else if (codec == BIN_FREQ && body + 8 <= end) {
+          const uint64_t tl = s.u64(body);
+          if (tl <= end - body - 8 && body + 8 + tl + 4 <= end) {
+            const uint32_t r = body + 12 + (uint32_t)tl, bm = s.u32(r - 4);
+            if (bm >= 8 && bm <= end - r) {
+              const uint32_t nc = s.u32(r + 4);
+              uint64_t t = 0;
+              if (8 + 8 * (uint64_t)nc <= bm)
+                for (uint32_t c = 0; c < nc; c++) t += (s.u32(r + 8 + 4 * c) >> 16) + 1;
+              tot = (uint32_t)min<uint64_t>(t, 0xFFFFFFFFull);
+              roar = true;
+            }
+          }
+        }
+        const BinLayout L = bin_layout(codec, n, k, tot, xex, false);
+        nd = align16(stage_end + L.end) + (zstd ? kZTablesBytes : 0) + kEmitBytes + kStagePad;
+        rneed = max<uint64_t>(bin_layout(codec, n, k, tot, xex, roar).end, 16);
+      }
+      need = (uint32_t)min<uint64_t>(nd, 0xFFFFFFFFull);
+    }
+    a.lds_need[page] = need;
+    a.rneed[page] = rneed;
+  }
+}
+
 template <int OW>
 __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
   extern __shared__ u32x4 stage[];
@@ -2615,10 +3242,14 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
   __shared__ BinInfo bi;
   __shared__ Stream idx;
   uint8_t* lds = (uint8_t*)stage;
-  const uint32_t n_staged = a.cls[3 * a.n_pages];
+  const uint32_t np = a.n_pages, n_staged = a.cls[4 * np];
   for (uint32_t i = blockIdx.x; i < n_staged; i += gridDim.x) {
     const uint32_t page = a.cls[i];
     const PageDesc pd = a.pages[page];
+    if (pd.reserved) {  // a big page: its tables live in its HBM region (k_bin_big)
+      if (threadIdx.x == 0) a.cls[3 * np + atomicAdd(&a.cls[4 * np + 2], 1u)] = page;
+      continue;
+    }
     if (threadIdx.x == 0) sh.err = 0;
     const uint32_t stage_end = ((pd.byte_len + 15 + kStagePad) + 15) & ~15u;
     if (stage_end + 64 > a.lds_bytes) {  // page larger than the LDS budget
@@ -2629,35 +3260,23 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
     }
     const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
     LdsSrc s{(const uint32_t*)stage, base};
-    if (threadIdx.x == 0 && bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, &idx) &&
-        (bi.codec == 1 || bi.codec == 3)) {
-      // Basic under LZ4 / Snappy: the offsets stream expands into scratch, the
-      // values stream straight into the values buffer at the page's base
-      const uint32_t slot = atomicAdd(a.job_count, 2u);
-      a.jobs[slot] = InflateJob{pd.byte_off + bi.ob, kDstScratch | ((pd.row_off + page) * OW), bi.ocs,
-                                (pd.num_values + 1) * (uint32_t)OW, bi.codec, page};
-      a.jobs[slot + 1] = InflateJob{pd.byte_off + bi.vb, kDstBinBase | page, bi.vcs, (uint32_t)bi.S, bi.codec, page};
-    }
+    if (threadIdx.x == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, nullptr, &idx);
     __syncthreads();
-    if (a.lds_need && threadIdx.x == 0 && !sh.err) {  // plan time: the LDS this page needs
-      uint32_t need = stage_end + 64;
-      if (bi.codec == 2 || (bi.codec == BIN_DICT && idx.codec == 2)) need = kDeferredLds;  // Zstd tables take the rest
-      else if (bi.codec == BIN_DICT || bi.codec == BIN_FREQ) need = max(need, bi.tab + 8 * bi.k + kStagePad);
-      atomicMax(a.lds_need, need);
-    }
-    if (!sh.err && bi.codec == BIN_DICT) {
-      const uint2* tab = (const uint2*)(lds + bi.tab);
-      const uint32_t k = bi.k;
-      uint32_t* xi = (uint32_t*)(lds + bi.xoff);
-      materialize_idx(s, sh, idx, xi, a.chunk + pd.byte_off, lds + bi.ztab, a.lds_bytes - bi.ztab - kStagePad);
-      uint64_t part = 0;
-      for (uint32_t i = threadIdx.x; i < pd.num_values; i += NT) {
-        if (xi[i] < k) part += tab[xi[i]].y;
-        else set_err(sh, ST_OUT_OF_SPEC);  // data_offsets[i] out of range panics
+    if (!sh.err) {
+      if (bi.codec == 1 || bi.codec == 3) {
+        // Basic under LZ4 / Snappy: the offsets stream expands into scratch, the
+        // values stream straight into the values buffer at the page's base
+        if (threadIdx.x == 0) {
+          const uint32_t slot = atomicAdd(a.job_count, 2u);
+          a.jobs[slot] = InflateJob{pd.byte_off + bi.ob, kDstScratch | ((pd.row_off + page) * OW), bi.ocs,
+                                    (pd.num_values + 1) * (uint32_t)OW, bi.codec, page};
+          a.jobs[slot + 1] = InflateJob{pd.byte_off + bi.vb, kDstBinBase | page, bi.vcs, (uint32_t)bi.S, bi.codec, page};
+        }
+      } else if (bi.codec == BIN_DICT) {
+        dict_tables(s, sh, bi, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, true);
+      } else if (bi.codec == BIN_FREQ) {
+        freq_tables(s, sh, bi, pd, a.chunk + pd.byte_off);
       }
-      uint64_t tot;
-      block_excl_scan<uint64_t>(part, sh, &tot);
-      if (threadIdx.x == 0) bi.S = tot;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2683,36 +3302,31 @@ __global__ __launch_bounds__(NT) void k_bin_scan(BinArgs a) {
   if (threadIdx.x == 0) *a.total = carry;
 }
 
-// Offsets and values for rows whose byte lengths come from len_of(i) and
-// bytes from src_of(i) (LDS position): Dict, Freq and OneValue pages.
-template <int OW, class LenF, class SrcF>
-__device__ void bin_emit_rows(Shared& sh, const uint8_t* lds, uint32_t n, uint64_t R, uint64_t V, const BinArgs& a,
-                              LenF len_of, SrcF src_of) {
-  const uint32_t tid = threadIdx.x;
-  uint64_t carry = 0;
-  for (uint32_t r0 = 0; r0 < n; r0 += NT * 4) {
-    uint32_t l[4];
-    uint64_t tsum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t i = r0 + tid * 4 + j;
-      l[j] = i < n ? len_of(i) : 0u;
-      tsum += l[j];
-    }
-    uint64_t tot;
-    uint64_t pre = block_excl_scan<uint64_t>(tsum, sh, &tot) + carry;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t i = r0 + tid * 4 + j;
-      if (i < n) {
-        uint8_t* dst = a.out_values + V + pre;
-        const uint32_t sp = src_of(i);
-        for (uint32_t b = 0; b < l[j]; b++) dst[b] = lds[sp + b];
-        pre += l[j];
-        bin_put_off(a.out_offsets, R + i + 1, V + pre, OW);
-      }
-    }
-    carry += tot;
+// The Extend rows of a parsed page (OneValue / Dict / Freq) whose tables are
+// built (dict_tables / freq_tables + freq_rows): offsets and values through
+// bin_emit.  All NT threads.
+template <int OW, class Src>
+__device__ void bin_emit_extend(Shared& sh, const Src& s, const BinInfo& bi, uint32_t* ea, uint32_t n, uint64_t R,
+                                uint64_t V, const BinArgs& a) {
+  if (bi.codec == BIN_ONE) {
+    const uint32_t L = bi.L, top = bi.top;
+    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t) { return L; }, [&](uint32_t) { return top; });
+  } else if (bi.codec == BIN_DICT) {
+    const uint32_t* xi = bi.x;
+    const uint2* tab = bi.tab;
+    const uint32_t k = bi.k;
+    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t i) { return xi[i] < k ? tab[xi[i]].y : 0u; },
+                 [&](uint32_t i) { return xi[i] < k ? tab[xi[i]].x : 0u; });
+  } else {  // Freq: exception rows by the bitmap + prefix popcount rank
+    const uint32_t nw = (n + 31) / 32;
+    const uint32_t* bits = bi.x;
+    const uint32_t* pref = bits + nw;
+    const uint2* tab = bi.tab;
+    const uint32_t L = bi.L, top = bi.top;
+    auto rank = [&](uint32_t i) { return pref[i >> 5] + __popc(bits[i >> 5] & ((1u << (i & 31)) - 1)); };
+    auto exc = [&](uint32_t i) { return (bits[i >> 5] >> (i & 31)) & 1u; };
+    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t i) { return exc(i) ? tab[rank(i)].y : L; },
+                 [&](uint32_t i) { return exc(i) ? tab[rank(i)].x : top; });
   }
 }
 
@@ -2724,25 +3338,27 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
   __shared__ Stream idx;
   uint8_t* lds = (uint8_t*)stage;
   const uint32_t tid = threadIdx.x;
-  const uint32_t n_staged = a.cls[3 * a.n_pages];
+  const uint32_t n_staged = a.cls[4 * a.n_pages];
   for (uint32_t i = blockIdx.x; i < n_staged; i += gridDim.x) {
     const uint32_t page = a.cls[i];
     const PageDesc pd = a.pages[page];
+    if (pd.reserved) continue;  // k_bin_big's
     const uint32_t n = pd.num_values;
     const uint64_t R = pd.row_off, V = a.bases[page];
-    if (tid == 0) sh.err = a.status[page];  // sizing errors stand
+    if (tid == 0) {
+      sh.err = a.status[page];  // sizing errors stand
+      if (!sh.err && V + a.sizes[page] > a.values_cap) sh.err = ST_OUT_OF_SPEC;
+    }
     const uint32_t stage_end = ((pd.byte_len + 15 + kStagePad) + 15) & ~15u;
     __syncthreads();
     if (sh.err || stage_end + 64 > a.lds_bytes) {
       __syncthreads();
+      if (tid == 0 && sh.err && !a.status[page]) a.status[page] = sh.err;
       continue;
     }
     const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
     LdsSrc s{(const uint32_t*)stage, base};
-    if (tid == 0) {
-      bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, &idx);
-      if (!sh.err && V + bi.S > a.values_cap) set_err(sh, ST_OUT_OF_SPEC);
-    }
+    if (tid == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, nullptr, &idx);
     __syncthreads();
     if (!sh.err) {
       if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
@@ -2798,52 +3414,89 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
             copy_lds_to_global(lds, base + bi.vb, a.out_values + V, bi.S);
           }
         }
-      } else if (bi.codec == BIN_ONE) {
-        const uint32_t L = bi.L, top = base + bi.top;
-        for (uint32_t i = tid + 1; i <= n; i += NT) bin_put_off(a.out_offsets, R + i, V + (uint64_t)i * L, OW);
-        for (uint64_t j = tid; j < (uint64_t)n * L; j += NT) a.out_values[V + j] = lds[top + (uint32_t)(j % L)];
-      } else if (bi.codec == BIN_DICT) {
-        uint32_t* xi = (uint32_t*)(lds + bi.xoff);
-        materialize_idx(s, sh, idx, xi, a.chunk + pd.byte_off, lds + bi.ztab, a.lds_bytes - bi.ztab - kStagePad);
-        const uint2* tab = (const uint2*)(lds + bi.tab);
-        const uint32_t k = bi.k;
-        if (!sh.err)
-          bin_emit_rows<OW>(sh, lds, n, R, V, a, [&](uint32_t i) { return xi[i] < k ? tab[xi[i]].y : 0u; },
-                            [&](uint32_t i) { return xi[i] < k ? base + tab[xi[i]].x : 0u; });
-      } else {  // Freq: row bitmap of exceptions + prefix popcount -> exception rank
-        uint32_t* bits = (uint32_t*)(lds + bi.xoff);
-        const uint32_t nw = (n + 31) / 32;
-        uint32_t* pref = bits + nw;
-        for (uint32_t w = tid; w < nw; w += NT) bits[w] = 0;
-        __syncthreads();
-        for (uint32_t e = tid; e < bi.k; e += NT) {
-          const uint32_t row = roaring_select(s, sh, e);
-          atomicOr(&bits[row >> 5], 1u << (row & 31));
+      } else {
+        if (bi.codec == BIN_DICT) {
+          dict_tables(s, sh, bi, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, false);
+        } else if (bi.codec == BIN_FREQ) {
+          freq_tables(s, sh, bi, pd, a.chunk + pd.byte_off);
+          if (!sh.err) freq_rows(s, sh, bi, n);
         }
-        __syncthreads();
-        uint64_t carry = 0;
-        for (uint32_t w0 = 0; w0 < nw; w0 += NT) {
-          const uint32_t w = w0 + tid;
-          const uint32_t pc = w < nw ? __popc(bits[w]) : 0u;
-          uint32_t tot;
-          const uint32_t pre = block_excl_scan<uint32_t>(pc, sh, &tot);
-          if (w < nw) pref[w] = (uint32_t)carry + pre;
-          carry += tot;
-        }
-        __syncthreads();
-        const uint2* tab = (const uint2*)(lds + bi.tab);
-        const uint32_t L = bi.L, top = base + bi.top;
-        auto rank = [&](uint32_t i) {
-          const uint32_t word = bits[i >> 5], b = i & 31;
-          return pref[i >> 5] + __popc(word & ((1u << b) - 1));
-        };
-        auto exc = [&](uint32_t i) { return (bits[i >> 5] >> (i & 31)) & 1u; };
-        bin_emit_rows<OW>(sh, lds, n, R, V, a, [&](uint32_t i) { return exc(i) ? tab[rank(i)].y : L; },
-                          [&](uint32_t i) { return exc(i) ? base + tab[rank(i)].x : top; });
+        if (!sh.err) bin_emit_extend<OW>(sh, s, bi, (uint32_t*)(lds + bi.emit), n, R, V, a);
       }
     }
     __syncthreads();
     if (tid == 0) a.status[page] = sh.err;
+    __syncthreads();
+  }
+}
+
+// Big Extend pages (OneValue / Dict / Freq pages whose tables do not fit one
+// workgroup's LDS, e.g. a write/common.rs:54-58 one-page column): read from
+// HBM, tables in the page's HBM region (PageDesc.reserved - 1).  STAGE 0
+// sizes them (entry walk, indices / exception rows into the region); STAGE 1
+// emits offsets and values from those tables.
+template <int OW, int STAGE>
+__global__ __launch_bounds__(NT) void k_bin_big(BinArgs a) {
+  extern __shared__ u32x4 dyn[];
+  __shared__ Shared sh;
+  __shared__ BinInfo bi;
+  __shared__ Stream idx;
+  uint8_t* lds = (uint8_t*)dyn;
+  const uint32_t tid = threadIdx.x, np = a.n_pages, nbig = a.cls[4 * np + 2];
+  for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
+    const uint32_t page = a.cls[3 * np + i];
+    const PageDesc pd = a.pages[page];
+    const uint32_t n = pd.num_values;
+    const GlbSrc s{a.chunk + pd.byte_off};
+    uint8_t* rgn = a.region + (pd.reserved - 1);
+    const uint64_t R = pd.row_off, V = STAGE ? a.bases[page] : 0;
+    if (tid == 0) {
+      sh.err = STAGE ? a.status[page] : 0u;
+      if (STAGE && !sh.err && V + a.sizes[page] > a.values_cap) sh.err = ST_OUT_OF_SPEC;
+    }
+    __syncthreads();
+    if (sh.err) {
+      __syncthreads();
+      if (tid == 0 && STAGE && !a.status[page]) a.status[page] = sh.err;
+      continue;
+    }
+    if (tid == 0) {
+      bin_parse<OW>(s, sh, bi, pd, a.nullable, nullptr, 0, 0, rgn, &idx);
+      if (!sh.err && bi.codec <= 3) set_err(sh, ST_NYI);  // (Basic pages are never big)
+    }
+    __syncthreads();
+    if (!sh.err) {
+      if (STAGE == 0) {
+        if (bi.codec == BIN_DICT) {
+          dict_tables(s, sh, bi, idx, pd, a.chunk + pd.byte_off, nullptr, 0, lds, true);
+        } else if (bi.codec == BIN_FREQ) {
+          freq_tables(s, sh, bi, pd, a.chunk + pd.byte_off);
+          if (!sh.err) freq_rows(s, sh, bi, n);
+        }
+      } else {
+        if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
+        if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);
+        if (bi.codec == BIN_FREQ) {  // the exceptions consumed (the bitmap and walk are in the region)
+          roaring_build(s, sh, bi.roar, (uint32_t)roar_cap(n));
+          if (tid == 0 && !sh.err) {
+            uint32_t ep = 0, hi_e = bi.tot;
+            while (ep < hi_e) {
+              const uint32_t mid = (ep + hi_e) / 2;
+              if (roaring_select(s, sh, mid) < n) ep = mid + 1;
+              else hi_e = mid;
+            }
+            bi.k = ep;
+          }
+          __syncthreads();
+        }
+        if (!sh.err) bin_emit_extend<OW>(sh, s, bi, (uint32_t*)(lds + kBigEmit), n, R, V, a);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      a.status[page] = sh.err;
+      if (STAGE == 0) a.sizes[page] = sh.err ? 0 : bi.S;
+    }
     __syncthreads();
   }
 }
@@ -3530,7 +4183,7 @@ __global__ __launch_bounds__(NT) void k_list_vbase(ListArgs a) {
         const uint64_t vpos = pd.byte_len >= 12 ? 12ull + g.u32(4) + g.u32(8) : ~0ull;
         const bool ok = vpos + 9 <= pd.byte_len;
         a.vpages[p] = PageDesc{pd.byte_off + (ok ? vpos : 0), lbase, ok ? pd.byte_len - (uint32_t)vpos : 0,
-                               ok ? (uint32_t)a.counts[p] : 0, 0};
+                               ok ? (uint32_t)a.counts[p] : 0, a.vpages[p].reserved};
       }
     }
   }
@@ -3582,7 +4235,7 @@ __global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
       // the page's values stream, decoded as a flat non-nullable page of `leaves` values
       if (!a.peek)
         a.vpages[page] = PageDesc{pd.byte_off + (ok ? w.ls.vpos : 0), lbase, ok ? pd.byte_len - w.ls.vpos : 0,
-                                  ok ? leaves_c : 0, 0};
+                                  ok ? leaves_c : 0, a.vpages[page].reserved};
       a.status[page] = err;
       if (page == a.n_pages - 1) {
         const uint64_t tr = rbase + (cnt >> 32), tl = lbase + (uint32_t)cnt;
@@ -3802,7 +4455,7 @@ __global__ __launch_bounds__(NT) void k_nest_walk(NestArgs a) {
           if (!err && carry[d] != a.counts[(uint64_t)page * (D + 1) + d]) err = ST_OUT_OF_SPEC;
         const bool ok = err == 0;
         a.vpages[page] = PageDesc{pd.byte_off + (ok ? w.vpos : 0), base[D], ok ? pd.byte_len - w.vpos : 0,
-                                  ok ? (uint32_t)carry[D] : 0u, 0};
+                                  ok ? (uint32_t)carry[D] : 0u, a.vpages[page].reserved};
         if (page == a.n_pages - 1)  // create_list appends each child's length
           for (uint32_t d = 0; d < D; d++) bin_put_off(a.out_offsets[d], a.totals[d], a.totals[d + 1], (int)a.ow);
       }
@@ -3819,6 +4472,14 @@ int launch_fix_light(const LaunchArgs& a, uint32_t n_pages, int width, bool is_f
   if (!n_pages) return 0;
   hipLaunchKernelGGL(sbk::k_fix_light, dim3((n_pages + sbk::NT - 1) / sbk::NT), dim3(sbk::NT), 0, (hipStream_t)stream,
                      a, n_pages, (uint32_t)width, (uint32_t)is_float, light);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_fix_probe(const uint8_t* chunk, const PageDesc* pages, const uint32_t* list, uint32_t n, int width,
+                     int nullable, uint32_t* probe, void* stream) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(sbk::k_fix_probe, dim3((n + sbk::NT - 1) / sbk::NT), dim3(sbk::NT), 0, (hipStream_t)stream, chunk,
+                     pages, list, n, (uint32_t)width, nullable, probe);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -3843,35 +4504,45 @@ namespace sb {
 int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream) {
   const uint32_t lds = L.lds_bytes ? std::min(L.lds_bytes, kDeferredLds) : kDeferredLds;
   sbk::BinArgs a{L.chunk, L.pages, L.n_pages, L.nullable, L.sizes, L.bases, L.total, L.out_offsets, L.out_values,
-                 L.values_cap, L.out_validity, L.status, lds, L.jobs, L.job_count, L.scratch, L.lds_need, L.cls};
+                 L.values_cap, L.out_validity, L.status, lds, L.jobs, L.job_count, L.scratch, L.lds_need, L.cls,
+                 L.region, L.rneed};
   hipStream_t st = (hipStream_t)stream;
   const dim3 block(sbk::NT);
   // staged passes: one workgroup per listed page (grid-stride), as many
   // resident per CU as the LDS budget allows; header-only pages: one thread
-  // each to classify, one workgroup each to write offsets and validity
+  // each to classify, one workgroup each to write offsets and validity; big
+  // pages: one workgroup each (grid-stride) with their tables in HBM
   const dim3 grid(std::max<uint32_t>(1, L.staged_grid));
   const dim3 cgrid((L.n_pages + sbk::NT - 1) / sbk::NT);
   const dim3 lgrid(std::min<uint32_t>(L.n_pages, 65535u));
+  const dim3 bgrid(std::max<uint32_t>(1, std::min<uint32_t>(L.n_big, 1024u)));
   ensure_lds_attr(sbk::k_bin_size<4>, (int)kDeferredLds);
   ensure_lds_attr(sbk::k_bin_size<8>, (int)kDeferredLds);
   ensure_lds_attr(sbk::k_bin_decode<4>, (int)kDeferredLds);
   ensure_lds_attr(sbk::k_bin_decode<8>, (int)kDeferredLds);
-  if (stage == 0) {
-    if (hipMemsetAsync(L.cls + 3 * (size_t)L.n_pages, 0, 2 * sizeof(uint32_t), st) != hipSuccess) return -1;
+  if (stage == 2) {  // plan time: per-page LDS / region needs
+    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_probe<8>, cgrid, block, 0, st, a);
+    else hipLaunchKernelGGL(sbk::k_bin_probe<4>, cgrid, block, 0, st, a);
+  } else if (stage == 0) {
+    if (hipMemsetAsync(L.cls + 4 * (size_t)L.n_pages, 0, 3 * sizeof(uint32_t), st) != hipSuccess) return -1;
     if (offset_width == 8) {
       hipLaunchKernelGGL(sbk::k_bin_light<8>, cgrid, block, 0, st, a);
       hipLaunchKernelGGL(sbk::k_bin_size<8>, grid, block, lds, st, a);
+      if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<8, 0>), bgrid, block, sbk::kBigLds, st, a);
     } else {
       hipLaunchKernelGGL(sbk::k_bin_light<4>, cgrid, block, 0, st, a);
       hipLaunchKernelGGL(sbk::k_bin_size<4>, grid, block, lds, st, a);
+      if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<4, 0>), bgrid, block, sbk::kBigLds, st, a);
     }
     hipLaunchKernelGGL(sbk::k_bin_scan, dim3(1), block, 0, st, a);
   } else {
     if (offset_width == 8) {
       hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, lds, st, a);
+      if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<8, 1>), bgrid, block, sbk::kBigLds, st, a);
       hipLaunchKernelGGL(sbk::k_bin_light_out<8>, lgrid, block, 0, st, a);
     } else {
       hipLaunchKernelGGL(sbk::k_bin_decode<4>, grid, block, lds, st, a);
+      if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<4, 1>), bgrid, block, sbk::kBigLds, st, a);
       hipLaunchKernelGGL(sbk::k_bin_light_out<4>, lgrid, block, 0, st, a);
     }
   }

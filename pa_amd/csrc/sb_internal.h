@@ -44,6 +44,23 @@ struct PageDesc {
 };
 static_assert(sizeof(PageDesc) == 32, "page table entry is 32 bytes");
 
+// PageDesc.reserved of a fixed-width page: its region in the plan's HBM
+// region buffer (sb_api plan_regions), 0 = none.  The region holds the
+// roaring container tables of a Freq page with more containers than the LDS
+// tables take (kRegionRoar, roar_area_bytes), then the area a leaf stream
+// too large for the deferred pass's LDS expands into (kRegionSpill,
+// spill_area_bytes).
+constexpr uint64_t kRegionRoar = 1ull << 62, kRegionSpill = 1ull << 63, kRegionOffMask = (1ull << 56) - 1;
+__host__ __device__ constexpr uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+// containers of a bitmap whose rows are < n
+__host__ __device__ constexpr uint64_t roar_cap(uint64_t n) { return (n + 65535) >> 16; }
+// keys, data positions, prefix (cap + 1) and bitmap indices (u32), then 64 u16 checkpoints per container
+__host__ __device__ constexpr uint64_t roar_area_bytes(uint64_t n) {
+  return align16(4 * (4 * roar_cap(n) + 1)) + align16(128 * roar_cap(n));
+}
+// an expanded leaf: at most n values of max(W, 4) bytes (Dict indices are u32)
+__host__ __device__ constexpr uint64_t spill_area_bytes(uint64_t n, uint64_t w) { return align16(n * (w < 4 ? 4 : w)); }
+
 // Per-page kernel status word (the kernel never traps).
 enum : uint32_t {
   ST_OK = 0,
@@ -104,10 +121,19 @@ struct LaunchArgs {
   uint32_t* job_count;    // [2]: inflate job counts, double-buffered like defer_count
   InflateJob* jobs;       // CH_LEAF LZ4 / Snappy pages, expanded by k_inflate
   const uint32_t* light;  // per page: 0, or 1 + validity bitmap position of a header-only page (k_fix_light)
+  uint8_t* region;        // the plan's HBM regions (PageDesc.reserved), or nullptr
+  uint32_t* spill_count;  // [2]: spilled leaf jobs, double-buffered like defer_count
+  InflateJob* spill_jobs; // leaves expanded into regions by k_inflate / k_zinflate, then k_decode_spilled
 };
 
-// kind: 0 = LDS-staged pages, 1 = pages read from HBM, 2 = deferred work list
+// kind: 0 = LDS-staged pages, 1 = pages read from HBM, 2 = deferred work list,
+// 3 = spilled work list (a.n_list = its upper bound)
 int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a, void* stream);
+// Plan time: per listed page (one thread each, from HBM) the cascade bits
+// probe[i] = 1 (a Freq in the cascade) | 2 (a general-codec / Patas leaf) |
+// 4 (under a Dict / Freq).
+int launch_fix_probe(const uint8_t* chunk, const PageDesc* pages, const uint32_t* list, uint32_t n, int width,
+                     int nullable, uint32_t* probe, void* stream);
 // Header-only fixed-width pages (LZ4 / Snappy leaf, Float Patas leaf): their
 // inflate jobs and light[] tags, one thread per page, before the staged pass.
 int launch_fix_light(const LaunchArgs& a, uint32_t n_pages, int width, bool is_float, uint32_t* light, void* stream);
@@ -142,10 +168,14 @@ struct BinLaunch {
   uint8_t* scratch;       // expanded offsets streams, (row_off + page) * offset width
   uint32_t lds_bytes;     // dynamic LDS per workgroup (0 = kDeferredLds)
   uint32_t* lds_need;     // sizing pass at plan time: max LDS bytes any page needs
-  uint32_t* cls;          // [3 n_pages + 2]: staged-page list | header-only page list | validity
-                          // bitmap positions | the two list lengths (reset by stage 0)
+  uint32_t* cls;          // [4 n_pages + 3]: staged-page list | header-only page list | validity
+                          // bitmap positions | big-page list | the three list lengths (reset by stage 0)
   uint32_t staged_grid;   // workgroups of the staged passes (any >= 1 is correct)
+  uint8_t* region;        // big Extend pages' tables (PageDesc.reserved = offset + 1), or nullptr
+  uint64_t* rneed;        // stage 2 (plan time) out: region bytes per page; lds_need: LDS bytes per page
+  uint32_t n_big;         // big pages of the plan (0: their kernels are not launched)
 };
+// stage 2: plan-time probe (lds_need / rneed per page).
 int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
 
 // List<primitive> columns: stage 0 = exact sizing pass (one wave per page,

@@ -53,8 +53,10 @@ def check(ctx, s, validity, nullable, page_rows, opts, phys):
     go = go.cpu().numpy().astype(np.int64)
     gv = gv.cpu().numpy().tobytes()[: dec.values_bytes]
     assert dec.values_bytes == len(ev)
-    assert (go == eo).all(), "offsets differ"
-    assert gv == ev, "values differ"
+    bad = np.flatnonzero(go != eo)
+    assert len(bad) == 0, f"{len(bad)} offsets differ, first at {bad[:4]}: {go[bad[:4]]} vs {eo[bad[:4]]}"
+    same = gv == ev
+    assert same, "values differ"
     if nullable:
         g = np.unpackbits(gm.cpu().numpy(), bitorder="little")[: len(s)].astype(bool)
         assert (g == evv).all(), "validity differs"
@@ -98,16 +100,61 @@ def test_binary_page_over_lds_budget(ctx):
     check(ctx, s, v, True, 2048, O.WriteOptions.make(), 13)
 
 
-def test_binary_dict_page_over_lds_budget_reports_nyi(ctx):
-    """A staged (Dict) page whose bytes + expansion exceed one workgroup's LDS
-    reports NotYetImplemented, never a wrong answer."""
+@pytest.mark.parametrize("entries,width", [(800, 200), (1500, 200)], ids=["160KiB", "300KiB"])
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+def test_binary_dict_page_over_lds_budget(ctx, entries, width, nullable):
+    """A Dict page whose dictionary (160 / 300 KiB) plus expansion exceeds one
+    workgroup's LDS is a big page: read from HBM, its entry table and indices
+    in the page's HBM region (binary/dict.rs:95-141), bit-exact."""
+    rng = np.random.default_rng(2)
+    s = [bytes(rng.integers(0, 256, width, dtype=np.uint8)) for _ in range(entries)] * 4
+    v = rng.random(len(s)) > 0.2 if nullable else None
+    assert check(ctx, s, v, nullable, len(s), O.WriteOptions.make(ratio=2.0, forced=O.DICT), 13) == {11}
+
+
+@pytest.mark.parametrize("opt", ["dict", "dict_lz4", "dict_zstd", "freq", "one"])
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+def test_binary_1m_row_single_page(ctx, opt, nullable):
+    """One page over 1M rows (write/common.rs:54-58 with no max_page_size):
+    Dict (indices bitpacked, LZ4, Zstd -- 4 MiB of indices), Freq (16 roaring
+    containers, bitmap ones) and OneValue, each a big page."""
+    rng = np.random.default_rng(21)
+    n = 1 << 20
+    pool = [f"category-{i:04d}".encode() for i in range(300)]
+    if opt == "freq":
+        s = [b"common-value" if r < 0.91 else str(x).encode() for r, x in zip(rng.random(n), rng.integers(0, 10**6, n))]
+    elif opt == "one":
+        s = [b"constant"] * n
+    else:
+        s = [pool[i] for i in rng.integers(0, 300, n)]
+    v = rng.random(n) > 0.1 if nullable else None
+    o = {"dict": dict(ratio=2.0, forced=O.DICT), "dict_lz4": dict(forced=O.DICT, default_codec=O.LZ4),
+         "dict_zstd": dict(forced=O.DICT, default_codec=O.ZSTD), "freq": dict(ratio=2.0, forced=O.FREQ),
+         "one": dict(ratio=2.0)}[opt]
+    codecs = check(ctx, s, v, nullable, n, O.WriteOptions.make(**o), 13)
+    assert codecs == {{"freq": 13, "one": 12}.get(opt, 11)}
+
+
+@pytest.mark.parametrize("codec", ["lz4", "zstd", "snappy"])
+@pytest.mark.parametrize("rows", [8000, 300_000])
+def test_binary_dict_freq_general_exceptions(ctx, codec, rows):
+    """A Dict whose index stream is Freq and whose exceptions stream is a
+    general codec (binary/dict.rs:80-81 forbids only Dict below a Dict,
+    integer/freq.rs:80-83 only Freq below a Freq): the exceptions expand into
+    LDS (small page) or the page's region (big page), then scatter."""
     import pa_amd
 
-    rng = np.random.default_rng(2)
-    s = [bytes(rng.integers(0, 256, 200, dtype=np.uint8)) for _ in range(800)] * 4  # a 160 KiB dictionary
-    with pytest.raises(pa_amd.StrawboatError) as e:
-        check(ctx, s, None, False, len(s), O.WriteOptions.make(ratio=2.0, forced=O.DICT), 13)
-    assert e.value.status == 2
+    rng = np.random.default_rng(5)
+    pool = [f"s{i:05d}".encode() for i in range(400)]
+    s = [pool[0] if r < 0.95 else pool[int(x)] for r, x in zip(rng.random(rows), rng.integers(1, 400, rows))]
+    dc = {"lz4": O.LZ4, "zstd": O.ZSTD, "snappy": O.SNAPPY}[codec]
+    vals, offs = pa_amd.binary.strings_to_arrow(s)
+    pg = O.write_binary_page(vals, offs, None, False, O.WriteOptions.make(ratio=2.0, forced=O.DICT, default_codec=dc),
+                             offset_width=4, parent_values_len=len(vals))
+    ib = 18
+    bm = int.from_bytes(pg[ib + 4:ib + 8], "little")
+    assert pg[0] == 11 and pg[9] == 13 and pg[ib + 8 + bm] == dc  # Dict -> Freq -> general exceptions
+    check(ctx, s, None, False, rows, O.WriteOptions.make(ratio=2.0, forced=O.DICT, default_codec=dc), 13)
 
 
 @pytest.mark.parametrize("page_rows", [1, 777, 8192])

@@ -76,7 +76,7 @@ def _decode(kind, chunk, metas, sh, gpu):
     return o, v, None
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, need_gpu=False):
     import torch
     import torch.distributed as dist
 
@@ -86,6 +86,9 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     gpu = torch.cuda.is_available()
+    if need_gpu and not gpu:
+        q.put((rank, {"gpu": False}, 0.0))
+        return
     ok = {}
     for kind, (chunk, metas) in zip(("int", "utf8", "list"), _columns()):
         shards = pa_amd.shard_pages(metas, world)
@@ -122,12 +125,11 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_page_shards_reassemble(world):
+def _run(world, need_gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, need_gpu)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
@@ -137,6 +139,25 @@ def test_page_shards_reassemble(world):
     for _, ok, _ in res:
         assert ok == {"int": True, "utf8": True, "list": True}, ok
     assert all(t == float(world) for _, _, t in res)
+
+
+@pytest.mark.parametrize("world", [2])
+def test_page_shards_reassemble(world):
+    _run(world, False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2])
+def test_page_shards_reassemble_gpu(world):
+    """The same under a real process group with both ranks on the box's GPU:
+    every rank plans and decodes its page range with pa_amd's HIP decoders
+    (for_shard), the bases come from the all-gather, and the reassembled
+    columns match the oracle's whole-column decode."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(world, True)
 
 
 def test_exclusive_bases():
