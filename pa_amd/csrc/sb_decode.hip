@@ -94,13 +94,18 @@ struct LdsSrc {
 // words are assembled from the aligned dwords that contain them, so no read
 // leaves the bytes the page owns.
 struct GlbSrc {
-  const uint8_t* p;
+  typedef const __attribute__((address_space(1))) uint8_t g8;
+  typedef const __attribute__((address_space(1))) uint32_t g32;
+  g8* p;  // global address space: global_load, not flat
+  __device__ __forceinline__ GlbSrc() : p(nullptr) {}
+  __device__ __forceinline__ GlbSrc(const uint8_t* q) : p((g8*)q) {}
+  __device__ __forceinline__ GlbSrc(g8* q) : p(q) {}
   __device__ __forceinline__ GlbSrc at(uint32_t o) const { return GlbSrc{p + o}; }
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
   __device__ __forceinline__ uint32_t u32(uint32_t i) const {
-    uintptr_t a = (uintptr_t)(p + i);
-    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
-    uint32_t sh = (uint32_t)(a & 3);
+    const uintptr_t a = (uintptr_t)(p + i);
+    g32* q = (g32*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
     if (sh == 0) return q[0];
     return __builtin_amdgcn_alignbyte(q[1], q[0], sh);
   }
@@ -160,6 +165,7 @@ struct Shared {
   uint64_t freq_top;
   uint32_t n_conts;
   uint32_t roar_r, roar_bm, roar_pending;  // position and size of the portable bitmap; tables still to build
+  uint32_t roar_lds, cp_lds;              // tables / checkpoints in the arrays below (else the region)
   uint32_t* rkey;                         // container keys
   uint32_t* rdata;                        // source position of each container's data
   uint32_t* rpre;                         // exceptions before each container (n_conts + 1)
@@ -386,7 +392,7 @@ __device__ __forceinline__ uint32_t rle_find(const Src& s, const Shared& sh, con
 // workgroup call this uniformly.  Dict and Freq are handled one level up.
 // ---------------------------------------------------------------------------
 template <int SW, class Src, class Fn>
-__device__ void run_leaf(const Src& s, Shared& sh, const Stream st, Fn&& fn) {
+__device__ __forceinline__ void run_leaf(const Src& s, Shared& sh, const Stream st, Fn&& fn) {
   using T = typename VT<SW>::T;
   const uint32_t tid = threadIdx.x;
   const uint32_t nq = (st.n + 3) >> 2;
@@ -513,7 +519,7 @@ __device__ void run_leaf(const Src& s, Shared& sh, const Stream st, Fn&& fn) {
 
 // Parse a nested [codec][csize][usize] header at p (bounded by end).
 template <class Src>
-__device__ bool parse_stream(const Src& s, uint32_t p, uint32_t end, uint32_t n, Stream* st) {
+__device__ __forceinline__ bool parse_stream(const Src& s, uint32_t p, uint32_t end, uint32_t n, Stream* st) {
   if (p + 9 > end) return false;
   st->codec = s.u8(p);
   st->csize = s.u32(p + 1);
@@ -528,20 +534,41 @@ __device__ bool parse_stream(const Src& s, uint32_t p, uint32_t end, uint32_t n,
 // exception prefix (a 1M-row page has 16 containers, a 100M-row one 1526).
 template <class Src>
 __device__ __forceinline__ uint32_t roaring_select(const Src& s, const Shared& sh, uint32_t i) {
-  const uint32_t* pre = sh.rpre;
-  uint32_t c = 0, hi = sh.n_conts;
-  while (hi - c > 1) {
-    const uint32_t mid = (c + hi) >> 1;
-    if (pre[mid] <= i) c = mid; else hi = mid;
+  typedef const __attribute__((address_space(1))) uint32_t g32;
+  typedef const __attribute__((address_space(1))) uint16_t g16;
+  uint32_t c = 0, hi = sh.n_conts, j, bmi, key, data;
+  if (sh.roar_lds) {  // tables in Shared (ds_ reads)
+    while (hi - c > 1) {
+      const uint32_t mid = (c + hi) >> 1;
+      if (sh.cont_prefix[mid] <= i) c = mid; else hi = mid;
+    }
+    j = i - sh.cont_prefix[c];
+    bmi = sh.cont_bm[c];
+    key = sh.cont_key[c];
+    data = sh.cont_data[c];
+  } else {  // tables in the page's HBM region (global_ reads)
+    g32* pre = (g32*)sh.rpre;
+    while (hi - c > 1) {
+      const uint32_t mid = (c + hi) >> 1;
+      if (pre[mid] <= i) c = mid; else hi = mid;
+    }
+    j = i - pre[c];
+    bmi = ((g32*)sh.rbm)[c];
+    key = ((g32*)sh.rkey)[c];
+    data = ((g32*)sh.rdata)[c];
   }
-  uint32_t j = i - pre[c];
-  const uint32_t bmi = sh.rbm[c], key = sh.rkey[c], data = sh.rdata[c];
   if (bmi == ~0u) return (key << 16) | (s.u32(data + 2 * j) & 0xFFFFu);
-  const uint16_t* cp = sh.rcp + 64 * bmi;
   uint32_t g = 0;
-  for (uint32_t step = 32; step; step >>= 1)
-    if (g + step < 64 && cp[g + step] <= j) g += step;
-  j -= cp[g];
+  if (sh.cp_lds) {
+    for (uint32_t step = 32; step; step >>= 1)
+      if (g + step < 64 && sh.cont_cp[bmi][g + step] <= j) g += step;
+    j -= sh.cont_cp[bmi][g];
+  } else {
+    g16* cp = (g16*)sh.rcp + 64 * bmi;
+    for (uint32_t step = 32; step; step >>= 1)
+      if (g + step < 64 && cp[g + step] <= j) g += step;
+    j -= cp[g];
+  }
   uint32_t w = 16 * g;
   uint64_t word = s.u64(data + 8 * w);
   for (uint32_t pc = __popcll(word); pc <= j && w + 1 < 1024; pc = __popcll(word)) {
@@ -556,7 +583,7 @@ __device__ __forceinline__ uint32_t roaring_select(const Src& s, const Shared& s
 // validity: copy the page's def-level bitmap to bit offset row_off
 // ---------------------------------------------------------------------------
 template <class Src>
-__device__ void write_validity(const Src& s, uint32_t vb, uint32_t n, uint64_t row_off, uint32_t* out) {
+__device__ __forceinline__ void write_validity(const Src& s, uint32_t vb, uint32_t n, uint64_t row_off, uint32_t* out) {
   if (n == 0) return;
   const uint64_t fw = row_off >> 5, lw = (row_off + n - 1) >> 5;
   for (uint64_t w = fw + threadIdx.x; w <= lw; w += NT) {
@@ -585,7 +612,7 @@ __device__ void write_validity(const Src& s, uint32_t vb, uint32_t n, uint64_t r
 // cardinality.  The container tables are built afterwards by the whole
 // workgroup (roaring_build).
 template <class Src>
-__device__ bool parse_roaring(const Src& s, Shared& sh, uint32_t r, uint32_t bm, uint32_t* total) {
+__device__ __forceinline__ bool parse_roaring(const Src& s, Shared& sh, uint32_t r, uint32_t bm, uint32_t* total) {
   if (bm < 8) { set_err(sh, ST_IO); return false; }
   if (s.u32(r) != 12346) { set_err(sh, ST_NYI); return false; }
   const uint32_t nc = s.u32(r + 4);
@@ -609,7 +636,7 @@ __device__ bool parse_roaring(const Src& s, Shared& sh, uint32_t r, uint32_t bm,
 // containers, else in the page's HBM region (`tabs`, room for `cap`
 // containers: roar_area_bytes); NYI when neither holds them.
 template <class Src>
-__device__ void roaring_build(const Src& s, Shared& sh, uint8_t* tabs, uint32_t cap) {
+__device__ __forceinline__ void roaring_build(const Src& s, Shared& sh, uint8_t* tabs, uint32_t cap) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t nc = sh.n_conts, r = sh.roar_r;
   __syncthreads();
@@ -681,6 +708,8 @@ __device__ void roaring_build(const Src& s, Shared& sh, uint8_t* tabs, uint32_t 
     sh.rpre = pre;
     sh.rbm = bmx;
     sh.rcp = cp;
+    sh.roar_lds = lds;
+    sh.cp_lds = cp_lds;
     sh.roar_pending = 0;
   }
   __syncthreads();
@@ -689,7 +718,7 @@ __device__ void roaring_build(const Src& s, Shared& sh, uint8_t* tabs, uint32_t 
 // Parses a Freq body [T top][u32 bm][roaring][exceptions stream] whose value
 // width is `vw` (integer/freq.rs:88-123).  Thread 0 only.
 template <class Src>
-__device__ bool parse_freq(const Src& s, Shared& sh, const Stream& st, uint32_t vw, Stream* ex) {
+__device__ __forceinline__ bool parse_freq(const Src& s, Shared& sh, const Stream& st, uint32_t vw, Stream* ex) {
   const uint32_t e = st.body + st.csize;
   if (st.body + vw + 4 > e) { set_err(sh, ST_IO); return false; }
   sh.freq_top = vw == 8 ? s.u64(st.body) : vw == 4 ? s.u32(st.body) : vw == 2 ? (s.u32(st.body) & 0xFFFFu) : s.u8(st.body);
@@ -703,7 +732,7 @@ __device__ bool parse_freq(const Src& s, Shared& sh, const Stream& st, uint32_t 
 
 // Parses a Dict body [u32 indices stream][u32 k][k * T] (integer/dict.rs:75-103).
 template <class Src>
-__device__ bool parse_dict(const Src& s, Shared& sh, const Stream& st, uint32_t vw, Stream* ix) {
+__device__ __forceinline__ bool parse_dict(const Src& s, Shared& sh, const Stream& st, uint32_t vw, Stream* ix) {
   const uint32_t end = st.body + st.csize;
   if (!parse_stream(s, st.body, end, st.n, ix)) { set_err(sh, ST_IO); return false; }
   const uint32_t e = ix->body + ix->csize;
@@ -1835,7 +1864,7 @@ __device__ uint32_t patas_expand(const lds_u8* in, uint32_t ilen, lds_u8* out, u
 // fewer than n bits is OutOfSpec; def_len 0 pushes nothing, which only an
 // empty page survives.  Thread 0; advances *p past the prefix.
 template <class Src>
-__device__ bool parse_validity(const Src& s, Shared& sh, uint32_t len, uint32_t n, uint32_t* pp) {
+__device__ __forceinline__ bool parse_validity(const Src& s, Shared& sh, uint32_t len, uint32_t n, uint32_t* pp) {
   uint32_t p = *pp;
   if (p + 4 > len) { set_err(sh, ST_IO); return false; }
   const uint32_t def_len = s.u32(p);
@@ -1884,7 +1913,7 @@ __device__ __forceinline__ uint8_t* region_spill(const LaunchArgs& a, const Page
 // Values of a parsed page (sh.chain / sh.sub / Dict / Freq state): the leaf
 // stream is read from `ls`, the page's dictionary and roaring bitmap from `s`.
 template <int W, class Src, class LSrc>
-__device__ void decode_values(const Src& s, const LSrc& ls, Shared& sh, const PageDesc& pd, const LaunchArgs& a) {
+__device__ __forceinline__ void decode_values(const Src& s, const LSrc& ls, Shared& sh, const PageDesc& pd, const LaunchArgs& a) {
   using T = typename VT<W>::T;
   const uint32_t tid = threadIdx.x;
   const uint32_t n = pd.num_values;
@@ -1969,7 +1998,7 @@ __device__ __forceinline__ bool general_codec(uint32_t c) { return c == 1 || c =
 // k_inflate / k_zinflate to expand into the page's HBM region, sh.defer = 3);
 // MODE 2: spilled pass (that expanded leaf, read from `lsrc` as a None stream).
 template <int W, bool FLT, int MODE, class Src>
-__device__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const LaunchArgs& a, uint32_t page,
+__device__ __forceinline__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const LaunchArgs& a, uint32_t page,
                             uint8_t* xbuf = nullptr, uint32_t xpos = 0, uint32_t xcap = 0,
                             const GlbSrc* lsrc = nullptr) {
   const uint32_t tid = threadIdx.x;
@@ -2477,6 +2506,12 @@ __global__ __launch_bounds__(64) void k_zinflate(InflateLaunch a) {
 // offsets, values and validity.  A workgroup holds its page, the expanded
 // offsets / index stream, the expanded values and the entry table in LDS.
 // ===========================================================================
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
 struct BinArgs {
   const uint8_t* chunk;
   const PageDesc* pages;
@@ -2524,14 +2559,27 @@ struct BinInfo {
   uint32_t ztab;       // LDS byte offset of the Zstd decoder's tables
   uint32_t emit;       // LDS byte offset of the emission tables
   uint32_t need;       // LDS bytes the page needs
-  // Extend tables, in LDS or in the page's HBM region: Dict indices (u32 per
-  // row) or the Freq exception-row bitmap + its prefix (u32 per 32 rows each),
-  // the (position, length) entry table, a Dict's expanded Freq exceptions,
-  // the roaring container tables (region only)
-  uint32_t* x;
-  uint2* tab;
-  uint32_t* xex;
-  uint8_t* roar;
+  // Extend tables (offsets from the tables' base: the LDS after the staged
+  // page, or the page's HBM region): Dict indices (u32 per row) or the Freq
+  // exception-row bitmap + its prefix (u32 per 32 rows each) at 0, the
+  // (position, length) entry table, a Dict's expanded Freq exceptions, the
+  // roaring container tables (region only)
+  uint32_t tb;         // LDS: byte offset of the tables' base
+  uint64_t otab, oxex, oroar;
+};
+
+// Typed table pointers: LDS (address space 3) for a staged page, global
+// (address space 1) for a big page's region, so every access is a ds_ or a
+// global_ instruction rather than a flat one.
+template <bool L, class T>
+using mptr = typename std::conditional<L, __attribute__((address_space(3))) T*, __attribute__((address_space(1))) T*>::type;
+template <class Src>
+constexpr bool kLdsSrc = std::is_same<Src, LdsSrc>::value;
+template <bool L>
+struct TabBase {
+  typename std::conditional<L, lds_u8*, __attribute__((address_space(1))) uint8_t*>::type b;
+  template <class T>
+  __device__ __forceinline__ mptr<L, T> at(uint64_t off) const { return (mptr<L, T>)(b + off); }
 };
 
 // Table layout of an Extend page from its header counts (offsets from the
@@ -2573,11 +2621,11 @@ __device__ bool idx_freq_header(const Src& s, uint32_t body, uint32_t end, uint3
 
 // Thread 0: validity prefix, binary header, and for Extend pages the counts
 // that size the tables and where they go: LDS after the staged page
-// (`lds` non-null: stage_end..lds_bytes) or the page's HBM region (`rgn`).
+// (`lds`: stage_end..lds_bytes) or the page's HBM region (lds false).
 // Records are not walked here (walk_records).  Returns false on error.
 template <int OW, class Src>
-__device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc& pd, int nullable, uint8_t* lds,
-                          uint32_t stage_end, uint32_t lds_bytes, uint8_t* rgn, Stream* idx) {
+__device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc& pd, int nullable, bool lds,
+                          uint32_t stage_end, uint32_t lds_bytes, Stream* idx) {
   const uint32_t len = pd.byte_len, n = pd.num_values;
   uint32_t p = 0;
   sh.has_valid = 0;
@@ -2661,6 +2709,9 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     return false;
   }
   const BinLayout L = bin_layout(bi.codec, n, k, bi.tot, xex, roar && !lds);
+  bi.otab = L.tab;
+  bi.oxex = L.xex;
+  bi.oroar = roar && !lds ? L.roar : ~0ull;
   if (lds) {
     const uint64_t zt = align16(stage_end + L.end);
     const uint64_t em = zt + (zstd ? kZTablesBytes : 0);
@@ -2669,16 +2720,7 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
     bi.ztab = (uint32_t)zt;
     bi.emit = (uint32_t)em;
     bi.need = (uint32_t)need;
-    uint8_t* t = lds + stage_end;
-    bi.x = (uint32_t*)t;
-    bi.tab = (uint2*)(t + L.tab);
-    bi.xex = (uint32_t*)(t + L.xex);
-    bi.roar = nullptr;
-  } else {
-    bi.x = (uint32_t*)rgn;
-    bi.tab = (uint2*)(rgn + L.tab);
-    bi.xex = (uint32_t*)(rgn + L.xex);
-    bi.roar = roar ? rgn + L.roar : nullptr;
+    bi.tb = stage_end;
   }
   return true;
 }
@@ -2710,40 +2752,65 @@ __device__ void copy_lds_to_global(const uint8_t* lds, uint32_t src, uint8_t* ds
   if (tid < len - done) dst[done + tid] = lds[src + done + tid];
 }
 
-// One wave walks `count` records [u64 len][len bytes] from page position q
-// (bounded by end) of the page at `pg` in HBM: the chase runs in scalar
-// registers over a register window of the page (WaveWin, readlane), each
-// record's (position, length) goes to lane e % 64 and 64 records at a time
-// to tab (one coalesced store).  binary/dict.rs:95-141 / freq.rs:127-142
-// read the same records one by one.  Returns the status; *sum = the lengths'
+// One wave finds `count` records [u64 len][len bytes] from page position q
+// (bounded by end) and writes tab[e] = position of its bytes | length << 32; the
+// reference reads them one by one (binary/dict.rs:95-141, freq.rs:127-142).
+// A window of 255 byte positions after the current record start: every lane
+// sizes the records that would start at 4 of them (successor x + 8 + len,
+// 0xFF when it leaves the window or the header is not a record), wave_chain
+// composes the successor tables and lane k gets the k-th record's start;
+// lanes then check their record and write its entry.  A window yields every
+// record it holds (at least one).  Returns the status; *sum = the lengths'
 // total.
-__device__ uint32_t walk_records(const uint8_t* pg, uint32_t q, uint32_t end, uint32_t count, uint2* tab,
-                                 uint64_t* sum) {
+template <class Src, class TabP>
+__device__ uint32_t walk_records(const Src& s, uint32_t q, uint32_t end, uint32_t count, TabP tab, uint64_t* sum) {
   const uint32_t lane = threadIdx.x & 63;
-  *sum = 0;
-  if (!count) return ST_OK;
-  const uint32_t al = (uint32_t)((uintptr_t)pg & 3);
-  WaveWin w;
-  w.init(pg, end);
-  uint32_t pos = q, mp = 0, ml = 0, st = ST_OK;
-  uint64_t s = 0;
-  uint32_t e = 0;
-  for (; e < count; e++) {
-    if (pos + 8 > end) { st = ST_IO; break; }
-    w.slide(pos + al);
-    const uint32_t lo32 = w.u32at(pos + al), hi32 = w.u32at(pos + al + 4);
-    const uint32_t p = pos + 8;
-    if (hi32 || lo32 > end - p) { st = ST_OUT_OF_SPEC; break; }
-    if (lane == (e & 63)) {
-      mp = p;
-      ml = lo32;
+  uint64_t part = 0;
+  uint32_t st = ST_OK;
+  for (uint32_t e = 0, p = q; e < count;) {
+    uint32_t t1 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t x = 4 * lane + k, pos = p + x;
+      uint32_t d = 0xFF;
+      if (x < 255 && pos <= end && end - pos >= 8) {
+        const uint32_t lo = s.u32(pos), hi = s.u32(pos + 4);
+        if (!hi && lo <= end - pos - 8 && x + 8 + lo < 255) d = x + 8 + lo;
+      }
+      t1 |= d << (8 * k);
     }
-    s += lo32;
-    pos = p + lo32;
-    if ((e & 63) == 63) tab[e - 63 + lane] = make_uint2(mp, ml);
+    const uint32_t kx = wave_chain(t1);
+    const bool has = kx != 0xFF;
+    uint32_t len = 0, bad = ST_OK;
+    const uint32_t pos = p + (has ? kx : 0u);
+    if (has) {
+      if (pos > end || end - pos < 8) {
+        bad = ST_IO;
+      } else {
+        const uint32_t lo = s.u32(pos), hi = s.u32(pos + 4);
+        if (hi || lo > end - pos - 8) bad = ST_OUT_OF_SPEC;
+        else len = lo;
+      }
+    }
+    const uint32_t m = (uint32_t)__popcll(__ballot(has));
+    const uint64_t badm = __ballot(has && bad != ST_OK);
+    uint32_t take = min(m, count - e);
+    if (badm) {  // only the window's last record can be bad (it stops the chain)
+      const uint32_t j = (uint32_t)__builtin_ctzll(badm);
+      if (j < take) {
+        st = __builtin_amdgcn_readlane(bad, j);
+        take = j;
+      }
+    }
+    if (lane < take) {
+      tab[e + lane] = (uint64_t)(pos + 8) | ((uint64_t)len << 32);
+      part += len;
+    }
+    if (st) break;
+    e += take;
+    p = __builtin_amdgcn_readlane(pos + 8 + len, take - 1);
   }
-  if (lane < (e & 63)) tab[(e & ~63u) + lane] = make_uint2(mp, ml);
-  *sum = s;
+  *sum = wave_sum64(part);
   return st;
 }
 
@@ -2783,30 +2850,34 @@ __device__ uint32_t expand_to_hbm(uint32_t codec, const uint8_t* src, uint32_t c
   return ST_NYI;
 }
 
-// A binary Dict's u32 index stream (n values) into bi.x: leaf codecs via
-// run_leaf; LZ4 / Snappy / Zstd expanded by wave 0 (into LDS for a staged
-// page, straight into the region for a big page); Freq: the top index filled,
-// then the exceptions (a leaf stream, or a general-codec stream expanded
-// into bi.xex first) scattered at their roaring rows.  All NT threads.
+// A binary Dict's u32 index stream (n values) into the tables' x: leaf codecs
+// via run_leaf; LZ4 / Snappy / Zstd expanded by wave 0 (into LDS for a
+// staged page, straight into the region for a big page); Freq: the top index
+// filled, then the exceptions (a leaf stream, or a general-codec stream
+// expanded into the xex table first) scattered at their roaring rows.  All
+// NT threads.
 template <class Src>
-__device__ void materialize_idx(const Src& s, Shared& sh, const BinInfo& bi, const Stream ix, const uint8_t* gpage,
-                                uint8_t* lds, uint32_t lds_bytes, uint8_t* biglds) {
-  constexpr bool kLds = std::is_same<Src, LdsSrc>::value;
+__device__ void materialize_idx(const Src& s, Shared& sh, const BinInfo& bi, TabBase<kLdsSrc<Src>> tb, const Stream ix,
+                                const uint8_t* gpage, uint8_t* lds, uint32_t lds_bytes, uint8_t* biglds,
+                                uint8_t* region) {
+  constexpr bool L = kLdsSrc<Src>;
   const uint32_t tid = threadIdx.x, n = ix.n;
-  uint32_t* xi = bi.x;
-  auto expand = [&](uint32_t codec, uint32_t body, uint32_t csize, uint32_t* dst, uint32_t bytes) -> uint32_t {
-    if constexpr (kLds) {
+  mptr<L, uint32_t> xi = tb.template at<uint32_t>(0);
+  mptr<L, uint32_t> xex = tb.template at<uint32_t>(bi.oxex);
+  auto expand = [&](uint32_t codec, uint32_t body, uint32_t csize, uint64_t off, uint32_t bytes) -> uint32_t {
+    if constexpr (L) {
+      lds_u8* dst = (lds_u8*)(lds + bi.tb + off);
       if (codec == 2)
-        return zs::zstd_to_lds(LdsSrc{s.w, s.base + body}, csize, (lds_u8*)dst, bytes, (lds_u8*)(lds + bi.ztab),
+        return zs::zstd_to_lds(LdsSrc{s.w, s.base + body}, csize, dst, bytes, (lds_u8*)(lds + bi.ztab),
                                lds_bytes - bi.ztab - kStagePad);
-      return expand_to_lds(codec, gpage + body, csize, (lds_u8*)dst, bytes);
+      return expand_to_lds(codec, gpage + body, csize, dst, bytes);
     } else {
-      return expand_to_hbm(codec, gpage + body, csize, (uint8_t*)dst, bytes, biglds);
+      return expand_to_hbm(codec, gpage + body, csize, region + off, bytes, biglds);
     }
   };
   if (ix.codec == 1 || ix.codec == 2 || ix.codec == 3) {
     if (tid < 64) {
-      const uint32_t st = expand(ix.codec, ix.body, ix.csize, xi, 4 * n);
+      const uint32_t st = expand(ix.codec, ix.body, ix.csize, 0, 4 * n);
       if (st) set_err(sh, st);
     }
     __syncthreads();
@@ -2820,13 +2891,13 @@ __device__ void materialize_idx(const Src& s, Shared& sh, const BinInfo& bi, con
     }
     __syncthreads();
     if (sh.err) return;
-    roaring_build(s, sh, bi.roar, bi.roar ? (uint32_t)roar_cap(n) : 0u);
+    roaring_build(s, sh, L ? nullptr : region + bi.oroar, L ? 0u : (uint32_t)roar_cap(n));
     if (sh.err) return;
     const uint32_t top = (uint32_t)sh.freq_top;
     for (uint32_t i = tid; i < n; i += NT) xi[i] = top;
     const bool gen = ex.codec == 1 || ex.codec == 2 || ex.codec == 3;
     if (gen && tid < 64) {
-      const uint32_t st = expand(ex.codec, ex.body, ex.csize, bi.xex, 4 * ex.n);
+      const uint32_t st = expand(ex.codec, ex.body, ex.csize, bi.oxex, 4 * ex.n);
       if (st) set_err(sh, st);
     }
     __syncthreads();
@@ -2840,11 +2911,11 @@ __device__ void materialize_idx(const Src& s, Shared& sh, const BinInfo& bi, con
     };
     if (!gen) {
       run_leaf<4>(s, sh, ex, scatter);
-    } else if constexpr (kLds) {
-      run_leaf<4>(LdsSrc{s.w, (uint32_t)((const uint8_t*)bi.xex - (const uint8_t*)s.w)}, sh, Stream{0u, 0u, 4 * ex.n, ex.n},
-                  scatter);
     } else {
-      run_leaf<4>(GlbSrc{(const uint8_t*)bi.xex}, sh, Stream{0u, 0u, 4 * ex.n, ex.n}, scatter);
+      for (uint32_t i = tid; i < ex.n; i += NT) {
+        const uint32_t v = xex[i];
+        scatter(i, &v, 1);
+      }
     }
     __syncthreads();
     return;
@@ -2860,9 +2931,11 @@ __device__ void materialize_idx(const Src& s, Shared& sh, const BinInfo& bi, con
 // in row order; select is increasing, so a binary search finds the first
 // row >= n), and wave 0's walk of their records.  S = (n - ep) * L + sum.
 template <class Src>
-__device__ void freq_tables(const Src& s, Shared& sh, BinInfo& bi, const PageDesc& pd, const uint8_t* gpage) {
+__device__ void freq_tables(const Src& s, Shared& sh, BinInfo& bi, TabBase<kLdsSrc<Src>> tb, const PageDesc& pd,
+                            uint8_t* region) {
+  constexpr bool L = kLdsSrc<Src>;
   const uint32_t n = pd.num_values;
-  roaring_build(s, sh, bi.roar, bi.roar ? (uint32_t)roar_cap(n) : 0u);
+  roaring_build(s, sh, L ? nullptr : region + bi.oroar, L ? 0u : (uint32_t)roar_cap(n));
   if (sh.err) return;
   if (threadIdx.x == 0) {
     uint32_t ep = 0, hi_e = bi.tot;
@@ -2876,8 +2949,8 @@ __device__ void freq_tables(const Src& s, Shared& sh, BinInfo& bi, const PageDes
   __syncthreads();
   if (threadIdx.x < 64) {
     uint64_t sum;
-    const uint32_t st = walk_records(gpage, bi.q, bi.end, bi.k, bi.tab, &sum);
-    if (st) set_err(sh, st);
+    const uint32_t st = walk_records(s, bi.q, bi.end, bi.k, tb.template at<uint64_t>(bi.otab), &sum);
+    if (st && threadIdx.x == 0) set_err(sh, st);
     if (threadIdx.x == 0) bi.S = (uint64_t)(n - bi.k) * bi.L + sum;
   }
   __syncthreads();
@@ -2888,43 +2961,50 @@ __device__ void freq_tables(const Src& s, Shared& sh, BinInfo& bi, const PageDes
 // page's values bytes, sum of its rows' entry lengths (an index >= k is
 // out of range, dict.rs:131-139 panics).
 template <class Src>
-__device__ void dict_tables(const Src& s, Shared& sh, BinInfo& bi, const Stream& ix, const PageDesc& pd,
-                            const uint8_t* gpage, uint8_t* lds, uint32_t lds_bytes, uint8_t* biglds, bool sized) {
+__device__ void dict_tables(const Src& s, Shared& sh, BinInfo& bi, TabBase<kLdsSrc<Src>> tb, const Stream& ix,
+                            const PageDesc& pd, const uint8_t* gpage, uint8_t* lds, uint32_t lds_bytes, uint8_t* biglds,
+                            uint8_t* region, bool sized) {
+  constexpr bool L = kLdsSrc<Src>;
   if (threadIdx.x < 64) {
     uint64_t sum;
-    const uint32_t st = walk_records(gpage, bi.q, bi.end, bi.k, bi.tab, &sum);
-    if (st) set_err(sh, st);
+    const uint32_t st = walk_records(s, bi.q, bi.end, bi.k, tb.template at<uint64_t>(bi.otab), &sum);
+    if (st && threadIdx.x == 0) set_err(sh, st);
   }
   __syncthreads();
   if (sh.err) return;
-  materialize_idx(s, sh, bi, ix, gpage, lds, lds_bytes, biglds);
+  materialize_idx(s, sh, bi, tb, ix, gpage, lds, lds_bytes, biglds, region);
   if (sh.err || !sized) return;
   const uint32_t k = bi.k;
+  mptr<L, uint32_t> xi = tb.template at<uint32_t>(0);
+  mptr<L, uint64_t> tab = tb.template at<uint64_t>(bi.otab);
   uint64_t part = 0;
+  bool bad = false;
   for (uint32_t i = threadIdx.x; i < pd.num_values; i += NT) {
-    const uint32_t x = bi.x[i];
-    if (x < k) part += bi.tab[x].y;
-    else set_err(sh, ST_OUT_OF_SPEC);
+    const uint32_t x = xi[i];
+    if (x < k) part += tab[x] >> 32;
+    else bad = true;
   }
+  if (bad) set_err(sh, ST_OUT_OF_SPEC);
   uint64_t tot;
   block_excl_scan<uint64_t>(part, sh, &tot);
   if (threadIdx.x == 0) bi.S = tot;
   __syncthreads();
 }
 
-// A binary Freq page's exception-row bitmap and its prefix popcounts (in
-// bi.x: ceil(n/32) words, then as many prefixes), after freq_tables; all NT
-// threads.  A row's exception rank is then pref[w] + popc(bits[w] & below).
+// A binary Freq page's exception-row bitmap and its prefix popcounts (at the
+// tables' x: ceil(n/32) words, then as many prefixes), after freq_tables; all
+// NT threads.  A row's exception rank is then pref[w] + popc(bits[w] & below).
 template <class Src>
-__device__ void freq_rows(const Src& s, Shared& sh, const BinInfo& bi, uint32_t n) {
+__device__ void freq_rows(const Src& s, Shared& sh, const BinInfo& bi, TabBase<kLdsSrc<Src>> tb, uint32_t n) {
+  constexpr bool L = kLdsSrc<Src>;
   const uint32_t tid = threadIdx.x, nw = (n + 31) / 32;
-  uint32_t* bits = bi.x;
-  uint32_t* pref = bits + nw;
+  mptr<L, uint32_t> bits = tb.template at<uint32_t>(0);
+  mptr<L, uint32_t> pref = bits + nw;
   for (uint32_t w = tid; w < nw; w += NT) bits[w] = 0;
   __syncthreads();
   for (uint32_t e = tid; e < bi.k; e += NT) {
     const uint32_t row = roaring_select(s, sh, e);
-    atomicOr(&bits[row >> 5], 1u << (row & 31));
+    atomicOr((uint32_t*)&bits[row >> 5], 1u << (row & 31));
   }
   __syncthreads();
   uint32_t carry = 0;
@@ -2947,11 +3027,11 @@ __device__ void freq_rows(const Src& s, Shared& sh, const BinInfo& bi, uint32_t 
 // order; units cut by the page's edges are stored byte by byte.  `ea` is
 // kEmitBytes of LDS for the tile's row starts and source positions.
 template <int OW, class Src, class LenF, class SrcF>
-__device__ void bin_emit(Shared& sh, const Src& src, uint32_t* ea, uint32_t n, uint64_t R, uint64_t V,
+__device__ __forceinline__ void bin_emit(Shared& sh, const Src& src, lds_u32* ea, uint32_t n, uint64_t R, uint64_t V,
                          const BinArgs& a, LenF len_of, SrcF src_of) {
   const uint32_t tid = threadIdx.x;
-  uint32_t* rs = ea;                  // kEmitRows + 1 tile-relative row starts
-  uint32_t* rp = ea + kEmitRows + 1;  // kEmitRows source positions
+  lds_u32* rs = ea;                  // kEmitRows + 1 tile-relative row starts
+  lds_u32* rp = ea + kEmitRows + 1;  // kEmitRows source positions
   uint64_t carry = 0;
   for (uint32_t r0 = 0; r0 < n; r0 += kEmitRows) {
     const uint32_t m = min(kEmitRows, n - r0);
@@ -2991,7 +3071,7 @@ __device__ void bin_emit(Shared& sh, const Src& src, uint32_t* ea, uint32_t n, u
       }
       uint32_t row = lo, re = rs[row + 1], base = rp[row];
       uint32_t wv[4] = {0, 0, 0, 0};
-      bool full = x0 >= 0 && (uint32_t)x0 + 16 <= tot;
+      const bool full = x0 >= 0 && (uint32_t)x0 + 16 <= tot;
 #pragma unroll
       for (int k = 0; k < 16; k++) {
         const int32_t x = x0 + k;
@@ -3260,9 +3340,10 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
     }
     const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
     LdsSrc s{(const uint32_t*)stage, base};
-    if (threadIdx.x == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, nullptr, &idx);
+    if (threadIdx.x == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, true, stage_end, a.lds_bytes, &idx);
     __syncthreads();
     if (!sh.err) {
+      const TabBase<true> tb{(lds_u8*)stage + bi.tb};
       if (bi.codec == 1 || bi.codec == 3) {
         // Basic under LZ4 / Snappy: the offsets stream expands into scratch, the
         // values stream straight into the values buffer at the page's base
@@ -3273,9 +3354,9 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
           a.jobs[slot + 1] = InflateJob{pd.byte_off + bi.vb, kDstBinBase | page, bi.vcs, (uint32_t)bi.S, bi.codec, page};
         }
       } else if (bi.codec == BIN_DICT) {
-        dict_tables(s, sh, bi, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, true);
+        dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, true);
       } else if (bi.codec == BIN_FREQ) {
-        freq_tables(s, sh, bi, pd, a.chunk + pd.byte_off);
+        freq_tables(s, sh, bi, tb, pd, nullptr);
       }
     }
     __syncthreads();
@@ -3306,27 +3387,29 @@ __global__ __launch_bounds__(NT) void k_bin_scan(BinArgs a) {
 // built (dict_tables / freq_tables + freq_rows): offsets and values through
 // bin_emit.  All NT threads.
 template <int OW, class Src>
-__device__ void bin_emit_extend(Shared& sh, const Src& s, const BinInfo& bi, uint32_t* ea, uint32_t n, uint64_t R,
-                                uint64_t V, const BinArgs& a) {
+__device__ __forceinline__ void bin_emit_extend(Shared& sh, const Src& s, const BinInfo& bi, TabBase<kLdsSrc<Src>> tb, lds_u32* ea,
+                                uint32_t n, uint64_t R, uint64_t V, const BinArgs& a) {
+  constexpr bool L = kLdsSrc<Src>;
   if (bi.codec == BIN_ONE) {
-    const uint32_t L = bi.L, top = bi.top;
-    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t) { return L; }, [&](uint32_t) { return top; });
+    const uint32_t len = bi.L, top = bi.top;
+    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t) { return len; }, [&](uint32_t) { return top; });
   } else if (bi.codec == BIN_DICT) {
-    const uint32_t* xi = bi.x;
-    const uint2* tab = bi.tab;
+    const mptr<L, uint32_t> xi = tb.template at<uint32_t>(0);
+    const mptr<L, uint64_t> tab = tb.template at<uint64_t>(bi.otab);
     const uint32_t k = bi.k;
-    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t i) { return xi[i] < k ? tab[xi[i]].y : 0u; },
-                 [&](uint32_t i) { return xi[i] < k ? tab[xi[i]].x : 0u; });
+    bin_emit<OW>(sh, s, ea, n, R, V, a,
+                 [&](uint32_t i) { const uint32_t x = xi[i]; return x < k ? (uint32_t)(tab[x] >> 32) : 0u; },
+                 [&](uint32_t i) { const uint32_t x = xi[i]; return x < k ? (uint32_t)tab[x] : 0u; });
   } else {  // Freq: exception rows by the bitmap + prefix popcount rank
     const uint32_t nw = (n + 31) / 32;
-    const uint32_t* bits = bi.x;
-    const uint32_t* pref = bits + nw;
-    const uint2* tab = bi.tab;
-    const uint32_t L = bi.L, top = bi.top;
+    const mptr<L, uint32_t> bits = tb.template at<uint32_t>(0);
+    const mptr<L, uint32_t> pref = bits + nw;
+    const mptr<L, uint64_t> tab = tb.template at<uint64_t>(bi.otab);
+    const uint32_t len = bi.L, top = bi.top;
     auto rank = [&](uint32_t i) { return pref[i >> 5] + __popc(bits[i >> 5] & ((1u << (i & 31)) - 1)); };
     auto exc = [&](uint32_t i) { return (bits[i >> 5] >> (i & 31)) & 1u; };
-    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t i) { return exc(i) ? tab[rank(i)].y : L; },
-                 [&](uint32_t i) { return exc(i) ? tab[rank(i)].x : top; });
+    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t i) { return exc(i) ? (uint32_t)(tab[rank(i)] >> 32) : len; },
+                 [&](uint32_t i) { return exc(i) ? (uint32_t)tab[rank(i)] : top; });
   }
 }
 
@@ -3358,7 +3441,7 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
     }
     const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
     LdsSrc s{(const uint32_t*)stage, base};
-    if (tid == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, lds, stage_end, a.lds_bytes, nullptr, &idx);
+    if (tid == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, true, stage_end, a.lds_bytes, &idx);
     __syncthreads();
     if (!sh.err) {
       if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
@@ -3415,13 +3498,14 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
           }
         }
       } else {
+        const TabBase<true> tb{(lds_u8*)stage + bi.tb};
         if (bi.codec == BIN_DICT) {
-          dict_tables(s, sh, bi, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, false);
+          dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, false);
         } else if (bi.codec == BIN_FREQ) {
-          freq_tables(s, sh, bi, pd, a.chunk + pd.byte_off);
-          if (!sh.err) freq_rows(s, sh, bi, n);
+          freq_tables(s, sh, bi, tb, pd, nullptr);
+          if (!sh.err) freq_rows(s, sh, bi, tb, n);
         }
-        if (!sh.err) bin_emit_extend<OW>(sh, s, bi, (uint32_t*)(lds + bi.emit), n, R, V, a);
+        if (!sh.err) bin_emit_extend<OW>(sh, s, bi, tb, (lds_u32*)((lds_u8*)stage + bi.emit), n, R, V, a);
       }
     }
     __syncthreads();
@@ -3449,6 +3533,7 @@ __global__ __launch_bounds__(NT) void k_bin_big(BinArgs a) {
     const uint32_t n = pd.num_values;
     const GlbSrc s{a.chunk + pd.byte_off};
     uint8_t* rgn = a.region + (pd.reserved - 1);
+    const TabBase<false> tb{(__attribute__((address_space(1))) uint8_t*)rgn};
     const uint64_t R = pd.row_off, V = STAGE ? a.bases[page] : 0;
     if (tid == 0) {
       sh.err = STAGE ? a.status[page] : 0u;
@@ -3461,23 +3546,23 @@ __global__ __launch_bounds__(NT) void k_bin_big(BinArgs a) {
       continue;
     }
     if (tid == 0) {
-      bin_parse<OW>(s, sh, bi, pd, a.nullable, nullptr, 0, 0, rgn, &idx);
+      bin_parse<OW>(s, sh, bi, pd, a.nullable, false, 0, 0, &idx);
       if (!sh.err && bi.codec <= 3) set_err(sh, ST_NYI);  // (Basic pages are never big)
     }
     __syncthreads();
     if (!sh.err) {
       if (STAGE == 0) {
         if (bi.codec == BIN_DICT) {
-          dict_tables(s, sh, bi, idx, pd, a.chunk + pd.byte_off, nullptr, 0, lds, true);
+          dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, nullptr, 0, lds, rgn, true);
         } else if (bi.codec == BIN_FREQ) {
-          freq_tables(s, sh, bi, pd, a.chunk + pd.byte_off);
-          if (!sh.err) freq_rows(s, sh, bi, n);
+          freq_tables(s, sh, bi, tb, pd, rgn);
+          if (!sh.err) freq_rows(s, sh, bi, tb, n);
         }
       } else {
         if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
         if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);
         if (bi.codec == BIN_FREQ) {  // the exceptions consumed (the bitmap and walk are in the region)
-          roaring_build(s, sh, bi.roar, (uint32_t)roar_cap(n));
+          roaring_build(s, sh, rgn + bi.oroar, (uint32_t)roar_cap(n));
           if (tid == 0 && !sh.err) {
             uint32_t ep = 0, hi_e = bi.tot;
             while (ep < hi_e) {
@@ -3489,7 +3574,7 @@ __global__ __launch_bounds__(NT) void k_bin_big(BinArgs a) {
           }
           __syncthreads();
         }
-        if (!sh.err) bin_emit_extend<OW>(sh, s, bi, (uint32_t*)(lds + kBigEmit), n, R, V, a);
+        if (!sh.err) bin_emit_extend<OW>(sh, s, bi, tb, (lds_u32*)((lds_u8*)dyn + kBigEmit), n, R, V, a);
       }
     }
     __syncthreads();
@@ -3824,11 +3909,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
 
 // n bits of an LDS bitmap (bit 0 at word 0) to global bit position row_off,
 // one wave: whole words stored, edge words merged with atomicOr (zeroed bitmap).
