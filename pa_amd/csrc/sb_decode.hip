@@ -2539,7 +2539,7 @@ enum : uint32_t { BIN_BASIC = 0, BIN_ONE = 12, BIN_DICT = 11, BIN_FREQ = 13 };
 
 // Rows per emission tile (bin_emit) and the LDS its row tables take.
 constexpr uint32_t kEmitRows = 4 * NT;
-constexpr uint32_t kEmitBytes = (4 * (2 * kEmitRows + 1) + 15) & ~15u;
+constexpr uint32_t kEmitBytes = 8192;  // LDS window of the binary emission (bin_emit)
 // Dynamic LDS of the big-page kernels: Zstd tables, one wave's inflate
 // buffers (ring, input ring, chain tables), the emission tables.
 constexpr uint32_t kBigZt = 0, kBigRing = kZTablesMax, kBigIb = kBigRing + kRing, kBigCt = kBigIb + kIb,
@@ -3019,23 +3019,40 @@ __device__ void freq_rows(const Src& s, Shared& sh, const BinInfo& bi, TabBase<k
   __syncthreads();
 }
 
+// len bytes of `src` from page position sp into the LDS window at byte w:
+// byte writes up to a dword boundary, whole dwords (each owned by this row
+// alone), byte writes for the tail -- neighbouring rows share only the edge
+// dwords, which both fill byte by byte.
+template <class Src>
+__device__ __forceinline__ void copy_to_win(const Src& src, uint32_t sp, uint32_t len, lds_u8* win, uint32_t w) {
+  while (len && (w & 3)) {
+    win[w++] = (uint8_t)src.u8(sp++);
+    len--;
+  }
+  for (; len >= 4; len -= 4, w += 4, sp += 4) ((lds_u32*)win)[w >> 2] = src.u32(sp);
+  while (len) {
+    win[w++] = (uint8_t)src.u8(sp++);
+    len--;
+  }
+}
+
 // Arrow offsets and values bytes of rows [0, n): row i has len_of(i) bytes at
 // page position src_of(i) of `src`.  Offsets[R + i + 1] = V + running length
-// (read_binary's rebase, binary/mod.rs:136-144).  The values go out in
-// 16-byte units aligned to the destination: one binary search over the
-// tile's row starts finds a unit's first row, its bytes are then read in row
-// order; units cut by the page's edges are stored byte by byte.  `ea` is
-// kEmitBytes of LDS for the tile's row starts and source positions.
+// (read_binary's rebase, binary/mod.rs:136-144).  Rows go NT*4 at a time,
+// four consecutive rows a thread; their bytes are gathered into an LDS
+// window of kEmitBytes (dword copies, copy_to_win) laid out as the
+// destination's 16-byte-aligned span, and each window leaves in 16-byte
+// stores (units cut by the page's edges byte by byte).  `ea` is the window.
 template <int OW, class Src, class LenF, class SrcF>
 __device__ __forceinline__ void bin_emit(Shared& sh, const Src& src, lds_u32* ea, uint32_t n, uint64_t R, uint64_t V,
-                         const BinArgs& a, LenF len_of, SrcF src_of) {
+                                         const BinArgs& a, LenF len_of, SrcF src_of) {
+  constexpr uint32_t WB = kEmitBytes & ~15u;
   const uint32_t tid = threadIdx.x;
-  lds_u32* rs = ea;                  // kEmitRows + 1 tile-relative row starts
-  lds_u32* rp = ea + kEmitRows + 1;  // kEmitRows source positions
+  lds_u8* win = (lds_u8*)ea;
   uint64_t carry = 0;
   for (uint32_t r0 = 0; r0 < n; r0 += kEmitRows) {
     const uint32_t m = min(kEmitRows, n - r0);
-    uint32_t l[4], sp[4];
+    uint32_t l[4], sp[4], st[4];
     uint32_t tsum = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -3049,52 +3066,41 @@ __device__ __forceinline__ void bin_emit(Shared& sh, const Src& src, lds_u32* ea
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const uint32_t i = 4 * tid + j;
+      st[j] = pre;
       if (i < m) {
-        rs[i] = pre;
-        rp[i] = sp[j] - pre;  // page position of tile byte x of row i = rp[i] + x
         pre += l[j];
         bin_put_off(a.out_offsets, R + r0 + i + 1, V + carry + pre, OW);
       }
     }
-    if (tid == 0) rs[m] = tot;
-    __syncthreads();
     uint8_t* d0 = a.out_values + V + carry;
     const uint32_t head = (uint32_t)((uintptr_t)d0 & 15);
-    const uint32_t nunits = (head + tot + 15) / 16;
-    for (uint32_t u = tid; u < nunits; u += NT) {
-      const int32_t x0 = (int32_t)(16 * u) - (int32_t)head;  // tile byte of the unit's first byte
-      const uint32_t xs = x0 < 0 ? 0u : (uint32_t)x0;
-      uint32_t lo = 0, hi = m;  // the last row starting at or before xs
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (rs[mid] <= xs) lo = mid; else hi = mid;
-      }
-      uint32_t row = lo, re = rs[row + 1], base = rp[row];
-      uint32_t wv[4] = {0, 0, 0, 0};
-      const bool full = x0 >= 0 && (uint32_t)x0 + 16 <= tot;
+    uint8_t* base0 = d0 - head;
+    const uint32_t span = head + tot;  // destination bytes from base0 (16-aligned)
+    for (uint32_t k0 = 0; k0 < span; k0 += WB) {
+      // tile bytes [xlo, xhi) land in this window at window byte x + head - k0
+      const int64_t xlo = (int64_t)k0 - head, xhi = xlo + WB;
 #pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const int32_t x = x0 + k;
-        if (x < 0 || (uint32_t)x >= tot) continue;
-        while ((uint32_t)x >= re) {
-          row++;
-          re = rs[row + 1];
-          base = rp[row];
-        }
-        wv[k >> 2] |= src.u8(base + (uint32_t)x) << (8 * (k & 3));
+      for (int j = 0; j < 4; j++) {
+        const int64_t lo = max<int64_t>(st[j], xlo), hi = min<int64_t>((int64_t)st[j] + l[j], xhi);
+        if (lo < hi)
+          copy_to_win(src, sp[j] + (uint32_t)(lo - st[j]), (uint32_t)(hi - lo), win, (uint32_t)(lo - xlo));
       }
-      uint8_t* d = d0 - head + 16 * u;
-      if (full) {
-        *(u32x4*)d = u32x4{wv[0], wv[1], wv[2], wv[3]};
-      } else {
-        for (int k = 0; k < 16; k++) {
-          const int32_t x = x0 + k;
-          if (x >= 0 && (uint32_t)x < tot) d[k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+      __syncthreads();
+      const uint32_t wl = min(WB, span - k0);
+      for (uint32_t u = tid; 16 * u < wl; u += NT) {
+        const uint32_t q = k0 + 16 * u;  // destination byte (from base0) of the unit
+        uint8_t* d = base0 + q;
+        const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(win + 16 * u);
+        if (q >= head && q + 16 <= span) {
+          *(u32x4*)d = v;
+        } else {
+          for (uint32_t b = 0; b < 16; b++)
+            if (q + b >= head && q + b < span) d[b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
         }
       }
+      __syncthreads();
     }
     carry += tot;
-    __syncthreads();
   }
 }
 

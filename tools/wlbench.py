@@ -1,7 +1,10 @@
-"""One bench workload alone (for per-workload rocprof kernel splits):
-python tools/wlbench.py c3|c4|c5 [steps] [warmup].  Builds bench.py's
-WorkloadC3 / C4 / C5 at the bench's default size and seed, times `steps`
-steps after `warmup`, prints ms/step and the step's kernel launches."""
+"""One bench workload alone (for per-workload rocprof kernel splits and PMC
+passes): python tools/wlbench.py c2|c3|c4|c5 [steps] [warmup] [bytes.json].
+Builds bench.py's Workload / WorkloadC3 / C4 / C5 at the bench's default
+size and seed, times `steps` steps after `warmup`, prints ms/step, and
+(optionally) writes the workload's algorithmic bytes per step -- compressed
+bytes read and Arrow bytes written, per column -- for the PMC summaries."""
+import json
 import os
 import sys
 
@@ -22,16 +25,29 @@ def main():
     warm = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     pa_amd.default_context(0)
     thr = bench.cpu_threads()
-    if wl_name == "c3":
+    cols = {}
+    if wl_name == "c2":
+        wl = bench.Workload(torch, pa_amd, 100_000_000, 42, "mix", 0, thr)
+        cols["int32"] = (wl.in_bytes, wl.out_bytes)
+    elif wl_name == "c3":
         wl = bench.WorkloadC3(torch, pa_amd, 100_000_000, 77, 0, thr)
+        nb = (wl.rows + 7) // 8
+        cols["float64"] = (len(wl.fchunk), wl.rows * 8 + nb)
+        cols["utf8"] = (len(wl.schunk), 4 * (wl.srows + 1) + wl.svals_len + (wl.srows + 7) // 8)
     elif wl_name == "c4":
         wl = bench.WorkloadC4(torch, pa_amd, 50_000_000, 99, 0, thr)
+        cols["list_int32"] = (wl.in_bytes, wl.out_bytes)
     else:
         wl = bench.WorkloadC5(torch, pa_amd, 8_388_608, 555, 0, thr)
+        cols["table"] = (wl.in_bytes, wl.out_bytes)
     print(f"{wl_name}: built", flush=True)
     wall, k, ok = bench.timed(torch, None, wl, steps, warm)
     ms = float(np.mean(k))
     print(f"{wl_name}: ok={ok} {ms:.3f} ms/step", flush=True)
+    if len(sys.argv) > 4:
+        json.dump({"workload": wl_name, "ms_per_step": ms, "in_bytes": wl.in_bytes, "out_bytes": wl.out_bytes,
+                   "columns": {c: {"in_bytes": i, "out_bytes": o} for c, (i, o) in cols.items()}},
+                  open(sys.argv[4], "w"), indent=1)
 
 
 if __name__ == "__main__":
