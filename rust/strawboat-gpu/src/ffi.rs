@@ -16,7 +16,7 @@ pub struct sb_leaf_info {
     pub list_nullable: [i32; SB_MAX_NEST], pub large_list: [i32; SB_MAX_NEST], pub flags: u32, pub top_field: i32,
 }
 
-#[repr(C)] #[derive(Clone, Copy)]
+#[repr(C)] #[derive(Debug, Clone, Copy, PartialEq, Eq)]
 pub struct sb_page_meta { pub length: u64, pub num_values: u64 }   // == crate::PageMeta
 
 #[repr(C)] #[derive(Clone, Copy)]
@@ -150,6 +150,8 @@ extern "C" {
     pub fn hipFree(ptr: *mut c_void) -> c_int;
     pub fn hipMemcpy(dst: *mut c_void, src: *const c_void, size: usize, kind: c_int) -> c_int;
     pub fn hipMemsetAsync(dst: *mut c_void, value: c_int, size: usize, stream: *mut c_void) -> c_int;
+    pub fn hipSetDevice(device: c_int) -> c_int;
+    pub fn hipGetDevice(device: *mut c_int) -> c_int;
 }
 pub const HIP_MEMCPY_HOST_TO_DEVICE: c_int = 1;
 pub const HIP_MEMCPY_DEVICE_TO_HOST: c_int = 2;

@@ -18,9 +18,11 @@
 //! them into arrow2 arrays or copies them out with [`DeviceBuffer::to_host`].
 //! Errors map onto the reference's `arrow2::error::Error` variants
 //! (src/errors.rs:19-31) through [`Error`].
+pub mod compat;
 pub mod ffi;
 
 use std::ffi::{CStr, CString};
+use std::marker::PhantomData;
 use std::os::raw::c_void;
 use std::ptr;
 
@@ -74,8 +76,12 @@ pub struct ColumnMeta {
 }
 
 impl ColumnMeta {
-    pub fn total_len(&self) -> u64 {
-        self.pages.iter().map(|p| p.length).sum()
+    /// The chunk's bytes (overflow-checked: page lengths come from the file).
+    pub fn total_len(&self) -> Result<u64> {
+        self.pages
+            .iter()
+            .try_fold(0u64, |acc, p| acc.checked_add(p.length))
+            .ok_or_else(|| Error::OutOfSpec("column chunk length overflows u64".into()))
     }
 }
 
@@ -112,24 +118,28 @@ impl PhysicalType {
     }
 }
 
-/// An HBM allocation (hipMalloc), freed on drop.
+/// An HBM allocation (hipMalloc) on one device, freed on drop.
 pub struct DeviceBuffer {
     ptr: *mut c_void,
     len: usize,
+    device: i32,
 }
 
 impl DeviceBuffer {
+    /// On the thread's current device (prefer [`Context::alloc`]).
     pub fn new(len: usize) -> Result<Self> {
+        let mut dev = 0;
+        unsafe { ffi::hipGetDevice(&mut dev) };
         let mut p = ptr::null_mut();
         let e = unsafe { ffi::hipMalloc(&mut p, len.max(16)) };
         if e != 0 {
             return Err(Error::Device(format!("hipMalloc({len}) failed: {e}")));
         }
-        Ok(DeviceBuffer { ptr: p, len })
+        Ok(DeviceBuffer { ptr: p, len, device: dev })
     }
-    /// A zero-filled buffer (zeroed on the context's stream).
+    /// A zero-filled buffer on the context's device (zeroed on its stream).
     pub fn zeroed(ctx: &Context, len: usize) -> Result<Self> {
-        let b = Self::new(len)?;
+        let b = ctx.alloc(len)?;
         let e = unsafe { ffi::hipMemsetAsync(b.ptr, 0, len.max(16), ffi::sb_ctx_stream(ctx.raw)) };
         if e != 0 {
             return Err(Error::Device(format!("hipMemsetAsync failed: {e}")));
@@ -161,6 +171,10 @@ impl DeviceBuffer {
     pub fn is_empty(&self) -> bool {
         self.len == 0
     }
+    /// The device the buffer was allocated on.
+    pub fn device(&self) -> i32 {
+        self.device
+    }
 }
 
 impl Drop for DeviceBuffer {
@@ -180,6 +194,33 @@ impl Context {
         let mut raw = ptr::null_mut();
         status(unsafe { ffi::sb_ctx_create(device, &mut raw) }, || format!("no usable GPU {device}"))?;
         Ok(Context { raw })
+    }
+    pub fn device(&self) -> i32 {
+        unsafe { ffi::sb_ctx_device(self.raw) }
+    }
+    /// An HBM buffer on this context's device (whatever the thread's current device).
+    pub fn alloc(&self, len: usize) -> Result<DeviceBuffer> {
+        let e = unsafe { ffi::hipSetDevice(self.device()) };
+        if e != 0 {
+            return Err(Error::Device(format!("hipSetDevice({}) failed: {e}", self.device())));
+        }
+        DeviceBuffer::new(len)
+    }
+    /// Host bytes into an HBM buffer on this context's device.
+    pub fn upload(&self, bytes: &[u8]) -> Result<DeviceBuffer> {
+        let b = self.alloc(bytes.len())?;
+        let e = unsafe { ffi::hipMemcpy(b.ptr, bytes.as_ptr() as *const c_void, bytes.len(), ffi::HIP_MEMCPY_HOST_TO_DEVICE) };
+        if e != 0 {
+            return Err(Error::Device(format!("hipMemcpy H2D failed: {e}")));
+        }
+        Ok(b)
+    }
+    /// A column chunk must live on this context's device.
+    fn check_chunk(&self, chunk: &DeviceBuffer) -> Result<()> {
+        if chunk.device != self.device() {
+            return Err(Error::Argument(format!("chunk on device {} but the context on {}", chunk.device, self.device())));
+        }
+        Ok(())
     }
     /// Launch on an external hipStream_t.
     pub fn set_stream(&mut self, stream: *mut c_void) -> Result<()> {
@@ -224,6 +265,8 @@ pub struct PrimitiveColumn<'a> {
     plan: Plan,
     ty: PhysicalType,
     nullable: bool,
+    // the plan keeps the chunk's device pointer: the chunk must outlive it
+    _chunk: PhantomData<&'a DeviceBuffer>,
 }
 
 /// Arrow buffers of a decoded flat column.
@@ -234,13 +277,14 @@ pub struct Primitive {
 }
 
 impl<'a> PrimitiveColumn<'a> {
-    pub fn plan(ctx: &'a Context, chunk: &DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, nullable: bool) -> Result<Self> {
+    pub fn plan(ctx: &'a Context, chunk: &'a DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, nullable: bool) -> Result<Self> {
+        ctx.check_chunk(chunk)?;
         let desc = ffi::sb_column_desc { physical_type: ty as i32, nullable: nullable as i32 };
         let mut raw = ptr::null_mut();
         status(unsafe {
             ffi::sb_plan_column(ctx.raw, &desc, chunk.ptr as *const u8, chunk.len as u64, pages.as_ptr(), pages.len() as u64, &mut raw)
         }, || ctx.last_error())?;
-        Ok(PrimitiveColumn { ctx, plan: Plan { raw }, ty, nullable })
+        Ok(PrimitiveColumn { ctx, plan: Plan { raw }, ty, nullable, _chunk: PhantomData })
     }
     pub fn num_rows(&self) -> u64 {
         unsafe { ffi::sb_plan_num_rows(self.plan.raw) }
@@ -250,11 +294,11 @@ impl<'a> PrimitiveColumn<'a> {
     pub fn decode(&self) -> Result<Primitive> {
         let n = self.num_rows();
         let values = if self.ty == PhysicalType::Boolean {
-            DeviceBuffer::new(bitmap_bytes(n))?
+            self.ctx.alloc(bitmap_bytes(n))?
         } else {
-            DeviceBuffer::new((n as usize) * self.ty.width())?
+            self.ctx.alloc((n as usize) * self.ty.width())?
         };
-        let validity = if self.nullable { Some(DeviceBuffer::new(bitmap_bytes(n))?) } else { None };
+        let validity = if self.nullable { Some(self.ctx.alloc(bitmap_bytes(n))?) } else { None };
         let out = ffi::sb_primitive_out {
             d_values: values.ptr,
             d_validity: validity.as_ref().map_or(ptr::null_mut(), |b| b.ptr as *mut u8),
@@ -277,6 +321,8 @@ pub struct BinaryColumn<'a> {
     plan: Plan,
     ty: PhysicalType,
     nullable: bool,
+    // the plan keeps the chunk's device pointer: the chunk must outlive it
+    _chunk: PhantomData<&'a DeviceBuffer>,
 }
 
 pub struct Binary {
@@ -287,7 +333,8 @@ pub struct Binary {
 }
 
 impl<'a> BinaryColumn<'a> {
-    pub fn plan(ctx: &'a Context, chunk: &DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, nullable: bool) -> Result<Self> {
+    pub fn plan(ctx: &'a Context, chunk: &'a DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, nullable: bool) -> Result<Self> {
+        ctx.check_chunk(chunk)?;
         if !ty.is_binary() {
             return Err(Error::Argument(format!("{ty:?} is not a binary type")));
         }
@@ -296,14 +343,14 @@ impl<'a> BinaryColumn<'a> {
         status(unsafe {
             ffi::sb_plan_column(ctx.raw, &desc, chunk.ptr as *const u8, chunk.len as u64, pages.as_ptr(), pages.len() as u64, &mut raw)
         }, || ctx.last_error())?;
-        Ok(BinaryColumn { ctx, plan: Plan { raw }, ty, nullable })
+        Ok(BinaryColumn { ctx, plan: Plan { raw }, ty, nullable, _chunk: PhantomData })
     }
     pub fn decode(&self) -> Result<Binary> {
         let n = unsafe { ffi::sb_plan_num_rows(self.plan.raw) };
         let vb = unsafe { ffi::sb_plan_values_bytes(self.plan.raw) };
-        let offsets = DeviceBuffer::new((n as usize + 1) * self.ty.offset_width())?;
-        let values = DeviceBuffer::new(vb as usize)?;
-        let validity = if self.nullable { Some(DeviceBuffer::new(bitmap_bytes(n))?) } else { None };
+        let offsets = self.ctx.alloc((n as usize + 1) * self.ty.offset_width())?;
+        let values = self.ctx.alloc(vb as usize)?;
+        let validity = if self.nullable { Some(self.ctx.alloc(bitmap_bytes(n))?) } else { None };
         let out = ffi::sb_binary_out {
             d_offsets: offsets.ptr,
             d_values: values.ptr as *mut u8,
@@ -323,6 +370,7 @@ pub struct ListColumn<'a> {
     plan: Plan,
     desc: ffi::sb_list_desc,
     ty: PhysicalType,
+    _chunk: PhantomData<&'a DeviceBuffer>,
 }
 
 pub struct List {
@@ -335,8 +383,9 @@ pub struct List {
 }
 
 impl<'a> ListColumn<'a> {
-    pub fn plan(ctx: &'a Context, chunk: &DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, list_nullable: bool,
+    pub fn plan(ctx: &'a Context, chunk: &'a DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, list_nullable: bool,
                 item_nullable: bool, large: bool) -> Result<Self> {
+        ctx.check_chunk(chunk)?;
         let desc = ffi::sb_list_desc {
             physical_type: ty as i32,
             list_nullable: list_nullable as i32,
@@ -347,15 +396,15 @@ impl<'a> ListColumn<'a> {
         status(unsafe {
             ffi::sb_plan_list_column(ctx.raw, &desc, chunk.ptr as *const u8, chunk.len as u64, pages.as_ptr(), pages.len() as u64, &mut raw)
         }, || ctx.last_error())?;
-        Ok(ListColumn { ctx, plan: Plan { raw }, desc, ty })
+        Ok(ListColumn { ctx, plan: Plan { raw }, desc, ty, _chunk: PhantomData })
     }
     pub fn decode(&self) -> Result<List> {
         let rows = unsafe { ffi::sb_plan_num_rows(self.plan.raw) };
         let leaves = unsafe { ffi::sb_plan_num_leaves(self.plan.raw) };
-        let offsets = DeviceBuffer::new((rows as usize + 1) * self.desc.offset_width as usize)?;
-        let values = DeviceBuffer::new(leaves as usize * self.ty.width())?;
-        let list_validity = if self.desc.list_nullable != 0 { Some(DeviceBuffer::new(bitmap_bytes(rows))?) } else { None };
-        let leaf_validity = if self.desc.item_nullable != 0 { Some(DeviceBuffer::new(bitmap_bytes(leaves))?) } else { None };
+        let offsets = self.ctx.alloc((rows as usize + 1) * self.desc.offset_width as usize)?;
+        let values = self.ctx.alloc(leaves as usize * self.ty.width())?;
+        let list_validity = if self.desc.list_nullable != 0 { Some(self.ctx.alloc(bitmap_bytes(rows))?) } else { None };
+        let leaf_validity = if self.desc.item_nullable != 0 { Some(self.ctx.alloc(bitmap_bytes(leaves))?) } else { None };
         let out = ffi::sb_list_out {
             d_offsets: offsets.ptr,
             d_list_validity: list_validity.as_ref().map_or(ptr::null_mut(), |b| b.ptr as *mut u8),
@@ -375,6 +424,7 @@ pub struct NestedColumn<'a> {
     plan: Plan,
     desc: ffi::sb_nested_desc,
     ty: PhysicalType,
+    _chunk: PhantomData<&'a DeviceBuffer>,
 }
 
 pub struct Nested {
@@ -390,8 +440,9 @@ pub struct Nested {
 }
 
 impl<'a> NestedColumn<'a> {
-    pub fn plan(ctx: &'a Context, chunk: &DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, list_nullable: &[bool],
+    pub fn plan(ctx: &'a Context, chunk: &'a DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, list_nullable: &[bool],
                 item_nullable: bool, large: bool) -> Result<Self> {
+        ctx.check_chunk(chunk)?;
         if list_nullable.is_empty() || list_nullable.len() > ffi::SB_MAX_NEST {
             return Err(Error::NotYetImplemented(format!("nesting depth {}", list_nullable.len())));
         }
@@ -410,7 +461,7 @@ impl<'a> NestedColumn<'a> {
         status(unsafe {
             ffi::sb_plan_nested_column(ctx.raw, &desc, chunk.ptr as *const u8, chunk.len as u64, pages.as_ptr(), pages.len() as u64, &mut raw)
         }, || ctx.last_error())?;
-        Ok(NestedColumn { ctx, plan: Plan { raw }, desc, ty })
+        Ok(NestedColumn { ctx, plan: Plan { raw }, desc, ty, _chunk: PhantomData })
     }
     pub fn decode(&self) -> Result<Nested> {
         let depth = self.desc.depth as usize;
@@ -427,27 +478,28 @@ impl<'a> NestedColumn<'a> {
         let mut offsets = Vec::new();
         let mut validity = Vec::new();
         for d in 0..depth {
-            let o = DeviceBuffer::new((counts[d] as usize + 1) * ow)?;
+            let o = self.ctx.alloc((counts[d] as usize + 1) * ow)?;
             out.d_offsets[d] = o.ptr;
             offsets.push(o);
-            let v = if self.desc.list_nullable[d] != 0 { Some(DeviceBuffer::new(bitmap_bytes(counts[d]))?) } else { None };
+            let v = if self.desc.list_nullable[d] != 0 { Some(self.ctx.alloc(bitmap_bytes(counts[d]))?) } else { None };
             out.d_validity[d] = v.as_ref().map_or(ptr::null_mut(), |b| b.ptr as *mut u8);
             validity.push(v);
         }
         let leaves = counts[depth];
         let (values, leaf_offsets) = if self.ty.is_binary() {
             let vb = unsafe { ffi::sb_plan_values_bytes(self.plan.raw) };
-            let lo = DeviceBuffer::new((leaves as usize + 1) * self.ty.offset_width())?;
+            // zeroed: with no pages the C decode writes only the level offsets
+            let lo = DeviceBuffer::zeroed(self.ctx, (leaves as usize + 1) * self.ty.offset_width())?;
             out.d_leaf_offsets = lo.ptr;
             out.values_capacity = vb;
-            (DeviceBuffer::new(vb as usize)?, Some(lo))
+            (self.ctx.alloc(vb as usize)?, Some(lo))
         } else if self.ty == PhysicalType::Boolean {
-            (DeviceBuffer::new(bitmap_bytes(leaves))?, None)
+            (self.ctx.alloc(bitmap_bytes(leaves))?, None)
         } else {
-            (DeviceBuffer::new(leaves as usize * self.ty.width())?, None)
+            (self.ctx.alloc(leaves as usize * self.ty.width())?, None)
         };
         out.d_values = values.ptr;
-        let leaf_validity = if self.desc.item_nullable != 0 { Some(DeviceBuffer::new(bitmap_bytes(leaves))?) } else { None };
+        let leaf_validity = if self.desc.item_nullable != 0 { Some(self.ctx.alloc(bitmap_bytes(leaves))?) } else { None };
         out.d_leaf_validity = leaf_validity.as_ref().map_or(ptr::null_mut(), |b| b.ptr as *mut u8);
         status(unsafe { ffi::sb_decode_nested_planned(self.ctx.raw, self.plan.raw, &out) }, || self.ctx.last_error())?;
         let mut bad = -1i64;
@@ -527,11 +579,21 @@ impl File {
     pub fn leaves(&self) -> Result<Vec<Leaf>> {
         parse_schema(&self.schema_bytes()?)
     }
+    /// Each schema leaf with its column meta (to_leaves order, one to one);
+    /// a schema whose leaf count differs from the footer's columns is OutOfSpec.
+    pub fn leaf_columns(&self) -> Result<Vec<(Leaf, ColumnMeta)>> {
+        let leaves = self.leaves()?;
+        let cols = self.columns()?;
+        if leaves.len() != cols.len() {
+            return Err(Error::OutOfSpec(format!("schema has {} leaves but the footer {} columns", leaves.len(), cols.len())));
+        }
+        Ok(leaves.into_iter().zip(cols).collect())
+    }
     /// Column chunk `col` into HBM (pinned double-buffered; ordered before
     /// later work on the context's stream).
     pub fn upload(&mut self, ctx: &Context, col: &ColumnMeta) -> Result<DeviceBuffer> {
-        let len = col.total_len();
-        let buf = DeviceBuffer::new(len as usize)?;
+        let len = col.total_len()?;
+        let buf = ctx.alloc(len as usize)?;
         status(unsafe { ffi::sb_file_upload(ctx.raw, self.raw, col.offset, len, buf.ptr) }, || self.err())?;
         Ok(buf)
     }
@@ -579,7 +641,7 @@ pub fn encode_column_device(ctx: &Context, ty: PhysicalType, values: &DeviceBuff
                             n_rows: u64, nullable: bool, opts: &WriteOptions) -> Result<(DeviceBuffer, Vec<PageMeta>)> {
     let page = opts.max_page_size.unwrap_or(0);
     let cap = unsafe { ffi::sb_encode_device_bound(ty as i32, n_rows, nullable as i32, page) };
-    let out = DeviceBuffer::new(cap as usize)?;
+    let out = ctx.alloc(cap as usize)?;
     let p = opts.max_page_size.unwrap_or(n_rows).min(n_rows).max(1);
     let mut metas = vec![PageMeta { length: 0, num_values: 0 }; ((n_rows + p - 1) / p).max(1) as usize];
     let (mut len, mut np) = (0u64, 0u64);

@@ -43,3 +43,50 @@ def test_rust_ffi_symbols_exported():
     lib = ctypes.CDLL(os.path.join(ROOT, "pa_amd", "libstrawboat_gpu.so"))
     for name in rust_functions():
         assert hasattr(lib, name), name
+
+
+COMPAT = os.path.join(ROOT, "rust", "strawboat-gpu", "src", "compat.rs")
+
+# The reference's signatures (b41sh/pa 0.2.6), parameter names in order:
+# the shim keeps them and puts the engine Context first.
+REFERENCE_SIGNATURES = {
+    # src/read/reader.rs:60
+    "new(page_reader": ["page_reader", "page_metas", "scratch"],
+    # src/read/deserialize.rs:237-243
+    "column_iter_to_arrays": ["readers", "leaves", "field", "is_nested"],
+    # src/read/batch_read.rs:190-196
+    "batch_read_array": ["readers", "leaves", "field", "is_nested", "page_metas"],
+    # src/write/writer.rs:59
+    "try_new": ["writer", "schema", "options"],
+}
+# src/read/reader.rs:69-145, read/mod.rs:55-57, write/writer.rs:66-173
+REFERENCE_METHODS = ["has_next", "current_page", "skip_page", "swap_buffer", "next", "nth", "into_inner", "start",
+                     "write", "finish", "total_size"]
+
+
+def _params(src, head):
+    i = src.index("pub fn " + head)
+    j = src.index("(", i + len("pub fn ") + len(head.split("(")[0]))
+    depth, k = 0, j
+    while True:
+        depth += {"(": 1, ")": -1}.get(src[k], 0)
+        if depth == 0:
+            break
+        k += 1
+    args = [a.strip() for a in re.split(r",(?![^<]*>)", src[j + 1:k]) if a.strip()]
+    return [a.split(":")[0].replace("mut ", "").strip() for a in args if a not in ("&self", "&mut self", "self")]
+
+
+def test_rust_compat_keeps_the_reference_signatures():
+    src = open(COMPAT).read()
+    for head, names in REFERENCE_SIGNATURES.items():
+        got = _params(src, head)
+        if got and got[0] == "ctx":
+            got = got[1:]
+        assert got == names, (head, got)
+    for m in REFERENCE_METHODS:
+        assert re.search(r"\bfn %s\b" % m, src), m
+    assert "pub struct NativeReader<R: Read + Seek>" in src and "pub struct NativeWriter<W: Write>" in src
+    assert "pub trait PageIterator" in src
+    lib = open(os.path.join(ROOT, "rust", "strawboat-gpu", "src", "lib.rs")).read()
+    assert "pub mod compat;" in lib
