@@ -903,15 +903,21 @@ class WorkloadC5:
         return ok
 
 
+TRAFFIC_FILE = "r03_pmc_traffic.json"  # tools/pmc_r03.sh -> tools/publish_traffic.py
+
+
 def load_traffic(workload: str):
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """This round's measured HBM bytes per step for `workload` (FETCH_SIZE /
+    WRITE_SIZE passes, calibrated correction, the commit they measured), or
+    None when the profile is absent."""
+    p = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
     if not os.path.exists(p):
         return None
-    try:
-        with open(p) as f:
-            return json.load(f).get(workload)
-    except Exception:
-        return None
+    with open(p) as f:
+        t = json.load(f).get(workload)
+    if t:
+        t = {k: v for k, v in t.items() if k != "kernels"}
+    return t
 
 
 def file_pipeline(torch, pa, wl, device, steps) -> dict:

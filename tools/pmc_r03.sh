@@ -1,25 +1,22 @@
 # Round-3 HBM traffic evidence: FETCH_SIZE / WRITE_SIZE per kernel (separate
-# --pmc passes) for the calibration kernels (tools/calib_fetch.hip) and the
-# C2 headline, C3, C4 and C5 decodes of this tree.  Outputs: gpurun_out/r03pmc/.
+# --pmc passes) and a kernel trace of the C2 headline, C3, C4 and C5 decodes
+# of this tree.  Outputs: gpurun_out/r03pmc/ (summaries: <wl>_traffic.json).
 set -o pipefail
 out=gpurun_out/r03pmc
 mkdir -p $out
+commit=${COMMIT:-unknown}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 run() {  # tag counter cmd...
   local tag=$1 ctr=$2; shift 2
-  timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $out/$tag -o p -- "$@" > $out/$tag.log 2>&1 || { echo "pmc $tag failed"; tail -5 $out/$tag.log; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $out/$tag -o p -- "$@" > $out/$tag.log 2>&1 || { echo "pmc $tag failed"; tail -5 $out/$tag.log; exit 1; }
   echo "done $tag"
 }
-run cal_f FETCH_SIZE tools/calib_fetch
-run cal_w WRITE_SIZE tools/calib_fetch
-python3 tools/prof_summary.py pmc $(ls $out/cal_f/*counter_collection.csv) $(ls $out/cal_w/*counter_collection.csv) $out/calib.json > /dev/null || exit 1
-C2="python3 bench.py --no-cpu --no-b12 --no-hard --no-c3 --no-c4 --no-c5 --no-encode --no-file --steps 6 --warmup 1"
-run c2_f FETCH_SIZE $C2
-run c2_w WRITE_SIZE $C2
-python3 tools/prof_summary.py pmc $(ls $out/c2_f/*counter_collection.csv) $(ls $out/c2_w/*counter_collection.csv) $out/c2.json > /dev/null || exit 1
-for wl in c4 c3 c5; do
-  run ${wl}_f FETCH_SIZE python3 tools/wlbench.py $wl 3 1
-  run ${wl}_w WRITE_SIZE python3 tools/wlbench.py $wl 3 1
-  python3 tools/prof_summary.py pmc $(ls $out/${wl}_f/*counter_collection.csv) $(ls $out/${wl}_w/*counter_collection.csv) $out/$wl.json > /dev/null || exit 1
+for wl in ${WLS:-c2 c2h c3 c4 c5}; do
+  run ${wl}_f FETCH_SIZE python3 tools/wlbench.py $wl 3 1 $out/${wl}_bytes.json
+  run ${wl}_w WRITE_SIZE python3 tools/wlbench.py $wl 3 1 $out/${wl}_bytes_w.json
+  python3 tools/pmc_summary.py $wl $(ls $out/${wl}_f/*counter_collection.csv) $(ls $out/${wl}_w/*counter_collection.csv) $out/${wl}_bytes.json $out/${wl}_traffic.json $commit || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/kt_$wl -o k -- python3 tools/wlbench.py $wl 10 3 $out/${wl}_bytes_k.json > $out/kt_$wl.log 2>&1 || { echo "trace $wl failed"; exit 1; }
+  python3 tools/prof_summary.py trace $(ls $out/kt_$wl/*kernel_trace.csv) 10 $out/${wl}_kernels.json > /dev/null || exit 1
+  tail -1 $out/kt_$wl.log
 done
 ls $out
