@@ -66,7 +66,7 @@ typedef enum {
   SB_T_FLOAT64 = 10,
   SB_T_BINARY = 11,       /* i32 offsets */
   SB_T_LARGE_BINARY = 12, /* i64 offsets */
-  SB_T_UTF8 = 13,         /* i32 offsets (bytes; UTF-8 validation is the caller's) */
+  SB_T_UTF8 = 13,         /* i32 offsets; values checked as Utf8Array::try_new does (OutOfSpec) */
   SB_T_LARGE_UTF8 = 14,   /* i64 offsets */
   SB_T_BOOLEAN = 15,      /* values are an LSB-first bitmap (read_boolean, read/array/boolean.rs:191-219) */
 } sb_physical_type;

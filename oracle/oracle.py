@@ -360,6 +360,29 @@ def read_binary_column(chunk: bytes, metas, nullable=False, offset_width=4):
     return offs, vals, (np.concatenate(valid) if nullable and valid else None)
 
 
+def check_utf8(values: bytes, offsets) -> bool:
+    """Utf8Array::try_new's check (read/array/binary.rs:305-306), restated from
+    arrow2 0.17 `try_check_utf8` (src/array/specification.rs; arrow2 is a
+    dependency, Cargo.toml:38, not vendored in the reference): an array of no
+    rows passes; else the whole values buffer must be UTF-8 (simdutf8 basic,
+    RFC 3629 -- Python's strict decoder accepts exactly that set), and unless
+    it is ASCII every offset up to `last` -- the last index >= 1 whose offset
+    is below the values length -- must not point at a 0b10xxxxxx byte."""
+    offs = [int(x) for x in offsets]
+    if len(offs) <= 1:
+        return True
+    if values.isascii():
+        return True
+    try:
+        values.decode("utf-8", "strict")
+    except UnicodeDecodeError:
+        return False
+    last = next((i for i in range(len(offs) - 1, 0, -1) if offs[i] < len(values)), None)
+    if last is None:
+        return True
+    return all(values[o] & 0xC0 != 0x80 for o in offs[:last + 1])
+
+
 # ---- nested List<primitive> ---------------------------------------------------
 def _list_lib():
     L = lib()

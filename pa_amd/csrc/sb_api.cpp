@@ -90,7 +90,7 @@ struct sb_plan {
   sb_plan* inner = nullptr;
   uint64_t n_leaves = 0;
   int offset_width = 0;
-  uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1 | (unused) 1] then BinLaunch::cls (u32)
+  uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1 | UTF-8 flags 1] then BinLaunch::cls (u32)
   uint32_t bin_grid = 0;      // staged-pass workgroups: the plan pass's staged page count
   uint32_t bin_lds = 0;       // dynamic LDS of the binary kernels (the largest page need, from the plan pass)
   uint64_t values_bytes = 0;
@@ -554,6 +554,16 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   }
   if (sb::launch_binary(1, p->offset_width, L, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (p->desc.physical_type == SB_T_UTF8 || p->desc.physical_type == SB_T_LARGE_UTF8) {
+    // Utf8Array::try_new (read/array/binary.rs:305-306): invalid UTF-8 or an
+    // offset inside a character is OutOfSpec for the page that holds it
+    uint32_t* flags = (uint32_t*)(p->d_bin + 2 * np + 1);
+    HIP_TRY(ctx, hipMemsetAsync(flags, 0, sizeof(uint32_t), ctx->stream));
+    sb::Utf8Launch U{out->d_values, p->values_bytes, (const uint8_t*)out->d_offsets, p->n_rows, p->d_pages,
+                     (uint32_t)np, p->d_bin + np, p->d_status, flags};
+    if (sb::launch_utf8_check(p->offset_width, U, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "utf8 check launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
   if (p->timing) {
     HIP_TRY(ctx, hipEventRecord(p->ev1, ctx->stream));
     p->timed = true;

@@ -2482,7 +2482,6 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
 // decoder's FSE / Huffman tables and sequence batches live in LDS.  Output
 // bytes are stored and re-read (matches, literals at the window's tail) by
 // the same wave in program order.
-constexpr uint32_t kZinfWaves = 1;
 __global__ __launch_bounds__(64) void k_zinflate(InflateLaunch a) {
   __shared__ u32x4 tabs[kZTablesMax / 16];
   const uint32_t n = a.count ? *a.count : a.n_jobs;
@@ -3593,6 +3592,126 @@ __global__ __launch_bounds__(NT) void k_bin_big(BinArgs a) {
 }
 
 // ===========================================================================
+// UTF-8 validation of a decoded Utf8 / LargeUtf8 column.  The reference builds
+// the array with Utf8Array::try_new (read/array/binary.rs:305-306), i.e.
+// arrow2 0.17 try_check_utf8: the whole values buffer must be UTF-8
+// (simdutf8::basic::from_utf8, RFC 3629: no overlong forms, no surrogates,
+// nothing above U+10FFFF) and, unless it is all ASCII, every offset up to the
+// last one below the values length must start a character (not 0b10xxxxxx).
+// k_utf8_bytes: 16 bytes a thread (a lead byte checks its trail bytes, a
+// trail byte finds its lead at most 3 bytes back); it raises flags[0] when it
+// sees a non-ASCII byte.  k_utf8_bounds: one offset a thread, only then.  A
+// failure marks the page that holds the byte / row OutOfSpec.
+// ===========================================================================
+using Utf8Args = Utf8Launch;
+
+// the last page whose key (values base / first row) is <= x: the non-empty
+// page holding x when empty pages share its key
+template <class KeyF>
+__device__ uint32_t utf8_page(uint32_t n, uint64_t x, KeyF key) {
+  uint32_t lo = 0, hi = n;  // key(lo) <= x < key(hi)
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) / 2;
+    if (key(m) <= x) lo = m;
+    else hi = m;
+  }
+  return lo;
+}
+
+// Bytes [pos, pos + 4) of the buffer as a little-endian word, 0 outside
+// [0, len) (a 0 byte is neither a lead nor a trail byte).  pos is a multiple
+// of 4 when ALIGNED.
+template <bool ALIGNED>
+__device__ __forceinline__ uint32_t utf8_word(const uint8_t* v, uint64_t len, int64_t pos) {
+  if (pos < 0 || (uint64_t)pos >= len) return 0;
+  const uint64_t rem = len - (uint64_t)pos;
+  uint32_t w;
+  if (ALIGNED) {
+    w = *(const uint32_t*)(v + pos);
+  } else {
+    w = 0;
+    for (uint32_t j = 0; j < 4 && j < rem; j++) w |= (uint32_t)v[pos + j] << (8 * j);
+  }
+  return rem >= 4 ? w : w & ((1u << (8 * rem)) - 1);
+}
+
+__device__ __forceinline__ bool utf8_trail(uint32_t b) { return (b & 0xC0u) == 0x80u; }
+// sequence length of a lead byte, 0 if the byte cannot start one
+__device__ __forceinline__ uint32_t utf8_len(uint32_t b) {
+  return b < 0x80u ? 1u : b < 0xC2u ? 0u : b < 0xE0u ? 2u : b < 0xF0u ? 3u : b < 0xF5u ? 4u : 0u;
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(NT) void k_utf8_bytes(Utf8Args a) {
+  const uint64_t chunks = (a.len + 15) / 16;
+  for (uint64_t c = blockIdx.x * (uint64_t)NT + threadIdx.x; c < chunks; c += (uint64_t)gridDim.x * NT) {
+    const int64_t p0 = (int64_t)(c * 16);
+    uint32_t w[6];  // bytes [p0 - 4, p0 + 20)
+    if (ALIGNED && (uint64_t)p0 + 16 <= a.len) {
+      const u32x4 m = *(const u32x4*)(a.values + p0);
+      w[1] = m.x, w[2] = m.y, w[3] = m.z, w[4] = m.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) w[1 + k] = utf8_word<ALIGNED>(a.values, a.len, p0 + 4 * k);
+    }
+    const bool ascii = ((w[1] | w[2] | w[3] | w[4]) & 0x80808080u) == 0;
+    const uint64_t na = __ballot(!ascii);
+    if (na && __lane_id() == __ffsll((unsigned long long)na) - 1 && *(volatile uint32_t*)a.flags == 0)
+      atomicOr(a.flags, 1u);
+    if (ascii) continue;  // no trail byte here; a lead just before is checked by its own thread
+    w[0] = utf8_word<ALIGNED>(a.values, a.len, p0 - 4);
+    w[5] = utf8_word<ALIGNED>(a.values, a.len, p0 + 16);
+    auto at = [&](int i) { return (w[(i + 4) >> 2] >> (8 * ((i + 4) & 3))) & 0xFFu; };  // i in [-4, 20)
+    bool bad = false;
+    int64_t bad_pos = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t b = at(j);
+      bool ok = true;
+      if (b < 0x80u) {
+      } else if (utf8_trail(b)) {  // its lead: the first non-trail byte 1..3 back must start a longer sequence
+        const uint32_t b1 = at(j - 1), b2 = at(j - 2), b3 = at(j - 3);
+        ok = !utf8_trail(b1) ? utf8_len(b1) > 1 : !utf8_trail(b2) ? utf8_len(b2) > 2 : !utf8_trail(b3) && utf8_len(b3) > 3;
+      } else {
+        const uint32_t L = utf8_len(b), c1 = at(j + 1);
+        ok = L >= 2 && utf8_trail(c1);
+        if (L >= 3) ok &= utf8_trail(at(j + 2));
+        if (L == 4) ok &= utf8_trail(at(j + 3));
+        // second-byte ranges: E0 A0..BF, ED 80..9F (no surrogates), F0 90..BF, F4 80..8F
+        if (b == 0xE0u) ok &= c1 >= 0xA0u;
+        if (b == 0xEDu) ok &= c1 < 0xA0u;
+        if (b == 0xF0u) ok &= c1 >= 0x90u;
+        if (b == 0xF4u) ok &= c1 < 0x90u;
+      }
+      if (!ok && !bad && (uint64_t)(p0 + j) < a.len) bad = true, bad_pos = p0 + j;
+    }
+    if (bad) {
+      const uint32_t pg = utf8_page(a.n_pages, (uint64_t)bad_pos, [&](uint32_t i) { return a.bases[i]; });
+      a.status[pg] = ST_OUT_OF_SPEC;
+    }
+  }
+}
+
+// Offsets j <= last, where last = the last j >= 1 whose offset is below the
+// values length (offsets are non-decreasing: j >= 1 is checked iff its offset
+// is below it, offset 0 iff offset 1 is).
+template <int OW>
+__global__ __launch_bounds__(NT) void k_utf8_bounds(Utf8Args a) {
+  if (*(volatile uint32_t*)a.flags == 0) return;  // all ASCII: every byte starts a character
+  using O = typename VT<OW>::T;
+  const O* off = (const O*)a.offsets;
+  for (uint64_t j = blockIdx.x * (uint64_t)NT + threadIdx.x; j <= a.n_rows; j += (uint64_t)gridDim.x * NT) {
+    const uint64_t o = (uint64_t)off[j];
+    const bool in = j == 0 ? (a.n_rows >= 1 && (uint64_t)off[1] < a.len && o < a.len) : o < a.len;
+    if (in && utf8_trail(a.values[o])) {
+      const uint64_t row = j < a.n_rows ? j : a.n_rows - 1;
+      const uint32_t pg = utf8_page(a.n_pages, row, [&](uint32_t i) { return a.pages[i].row_off; });
+      a.status[pg] = ST_OUT_OF_SPEC;
+    }
+  }
+}
+
+// ===========================================================================
 // Boolean pages (BooleanIter::deserialize / read_boolean,
 // read/array/boolean.rs:59-79, 191-219; decompress_boolean,
 // compression/boolean/mod.rs:63-102).  One workgroup per page: the page is
@@ -4632,6 +4751,20 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
       hipLaunchKernelGGL(sbk::k_bin_light_out<4>, lgrid, block, 0, st, a);
     }
   }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_utf8_check(int offset_width, const Utf8Launch& a, void* stream) {
+  if (a.n_rows == 0 || a.n_pages == 0) return 0;  // an empty array: nothing to check (try_check_utf8)
+  hipStream_t st = (hipStream_t)stream;
+  const uint64_t chunks = (a.len + 15) / 16;
+  if (chunks) {
+    const dim3 g((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + sbk::NT - 1) / sbk::NT, 8192)));
+    if ((uintptr_t)a.values % 16) hipLaunchKernelGGL(sbk::k_utf8_bytes<false>, g, dim3(sbk::NT), 0, st, a);
+    else hipLaunchKernelGGL(sbk::k_utf8_bytes<true>, g, dim3(sbk::NT), 0, st, a);
+  }
+  const dim3 g((uint32_t)std::min<uint64_t>((a.n_rows + sbk::NT) / sbk::NT, 8192));
+  if (offset_width == 8) hipLaunchKernelGGL(sbk::k_utf8_bounds<8>, g, dim3(sbk::NT), 0, st, a);
+  else hipLaunchKernelGGL(sbk::k_utf8_bounds<4>, g, dim3(sbk::NT), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb

@@ -178,6 +178,22 @@ struct BinLaunch {
 // stage 2: plan-time probe (lds_need / rneed per page).
 int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
 
+// Utf8 / LargeUtf8 columns after the decode: the checks of Utf8Array::try_new
+// (read/array/binary.rs:305-306; arrow2 0.17 try_check_utf8).  A failure
+// marks its page ST_OUT_OF_SPEC; flags[0] must be zero before the launch.
+struct Utf8Launch {
+  const uint8_t* values;
+  uint64_t len;            // values bytes of the column
+  const uint8_t* offsets;  // n_rows + 1 offsets of offset_width bytes
+  uint64_t n_rows;
+  const PageDesc* pages;
+  uint32_t n_pages;
+  const uint64_t* bases;   // first values byte of each page
+  uint32_t* status;
+  uint32_t* flags;         // [0]: a non-ASCII byte was seen
+};
+int launch_utf8_check(int offset_width, const Utf8Launch& a, void* stream);
+
 // List<primitive> columns: stage 0 = exact sizing pass (one wave per page,
 // walks the levels); stage 1 = block bases (peek = 1: counts from the page
 // headers instead); stage 2 = offsets + bitmaps + values-stream descriptors.

@@ -87,6 +87,8 @@ def test_binary_columns(ctx, kind, opt, nullable, phys):
     s = strings(kind, n, rng)
     validity = (rng.random(n) > 0.2) if nullable else None
     page_rows = 256 if kind == "long" else 2048
+    if kind == "long" and phys == 13:  # random bytes are not UTF-8 (tests/test_gpu_utf8.py): read as Binary
+        phys = 11
     assert check(ctx, s, validity, nullable, page_rows, O.WriteOptions.make(**OPTS[opt]), phys)
 
 
@@ -95,9 +97,9 @@ def test_binary_page_over_lds_budget(ctx):
     header-only page: offsets and values are copied from HBM (k_bin_light_out)."""
     rng = np.random.default_rng(2)
     s = strings("long", 2048, rng)
-    check(ctx, s, None, False, 2048, O.WriteOptions.make(), 13)
+    check(ctx, s, None, False, 2048, O.WriteOptions.make(), 11)
     v = rng.random(2048) > 0.3
-    check(ctx, s, v, True, 2048, O.WriteOptions.make(), 13)
+    check(ctx, s, v, True, 2048, O.WriteOptions.make(), 11)
 
 
 @pytest.mark.parametrize("entries,width", [(800, 200), (1500, 200)], ids=["160KiB", "300KiB"])
@@ -109,7 +111,7 @@ def test_binary_dict_page_over_lds_budget(ctx, entries, width, nullable):
     rng = np.random.default_rng(2)
     s = [bytes(rng.integers(0, 256, width, dtype=np.uint8)) for _ in range(entries)] * 4
     v = rng.random(len(s)) > 0.2 if nullable else None
-    assert check(ctx, s, v, nullable, len(s), O.WriteOptions.make(ratio=2.0, forced=O.DICT), 13) == {11}
+    assert check(ctx, s, v, nullable, len(s), O.WriteOptions.make(ratio=2.0, forced=O.DICT), 11) == {11}
 
 
 @pytest.mark.parametrize("opt", ["dict", "dict_lz4", "dict_zstd", "freq", "one"])
