@@ -13,7 +13,8 @@ from .read import (  # noqa: F401
     read_meta,
     unpack_bitmap,
 )
-from .write import NativeWriter, WriteOptions, assemble_file, encode_column, encode_column_device, encode_page, page_seed  # noqa: F401,E402
+from .write import (DeviceColumn, NativeWriter, WriteOptions, assemble_file, encode_column, encode_column_device,  # noqa: F401,E402
+                    encode_page, encode_table_device, page_seed)
 from .shard import (Shard, exclusive_bases, gather_sizes, rebase_offsets, shard_base, shard_pages,  # noqa: F401,E402
                     shard_slice)
 from .binary import (  # noqa: F401,E402

@@ -22,7 +22,8 @@
 //     cascades), OneValue, Bitpacking / DeltaBitpacking (bp.rs:37-65,
 //     delta_bp.rs:37-67; BitPacker4x words computed per lane word), Patas
 //     (double/patas.rs:37-105; the back reference found by a 127-row window
-//     search), and the Basic codecs None / LZ4 / Snappy (sb_lz4c.h, one lane;
+//     search), and the Basic codecs None / LZ4 (sb_lz4c.h, one wave) /
+//     Snappy (one lane;
 //     Zstd level 3 is not restated: NotYetImplemented).
 // Pages are written into per-page slots of a batch, then compacted.
 // Integer work; bound by the per-page hash/scan work, not by MFMA.
@@ -39,7 +40,8 @@
 namespace sba {
 
 constexpr int NT = 256, NW = NT / 64;
-constexpr uint32_t kMaxRows = 16384;
+constexpr uint32_t kMaxRows = 16384;      // pages whose statistics' tables fit the LDS work area
+constexpr uint32_t kMaxBigRows = 65535;   // pages with statistics, tables in HBM (16-bit rows in the table words)
 constexpr uint32_t SC = 10, SS = 64, kSample = SC * SS;
 
 enum : int { C_NONE = 0, C_LZ4 = 1, C_ZSTD = 2, C_SNAPPY = 3, C_RLE = 10, C_DICT = 11, C_ONE = 12, C_FREQ = 13, C_BP = 14,
@@ -136,7 +138,8 @@ struct Sh {
 };
 
 struct Ctx {
-  uint32_t* work;   // LDS work area: hash tables, run starts, bitmaps, LZ4 / Snappy tables
+  uint32_t* work;   // work area: hash tables, run starts, bitmaps, the Snappy table (LDS, or HBM for big pages)
+  uint8_t* lz4;     // LDS: the wave LZ4 compressor's tables (sbc::kLz4WaveLds bytes)
   uint32_t work_bytes;
   uint8_t* samp;    // LDS: kSample * 8 value bytes + kSample / 8 validity bytes
   uint8_t* scratch; // global: 2 levels x nmax x 8 bytes
@@ -147,6 +150,11 @@ struct Ctx {
 };
 
 __device__ __forceinline__ void set_err(Sh& sh, uint32_t e) { atomicMax(&sh.err, e); }
+
+// choose_compressor needs the statistics only with a ratio or an allowed forced codec
+__host__ __device__ __forceinline__ bool needs_stats(const Opts& o, uint32_t fm) {
+  return o.has_ratio || (o.forced >= 0 && !(fm & (1u << o.forced)));
+}
 
 __device__ __forceinline__ uint64_t rng_next(uint64_t& s) {  // splitmix64 (sb_encode.cpp Rng)
   uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -462,8 +470,8 @@ template <bool WRITE>
 __device__ uint32_t bp_body(Ctx& c, Sh& sh, const Av& a, uint32_t pos, bool delta) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t nblk = a.n / 128;
-  uint32_t* bw = c.work;          // [nblk] widths
-  uint32_t* boff = c.work + 256;  // [nblk + 1] block offsets (nblk <= 128)
+  uint32_t* bw = c.work;                             // [nblk] widths
+  uint32_t* boff = c.work + ((nblk + 255) & ~255u);  // [nblk] block offsets
   for (uint32_t k = wv; k < nblk; k += NW) {
     uint32_t acc = (uint32_t)ld<4>(a.p, 128 * k + lane) | (uint32_t)ld<4>(a.p, 128 * k + 64 + lane);
 #pragma unroll
@@ -471,11 +479,16 @@ __device__ uint32_t bp_body(Ctx& c, Sh& sh, const Av& a, uint32_t pos, bool delt
     if (lane == 0) bw[k] = acc ? 32 - __builtin_clz(acc) : 0;
   }
   __syncthreads();
-  uint32_t tot;
-  const uint32_t ex = bscan(sh, tid < nblk ? 1 + 16 * bw[tid] : 0u, &tot);
+  uint32_t tot = 0;
+  for (uint32_t k0 = 0; k0 < nblk; k0 += NT) {  // (one tile of blocks per 32768 rows)
+    const uint32_t k = k0 + tid;
+    uint32_t t;
+    const uint32_t ex = bscan(sh, k < nblk ? 1 + 16 * bw[k] : 0u, &t);
+    if (WRITE && k < nblk) boff[k] = tot + ex;
+    tot += t;
+  }
   if (!WRITE) return tot;
   if (!room(c, sh, (uint64_t)pos + tot)) return 0;
-  if (tid < nblk) boff[tid] = ex;
   __syncthreads();
   for (uint32_t s = tid; s < nblk * 128; s += NT) {
     const uint32_t k = s >> 7, w = s & 127, b = bw[k];
@@ -683,12 +696,21 @@ __device__ uint32_t basic_body(Ctx& c, Sh& sh, int codec, const uint8_t* src, ui
   if (codec == C_LZ4 || codec == C_SNAPPY) {
     const uint64_t bound = codec == C_LZ4 ? sbc::lz4_bound(len) : (uint64_t)len + len / 20 + 32;
     if (!room(c, sh, (uint64_t)pos + bound)) return 0;
-    if (codec == C_LZ4)
-      for (uint32_t i = tid; i < sbc::kLz4TableBytes / 4; i += NT) c.work[i] = 0;
+    if (codec == C_LZ4)  // the position table (16 KiB)
+      for (uint32_t i = tid; i < 4096; i += NT) ((uint32_t*)c.lz4)[i] = 0;
     __syncthreads();
-    if (tid == 0) {
-      sh.redu[0] = codec == C_LZ4 ? sbc::lz4_compress(src, len, c.out + pos, c.work)
-                                  : sbc::snappy_compress(src, len, c.out + pos, c.work);
+#ifdef SB_LZ4_SERIAL  // A/B: the one-lane compressor
+    if (codec == C_LZ4 && tid == 0) {
+      sh.redu[0] = sbc::lz4_compress(src, len, c.out + pos, c.lz4);
+    }
+#else
+    if (codec == C_LZ4 && tid < 64) {
+      const uint32_t r = sbc::lz4_compress_wave(src, len, c.out + pos, (sbc::lz4_lds8*)c.lz4);  // (c.lz4 is LDS)
+      if (tid == 0) sh.redu[0] = r;
+    }
+#endif
+    if (codec == C_SNAPPY && tid == 0) {
+      sh.redu[0] = sbc::snappy_compress(src, len, c.out + pos, c.work);
     }
     __syncthreads();
     const uint32_t r = sh.redu[0];
@@ -846,7 +868,9 @@ template <int W, bool FLT, bool SGN, int D>
 __device__ uint32_t enc_stream(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos) {
   const uint32_t tid = threadIdx.x, n = a.n;
   if (!room(c, sh, (uint64_t)pos + 9)) return pos;
-  gen_stats<W, FLT, SGN>(c, sh, a);
+  // the statistics only choose among codecs: with no ratio and no forced
+  // codec the page is Basic(default) (integer/mod.rs:267-307)
+  if (needs_stats(c.o, fm)) gen_stats<W, FLT, SGN>(c, sh, a);
   int codec = choose<W, FLT, SGN>(c, sh, a, fm);
   const uint32_t body = pos + 9;
   uint32_t end = body;
@@ -911,7 +935,9 @@ struct AdArgs {
   uint64_t slot_bytes;
   uint8_t* scratch;
   uint64_t scratch_bytes;  // per page
-  uint32_t work_bytes;
+  uint32_t work_bytes;     // LDS work area (0: big pages, whose work area is gwork)
+  uint8_t* gwork;          // big pages: per batch page, gwork_bytes of HBM work area
+  uint64_t gwork_bytes;
   uint64_t* sizes;         // [n_pages]
   uint32_t* status;        // [n_pages]
   uint64_t* offs;          // [n_pages + 1]: page offsets in the output; [n_pages] running total
@@ -971,6 +997,19 @@ __device__ uint32_t write_prefix(Ctx& c, const AdArgs& A, uint64_t r0, uint32_t 
   return 4 + hl + nb;
 }
 
+// The work area: LDS (work_bytes of it), or for a big page its HBM region,
+// the LDS then holding the LZ4 tables and the sample.
+__device__ __forceinline__ void set_work(Ctx& c, const AdArgs& A, uint32_t* lds) {
+  c.lz4 = (uint8_t*)lds;
+  if (A.gwork) {
+    c.work = (uint32_t*)(A.gwork + (uint64_t)blockIdx.x * A.gwork_bytes);
+    c.samp = (uint8_t*)lds + sbc::kLz4WaveLds;
+  } else {
+    c.work = lds;
+    c.samp = (uint8_t*)lds + A.work_bytes;
+  }
+}
+
 __device__ void ctx_init(Ctx& c, Sh& sh, const AdArgs& A, uint32_t p) {
   c.work = nullptr;
   c.work_bytes = A.work_bytes;
@@ -1004,6 +1043,7 @@ __global__ __launch_bounds__(NT) void k_enc_bool(AdArgs A) {
   Ctx c;
   ctx_init(c, sh, A, p);
   c.work = lds;
+  c.lz4 = (uint8_t*)lds;
   c.samp = (uint8_t*)lds + A.work_bytes;
   uint8_t* vals = c.samp + kSample * 8 + kSample / 8 + 16;
   uint8_t* rebuilt = vals + ((A.P + 15) & ~15u);
@@ -1087,8 +1127,7 @@ __global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
   const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
   Ctx c;
   ctx_init(c, sh, A, p);
-  c.work = lds;
-  c.samp = (uint8_t*)lds + A.work_bytes;
+  set_work(c, A, lds);
   const bool has_vb = A.nullable && A.validity;
   uint32_t pos = write_prefix(c, A, r0, n);
   const Av a{A.values + r0 * W, has_vb ? A.validity : nullptr, r0, n};
@@ -1179,8 +1218,7 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
   const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
   Ctx c;
   ctx_init(c, sh, A, p);
-  c.work = lds;
-  c.samp = (uint8_t*)lds + A.work_bytes;
+  set_work(c, A, lds);
   uint32_t* idx = (uint32_t*)c.scratch;  // region 0: ids, then rows of ids
   uint32_t* row_of = idx + A.P;
   uint64_t* hsh = (uint64_t*)(c.scratch + (uint64_t)2 * A.P * 8);
@@ -1191,8 +1229,6 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
   const bool has_vb = A.nullable && A.validity;
   const Av va{nullptr, has_vb ? A.validity : nullptr, r0, n};
   uint32_t pos = write_prefix(c, A, r0, n);
-  for (uint32_t r = tid; r < n; r += NT) hsh[r] = str_hash(sptr(r), slen(r));
-  __syncthreads();
   auto same = [&](uint32_t a, uint32_t b) {
     if (hsh[a] != hsh[b]) return false;
     const uint32_t l = slen(a);
@@ -1203,30 +1239,38 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
       if (x[i] != y[i]) return false;
     return true;
   };
-  // stats over every row (nulls included)
+  // stats over every row (nulls included): only to choose among codecs
+  // (binary/mod.rs:303-330); a Basic(default) page needs none
+  uint32_t NU = 0, U = 0, maxc = 0, top_row = 0;
+  uint64_t TU = 0;
   const uint32_t Sl = tab_slots(n);
   uint32_t* tab = c.work;
-  for (uint32_t i = tid; i < Sl; i += NT) tab[i] = 0;
-  __syncthreads();
-  uint32_t nulls = 0;
-  for (uint32_t r = tid; r < n; r += NT) {
-    tab_insert_h(tab, Sl, r, hsh[r], [&](uint32_t o) { return same(o, r); });
-    nulls += !valid_at(va, r);
-  }
-  __syncthreads();
-  uint32_t uniq = 0;
-  uint64_t best = 0, tu = 0;
-  for (uint32_t i = tid; i < Sl; i += NT) {
-    const uint32_t e = tab[i];
-    if (e) {
-      uniq++;
-      tu += slen((e & 0xFFFFu) - 1) + 8;
-      best = max(best, ((uint64_t)(e >> 16) << 32) | (0xFFFFFFFFu - ((e & 0xFFFFu) - 1)));
+  if (needs_stats(A.o, A.o.forbidden)) {
+    for (uint32_t r = tid; r < n; r += NT) hsh[r] = str_hash(sptr(r), slen(r));
+    __syncthreads();
+    for (uint32_t i = tid; i < Sl; i += NT) tab[i] = 0;
+    __syncthreads();
+    uint32_t nulls = 0;
+    for (uint32_t r = tid; r < n; r += NT) {
+      tab_insert_h(tab, Sl, r, hsh[r], [&](uint32_t o) { return same(o, r); });
+      nulls += !valid_at(va, r);
     }
+    __syncthreads();
+    uint32_t uniq = 0;
+    uint64_t best = 0, tu = 0;
+    for (uint32_t i = tid; i < Sl; i += NT) {
+      const uint32_t e = tab[i];
+      if (e) {
+        uniq++;
+        tu += slen((e & 0xFFFFu) - 1) + 8;
+        best = max(best, ((uint64_t)(e >> 16) << 32) | (0xFFFFFFFFu - ((e & 0xFFFFu) - 1)));
+      }
+    }
+    NU = (uint32_t)bsum(sh, nulls), U = (uint32_t)bsum(sh, uniq);
+    TU = bsum(sh, tu);
+    const uint64_t BEST = bmax(sh, best);
+    maxc = (uint32_t)(BEST >> 32), top_row = 0xFFFFFFFFu - (uint32_t)BEST;
   }
-  const uint32_t NU = (uint32_t)bsum(sh, nulls), U = (uint32_t)bsum(sh, uniq);
-  const uint64_t TU = bsum(sh, tu), BEST = bmax(sh, best);
-  const uint32_t maxc = (uint32_t)(BEST >> 32), top_row = 0xFFFFFFFFu - (uint32_t)BEST;
   const uint64_t total_bytes = A.parent_len + (uint64_t)(n + 1) * OW;
   int codec = A.o.dflt;
   const uint32_t fm = A.o.forbidden;
@@ -1481,10 +1525,29 @@ uint64_t adaptive_slot_bytes(uint64_t P, uint32_t w, int nullable) {
   return (pre + stream_bound(P, w, 2) + 64 + 15) & ~15ull;
 }
 
-uint32_t adaptive_work_bytes(uint64_t P) {
+// LDS work area of a page's workgroup: the statistics' hash table (two slots
+// a row) and the general codecs' tables; a Basic(default) page with no
+// statistics needs only its codec's (more workgroups per CU for LZ4 pages)
+uint32_t adaptive_work_bytes(uint64_t P, const sba::Opts& o) {
+  if (!sba::needs_stats(o, o.forbidden))
+    return o.dflt == sba::C_SNAPPY ? sbc::kSnappyTableBytes : o.dflt == sba::C_LZ4 ? sbc::kLz4WaveLds : 8192;
   uint64_t s = 64;
   while (s < 2 * P) s <<= 1;
   return (uint32_t)std::max<uint64_t>({4 * s, sbc::kSnappyTableBytes, 8192});
+}
+
+// A big page's HBM work area (pages over kMaxRows rows): the statistics'
+// hash table (rows < 65536: the 16-bit table words hold them), or for a
+// Basic page only the Snappy table.
+uint64_t big_work_bytes(uint64_t P, bool stats) {
+  uint64_t s = 64;
+  while (s < 2 * P) s <<= 1;
+  return stats ? std::max<uint64_t>(4 * s, sbc::kSnappyTableBytes) : sbc::kSnappyTableBytes;
+}
+
+// Pages of a batch: at most 2048, and at most ~2 GiB of slots + scratch + work.
+static uint32_t batch_pages(uint64_t np, uint64_t per_page) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({np, 2048, (2ull << 30) / std::max<uint64_t>(per_page, 1)}));
 }
 
 template <int W, bool FLT, bool SGN>
@@ -1515,17 +1578,26 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
     default: return SB_E_NYI;
   }
   const bool is_bool = phys == SB_T_BOOLEAN;
-  if (P > sba::kMaxRows) return SB_E_NYI;
+  // Pages over kMaxRows rows keep their work area in HBM: any size for a
+  // Basic(default) page, up to kMaxBigRows when the statistics are needed;
+  // Boolean pages stage their bits in LDS (kMaxRows)
+  const bool stats = sba::needs_stats(o, o.forbidden);
+  const bool big = P > sba::kMaxRows;
+  if (big && (is_bool || (stats && P > sba::kMaxBigRows) || P * w > 0xFFFFFFF0ull)) return SB_E_NYI;
   const uint64_t slot = adaptive_slot_bytes(P, w, nullable);
   const uint64_t scr = (2 * P * 8 + 255) & ~255ull;
-  const uint32_t batch = (uint32_t)std::min<uint64_t>(np, 2048);
-  const uint32_t work = adaptive_work_bytes(P);
-  uint32_t lds = work + sba::kSample * 8 + sba::kSample / 8 + 16;
+  const uint64_t gwb = big ? big_work_bytes(P, stats) : 0;
+  const uint32_t batch = batch_pages(np, slot + scr + gwb);
+  sba::Opts wo = o;
+  if (is_bool) wo.has_ratio = 1;  // (k_enc_bool stages its bits after the full work area)
+  const uint32_t work = big ? 0u : adaptive_work_bytes(P, wo);
+  uint32_t lds = (big ? sbc::kLz4WaveLds : work) + sba::kSample * 8 + sba::kSample / 8 + 16;
   if (is_bool) lds += (uint32_t)(((P + 15) & ~15ull) + (P + 7) / 8 + 16);  // staged bits + rebuilt bitmap
   uint8_t* slots = (uint8_t*)ctx_scratch(ctx, batch * slot + 256, 0);
   uint8_t* scratch = (uint8_t*)ctx_scratch(ctx, batch * scr, 1);
   uint64_t* meta = (uint64_t*)ctx_scratch(ctx, (2 * np + 2) * 8 + np * 4, 2);
-  if (!slots || !scratch || !meta) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 1");
+  uint8_t* gwork = big ? (uint8_t*)ctx_scratch(ctx, batch * gwb, 4) : nullptr;
+  if (!slots || !scratch || !meta || (big && !gwork)) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 1");
   hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
   uint64_t* sizes = meta;
   uint64_t* offs = meta + np;  // [np + 1]
@@ -1533,7 +1605,7 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
   if (hipMemsetAsync(offs + np, 0, 8, st) != hipSuccess) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 2");
   for (uint64_t b0 = 0; b0 < np; b0 += batch) {
     sba::AdArgs a{d_values, d_validity, n_rows, (uint32_t)P, (uint32_t)b0, (uint32_t)std::min<uint64_t>(batch, np - b0),
-                  nullable, o, opts->seed, slots, slot, scratch, scr, work, sizes, status, offs, d_out, out_cap,
+                  nullable, o, opts->seed, slots, slot, scratch, scr, work, gwork, gwb, sizes, status, offs, d_out, out_cap,
                   (uint32_t)np, nullptr, 0, 0, nullptr};
     if (is_bool) {
       ensure_lds_attr(sba::k_enc_bool, (int)lds);
@@ -1597,7 +1669,13 @@ int encode_binary_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, uint6
                            uint64_t* out_len, sb_page_meta* h_metas, uint64_t np) {
   const int ow = (phys == SB_T_BINARY || phys == SB_T_UTF8) ? 4 : (phys == SB_T_LARGE_BINARY || phys == SB_T_LARGE_UTF8) ? 8 : 0;
   if (!ow) return SB_E_NYI;
-  if (P > sba::kMaxRows) return SB_E_NYI;
+  const sba::Opts o{opts->default_codec, opts->has_ratio, opts->ratio, opts->forbidden_mask, opts->forced_codec};
+  const bool stats = sba::needs_stats(o, o.forbidden);
+  const bool big = P > sba::kMaxRows;  // (work area in HBM, as encode_adaptive's)
+  if (big && stats && P > sba::kMaxBigRows) return SB_E_NYI;
+  const uint64_t scr = (32 * P + 64 + 255) & ~255ull;
+  const uint64_t gwb = big ? big_work_bytes(P, stats) : 0;
+  const uint64_t maxpp = batch_pages(np, scr + gwb);
   hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
   // value bytes of every page from the offsets at the page boundaries
   int64_t* d_po = (int64_t*)ctx_scratch(ctx, (np + 1) * 8, 3);
@@ -1615,7 +1693,7 @@ int encode_binary_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, uint6
     const uint64_t n = std::min<uint64_t>(P, n_rows - p * P);
     if (po[p + 1] < po[p]) return SB_E_ARG;
     const uint64_t sb = binary_slot_bytes(n, (uint64_t)(po[p + 1] - po[p]), ow, nullable);
-    if (batches.empty() || (acc + sb > (1ull << 30) && p > batches.back().first) || p - batches.back().first >= 2048) {
+    if (batches.empty() || (acc + sb > (1ull << 30) && p > batches.back().first) || p - batches.back().first >= maxpp) {
       if (!batches.empty()) soff.push_back(acc);
       batches.push_back({p, soff.size()});
       acc = 0;
@@ -1629,14 +1707,14 @@ int encode_binary_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, uint6
     const uint64_t end = b + 1 < batches.size() ? soff[batches[b + 1].second - 1] : soff.back();
     max_batch = std::max(max_batch, end);
   }
-  const uint64_t scr = (32 * P + 64 + 255) & ~255ull;
-  const uint32_t work = adaptive_work_bytes(P);
-  const uint32_t lds = work + sba::kSample * 8 + sba::kSample / 8 + 16;
+  const uint32_t work = big ? 0u : adaptive_work_bytes(P, o);
+  const uint32_t lds = (big ? sbc::kLz4WaveLds : work) + sba::kSample * 8 + sba::kSample / 8 + 16;
   uint8_t* slots = (uint8_t*)ctx_scratch(ctx, max_batch + 256, 0);
-  const uint32_t maxn = (uint32_t)std::min<uint64_t>(np, 2048);
+  const uint32_t maxn = (uint32_t)std::min<uint64_t>(np, maxpp);
   uint8_t* scratch = (uint8_t*)ctx_scratch(ctx, maxn * scr, 1);
   uint64_t* meta = (uint64_t*)ctx_scratch(ctx, (2 * np + 2) * 8 + np * 4 + 8 + soff.size() * 8, 2);
-  if (!slots || !scratch || !meta) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 7");
+  uint8_t* gwork = big ? (uint8_t*)ctx_scratch(ctx, maxn * gwb, 4) : nullptr;
+  if (!slots || !scratch || !meta || (big && !gwork)) return ctx_fail(ctx, SB_E_DEVICE, "device encode step 7");
   uint64_t* sizes = meta;
   uint64_t* offs = meta + np;
   uint32_t* status = (uint32_t*)(meta + 2 * np + 2);
@@ -1644,12 +1722,11 @@ int encode_binary_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, uint6
   if (hipMemcpyAsync(d_soff, soff.data(), soff.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
       hipMemsetAsync(offs + np, 0, 8, st) != hipSuccess)
     return ctx_fail(ctx, SB_E_DEVICE, "device encode step 8");
-  sba::Opts o{opts->default_codec, opts->has_ratio, opts->ratio, opts->forbidden_mask, opts->forced_codec};
   for (size_t b = 0; b < batches.size(); b++) {
     const uint64_t b0 = batches[b].first;
     const uint64_t b1 = b + 1 < batches.size() ? batches[b + 1].first : np;
     sba::AdArgs a{d_values, d_validity, n_rows, (uint32_t)P, (uint32_t)b0, (uint32_t)(b1 - b0), nullable, o,
-                  opts->seed, slots, 0, scratch, scr, work, sizes, status, offs, d_out, out_cap, (uint32_t)np,
+                  opts->seed, slots, 0, scratch, scr, work, gwork, gwb, sizes, status, offs, d_out, out_cap, (uint32_t)np,
                   d_offsets, values_len, ow, d_soff + batches[b].second};
     if (ow == 4) {
       ensure_lds_attr(sba::k_enc_binary<4>, (int)lds);

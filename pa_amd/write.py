@@ -141,6 +141,106 @@ def encode_column_device(values, validity=None, nullable: bool = False, options:
     return out[: olen.value], [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
 
 
+@dataclass
+class DeviceColumn:
+    """One leaf of a chunk for encode_table_device: device tensors of the
+    values (and, for Binary / Utf8 leaves, int64 offsets), optional validity."""
+
+    values: object
+    validity: object = None
+    nullable: bool = False
+    options: Optional[WriteOptions] = None
+    offsets: object = None      # Binary / Utf8: n + 1 absolute positions into values
+    physical_type: int = 0      # Binary / Utf8: pa_amd.UTF8 ...; 0 = from the values' dtype
+
+
+_table_ctx = {}
+
+
+def _table_contexts(device: int, n: int):
+    """n contexts of this device, each on its own torch side stream (cached:
+    their grow-only scratch is reused by the next table)."""
+    import torch
+
+    from .read import Context
+
+    key = (device, n)
+    if key not in _table_ctx:
+        ctxs = []
+        for _ in range(n):
+            st = torch.cuda.Stream(device=device)
+            c = Context(device)
+            c.use_stream(st)
+            ctxs.append((c, st))
+        _table_ctx[key] = ctxs
+    return _table_ctx[key]
+
+
+def encode_table_device(columns: Sequence[DeviceColumn], n_streams: int = 4, device: Optional[int] = None):
+    """encode_chunk for every leaf of a chunk on the GPU (NativeWriter::write,
+    write/writer.rs:113-143, encodes the chunk's columns one after another;
+    they are independent, so here up to n_streams of them are in flight at
+    once, each through its own context and HIP stream).  A page's Basic LZ4
+    stream is one serial parse (latency-bound on one wave), so columns made
+    of such pages go first and overlap the rest.  Returns [(device uint8
+    chunk, page metas)] in column order, each byte-identical to the host
+    writer's (encode_column / encode_binary_column)."""
+    import threading
+
+    import torch
+
+    from .binary import encode_binary_column_device
+
+    cols = list(columns)
+    if not cols:
+        return []
+    dev = cols[0].values.device.index if device is None else device
+    ctxs = _table_contexts(dev, max(1, n_streams))
+    cur = torch.cuda.current_stream(dev)
+    for _, st in ctxs:
+        st.wait_stream(cur)  # the inputs were produced on the caller's stream
+
+    def cost(i):
+        o = cols[i].options or WriteOptions()
+        serial = o.default_compress_ratio is None and o.default_compression in (LZ4, SNAPPY)
+        return (not serial, -cols[i].values.numel() * cols[i].values.element_size())
+
+    order = sorted(range(len(cols)), key=cost)
+    out = [None] * len(cols)
+    lock = threading.Lock()
+    errors = []
+
+    def worker(k):
+        ctx, st = ctxs[k]
+        try:
+            with torch.cuda.device(dev), torch.cuda.stream(st):
+                while True:
+                    with lock:
+                        if not order or errors:
+                            return
+                        i = order.pop(0)
+                    c = cols[i]
+                    if c.offsets is not None:
+                        out[i] = encode_binary_column_device(c.values, c.offsets, c.validity, c.nullable, c.options,
+                                                             c.physical_type or 13, ctx=ctx)
+                    else:
+                        out[i] = encode_column_device(c.values, c.validity, c.nullable, c.options, ctx=ctx)
+        except Exception as e:  # noqa: BLE001 -- re-raised below, in the caller's thread
+            with lock:
+                errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(len(ctxs))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    for _, st in ctxs:
+        cur.wait_stream(st)
+    return out
+
+
 def encode_page(values: np.ndarray, validity=None, nullable: bool = False,
                 options: Optional[WriteOptions] = None, seed: Optional[int] = None) -> bytes:
     options = options or WriteOptions()

@@ -98,16 +98,96 @@ def test_config1_int64_none(ctx):
 
 def test_unsupported_options_are_nyi(ctx):
     """Zstd as the default codec (libzstd's compressor is not restated on the
-    device) and adaptive pages over 16384 rows report NotYetImplemented."""
+    device), pages with statistics over 65535 rows (the 16-bit rows of the
+    table words) and Boolean pages over 16384 rows report NotYetImplemented."""
     import pa_amd
 
-    tv = torch.arange(40000, dtype=torch.int32, device="cuda")
+    tv = torch.arange(70000, dtype=torch.int32, device="cuda")
     for opts in (pa_amd.WriteOptions(default_compression=2), pa_amd.WriteOptions(default_compression=2,
                                                                                   default_compress_ratio=1.2),
-                 pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=20000)):
+                 pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=65536)):
         with pytest.raises(pa_amd.StrawboatError) as e:
             pa_amd.encode_column_device(tv, None, False, opts, ctx=ctx)
         assert e.value.status == 2
+    with pytest.raises(pa_amd.StrawboatError) as e:
+        pa_amd.encode_column_device(torch.ones(20000, dtype=torch.bool, device="cuda"), None, False,
+                                    pa_amd.WriteOptions(max_page_size=20000), ctx=ctx)
+    assert e.value.status == 2
+
+
+@pytest.mark.parametrize("P", [20000, 40000, 65535])
+@pytest.mark.parametrize("kind", ["int32_mix", "f64_mix", "int64_freq", "int32_dict"])
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+def test_big_adaptive_pages(ctx, P, kind, nullable):
+    """Pages over 16384 rows with the adaptive cascade (their statistics'
+    tables in HBM): byte-identical to the host writer, decoded back."""
+    import pa_amd
+
+    rng = np.random.default_rng(P + len(kind))
+    n = 2 * P + 777
+    if kind == "int32_mix":
+        v = np.concatenate([rng.integers(0, 1 << 12, n // 2), np.repeat(rng.integers(0, 1 << 30, n // 64 + 1), 32)])[:n]
+        v = v.astype(np.int32)
+    elif kind == "f64_mix":
+        v = np.concatenate([np.round(rng.standard_normal(n // 2), 1), np.full(n - n // 2, 2.5)])
+    elif kind == "int64_freq":
+        v = np.where(rng.random(n) < 0.93, 1 << 40, rng.integers(0, 1 << 50, n)).astype(np.int64)
+    else:
+        v = rng.integers(0, 1000, n).astype(np.int32) * 100_003
+    valid = rng.random(n) > 0.1
+    for ratio in (1.2, 2.0):
+        opts = pa_amd.WriteOptions(default_compress_ratio=ratio, max_page_size=P)
+        host, hm = pa_amd.encode_column(v, valid, nullable, opts)
+        dev, dm = pa_amd.encode_column_device(torch.from_numpy(v.copy()).cuda(), torch.from_numpy(valid).cuda(),
+                                              nullable, opts, ctx=ctx)
+        assert [(m.length, m.num_values) for m in dm] == [(m.length, m.num_values) for m in hm]
+        assert dev.cpu().numpy().tobytes() == host
+        # decodes to the input on the valid rows (a null slot's bytes follow the codec: Appendix C)
+        ov, ovalid = O.read_column(host, [(m.length, m.num_values) for m in hm], v.dtype, nullable)
+        keep = valid if nullable else np.ones(n, bool)
+        assert (ov[keep].view(np.uint8).tobytes() == v[keep].view(np.uint8).tobytes())
+
+
+@pytest.mark.parametrize("codec", [0, 1, 3], ids=["none", "lz4", "snappy"])
+@pytest.mark.parametrize("P", [None, 300_000])
+def test_big_basic_pages(ctx, codec, P):
+    """Basic pages of any size (no statistics): max_page_size None writes the
+    whole column as one page (write/common.rs:54-58)."""
+    import pa_amd
+
+    rng = np.random.default_rng(codec)
+    n = 700_001
+    v = np.round(rng.standard_normal(n) * 1e4, 2)
+    valid = rng.random(n) > 0.1
+    for nullable in (False, True):
+        roundtrip(ctx, v, valid, nullable, pa_amd.WriteOptions(default_compression=codec, max_page_size=P))
+
+
+@pytest.mark.parametrize("opt", ["lz4", "dict", "freq", "adaptive"])
+def test_big_binary_pages(ctx, opt):
+    """Utf8 pages over 16384 rows: Basic LZ4 of any size, Dict / Freq /
+    adaptive up to 65535 rows, byte-identical to the host writer."""
+    import pa_amd
+
+    rng = np.random.default_rng(5)
+    P = 300_000 if opt == "lz4" else 50_000
+    n = 2 * P + 11
+    pool = [f"v{i}".encode() for i in range(700)]
+    strs = [pool[i] if r < 0.95 else str(x).encode()
+            for i, r, x in zip(rng.integers(0, 700, n), rng.random(n), rng.integers(0, 10**7, n))]
+    if opt == "freq":
+        strs = [s if rng.random() < 0.03 else b"common" for s in strs]
+    vals, offs = pa_amd.binary.strings_to_arrow(strs)
+    o = {"lz4": dict(default_compression=1), "dict": dict(default_compress_ratio=2.0, forced_codec=11),
+         "freq": dict(default_compress_ratio=2.0, forced_codec=13), "adaptive": dict(default_compress_ratio=2.0)}[opt]
+    opts = pa_amd.WriteOptions(max_page_size=P, **o)
+    valid = rng.random(n) > 0.1
+    host, hm = pa_amd.encode_binary_column(vals, offs, valid, True, opts, physical_type=pa_amd.UTF8)
+    dev, dm = pa_amd.encode_binary_column_device(torch.from_numpy(np.frombuffer(vals, np.uint8).copy()).cuda(),
+                                                 torch.from_numpy(offs).cuda(), torch.from_numpy(valid).cuda(), True,
+                                                 opts, pa_amd.UTF8, ctx=ctx)
+    assert [(m.length, m.num_values) for m in dm] == [(m.length, m.num_values) for m in hm]
+    assert dev.cpu().numpy().tobytes() == host
 
 
 def test_page_size_clamped_and_missing_validity(ctx):
@@ -123,3 +203,86 @@ def test_page_size_clamped_and_missing_validity(ctx):
     dev, dm = pa_amd.encode_column_device(torch.from_numpy(v).cuda(), None, True,
                                           pa_amd.WriteOptions(max_page_size=1024), ctx=ctx)
     assert dev.cpu().numpy().tobytes() == host
+
+
+def lz4_shapes(rng, n):
+    """byte patterns that exercise every branch of the wave LZ4 search:
+    incompressible (long skip steps), short and long matches, self-overlapping
+    runs, matches at the 64 KiB distance limit, hash collisions in a batch"""
+    return {
+        "random": rng.integers(0, 256, n, dtype=np.uint8),
+        "zeros": np.zeros(n, np.uint8),
+        "period3": np.resize(np.array([1, 2, 3], np.uint8), n),
+        "text": np.frombuffer(b"".join(str(x).encode() + b"," for x in rng.integers(0, 10**6, n // 4 + 1)), np.uint8)[:n],
+        "runs": np.repeat(rng.integers(0, 256, n // 37 + 1, dtype=np.uint8), 37)[:n],
+        "blocks": np.tile(rng.integers(0, 256, 4096, dtype=np.uint8), n // 4096 + 1)[:n],
+        "far": np.concatenate([rng.integers(0, 256, 65530, dtype=np.uint8)] * (n // 65530 + 1))[:n],
+        "sparse": np.where(rng.random(n) < 0.02, rng.integers(0, 256, n), 0).astype(np.uint8),
+        "mixed": np.concatenate([rng.integers(0, 256, n // 2, dtype=np.uint8), np.zeros(n - n // 2, np.uint8)]),
+    }
+
+
+@pytest.mark.parametrize("nbytes", [0, 5, 12, 13, 14, 100, 4096, 16384, 65536, 65544, 65552, 131072])
+def test_device_lz4_matches_host(ctx, nbytes):
+    """Basic LZ4 pages (ratio None, default codec LZ4): the wave-cooperative
+    compressor (sb_lz4c.h lz4_compress_wave) writes the host writer's bytes --
+    liblz4's greedy parse -- for every data shape, both table modes (pages
+    below / above LZ4_64Klimit = 65547 bytes) and tiny inputs."""
+    import pa_amd
+
+    rng = np.random.default_rng(nbytes)
+    dt = np.uint8 if nbytes <= 16384 else np.uint64
+    for name, b in lz4_shapes(rng, max(nbytes, 8)).items():
+        v = np.ascontiguousarray(b[:nbytes]).view(dt)
+        opts = pa_amd.WriteOptions(default_compression=1, max_page_size=max(len(v), 1))
+        assert roundtrip(ctx, v, np.ones(len(v), bool), False, opts) <= {frozenset({1}), frozenset()}, name
+
+
+@pytest.mark.parametrize("nbytes", [65535, 65546, 65547, 65548, 200_001])
+def test_device_lz4_binary_values_stream(ctx, nbytes):
+    """Odd stream sizes around LZ4_64Klimit through a Utf8 page's values
+    stream (one row holding the whole blob, and 1000-row pages of it)."""
+    import pa_amd
+
+    rng = np.random.default_rng(nbytes)
+    for name, b in lz4_shapes(rng, nbytes).items():
+        blob = (b % 128).astype(np.uint8).tobytes()  # ASCII: a valid Utf8 column
+        for rows in (1, 1000):
+            cuts = np.sort(rng.integers(0, nbytes, rows - 1)) if rows > 1 else np.zeros(0, np.int64)
+            offs = np.concatenate([[0], cuts, [nbytes]]).astype(np.int64)
+            opts = pa_amd.WriteOptions(default_compression=1, max_page_size=rows)
+            host, hm = pa_amd.encode_binary_column(blob, offs, None, False, opts, physical_type=pa_amd.UTF8)
+            tv = torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).cuda()
+            dev, dm = pa_amd.encode_binary_column_device(tv, torch.from_numpy(offs).cuda(), None, False, opts,
+                                                         pa_amd.UTF8, ctx=ctx)
+            assert dev.cpu().numpy().tobytes() == host, (name, rows)
+
+
+def test_encode_table_device_concurrent(ctx):
+    """encode_table_device: columns in flight on four contexts / streams give
+    each column the bytes of its own host encode (and of encode_column_device)."""
+    import pa_amd
+
+    rng = np.random.default_rng(12)
+    n = 50_000
+    f = np.round(rng.standard_normal(n) * 1e4, 2)
+    ints = rng.integers(0, 1 << 20, n).astype(np.int32)
+    valid = rng.random(n) > 0.1
+    strs = [str(x).encode() for x in rng.integers(0, 10**6, n)]
+    vals, offs = pa_amd.binary.strings_to_arrow(strs)
+    lz4 = pa_amd.WriteOptions(default_compression=1, max_page_size=8192)
+    ad = pa_amd.WriteOptions(default_compress_ratio=2.0, max_page_size=8192)
+    cols = [pa_amd.DeviceColumn(torch.from_numpy(f).cuda(), None, False, lz4),
+            pa_amd.DeviceColumn(torch.from_numpy(ints).cuda(), torch.from_numpy(valid).cuda(), True, ad),
+            pa_amd.DeviceColumn(torch.from_numpy(np.frombuffer(vals, np.uint8).copy()).cuda(), None, False, lz4,
+                                torch.from_numpy(offs).cuda(), pa_amd.UTF8),
+            pa_amd.DeviceColumn(torch.from_numpy(ints).cuda(), None, False, lz4),
+            pa_amd.DeviceColumn(torch.from_numpy(f).cuda(), torch.from_numpy(valid).cuda(), True, ad)]
+    hosts = [pa_amd.encode_column(f, None, False, lz4), pa_amd.encode_column(ints, valid, True, ad),
+             pa_amd.encode_binary_column(vals, offs, None, False, lz4, physical_type=pa_amd.UTF8),
+             pa_amd.encode_column(ints, None, False, lz4), pa_amd.encode_column(f, valid, True, ad)]
+    for rep in range(2):
+        got = pa_amd.encode_table_device(cols, n_streams=4)
+        for (c, m), (h, hm) in zip(got, hosts):
+            assert c.cpu().numpy().tobytes() == h
+            assert [(x.length, x.num_values) for x in m] == [(x.length, x.num_values) for x in hm]
