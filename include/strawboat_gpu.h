@@ -229,6 +229,28 @@ sb_status sb_decode_nested_planned(sb_ctx* ctx, sb_plan* plan, const sb_nested_o
  * status (SB_OK if every page decoded); *h_bad_page = its index or -1. */
 sb_status sb_plan_status(sb_ctx* ctx, sb_plan* plan, int64_t* h_bad_page);
 
+/* ---- page-level unit entry points (synchronous) -------------------------
+ * For a caller that walks the pages itself; the column decoders above fuse
+ * both steps into their page kernels.
+ *
+ * read_validity (read/read_basic.rs:36-63) of one flat nullable page at
+ * d_page: its [u32 def_len][hybrid RLE / bit-packed def levels] prefix, one
+ * bit-packed run (an RLE run is OutOfSpec, :59 unreachable!()), whose first
+ * `length` bits are written to the Arrow bitmap d_validity (32-bit words)
+ * at bit bit_offset; the bitmap's other bits are kept.  *h_consumed = the
+ * prefix bytes (4 + def_len): the values stream starts there.  def_len 0 is
+ * OutOfSpec unless length is 0 (nothing pushed, the array would not build). */
+sb_status sb_decode_page_validity(sb_ctx* ctx, const uint8_t* d_page, uint64_t page_len, uint64_t length,
+                                  uint32_t* d_validity, uint64_t bit_offset, uint64_t* h_consumed);
+/* The level streams of read_validity_nested (read/read_basic.rs:65-86) of one
+ * nested page: [u32 rows][u32 rep_len][u32 def_len][rep levels][def levels],
+ * each decoded by parquet2's HybridRleDecoder with bit width
+ * get_bit_width(max level) into num_levels u16 levels (d_rep, d_def).
+ * *h_rows = the page's row count, *h_consumed = 12 + rep_len + def_len. */
+sb_status sb_decode_page_levels(sb_ctx* ctx, const uint8_t* d_page, uint64_t page_len, uint64_t num_levels,
+                                uint32_t max_rep_level, uint32_t max_def_level, uint16_t* d_rep, uint16_t* d_def,
+                                uint32_t* h_rows, uint64_t* h_consumed);
+
 /* One-shot: plan + decode + wait + status.  The batch_read_array
  * equivalent for one flat primitive leaf. */
 sb_status sb_decode_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk,

@@ -31,6 +31,7 @@ EXPORTED = [
     "sb_encode_binary_device_bound", "sb_encode_binary_column_device", "sb_plan_nested_column",
     "sb_plan_nested_count", "sb_decode_nested_planned", "sb_parse_schema", "sb_file_open", "sb_file_close",
     "sb_file_last_error", "sb_file_num_columns", "sb_file_column", "sb_file_schema", "sb_file_upload",
+    "sb_decode_page_validity", "sb_decode_page_levels",
 ]
 
 MAX_NEST = 4
@@ -130,6 +131,11 @@ def lib():
     L.sb_plan_last_kernel_ms.restype = I32
     L.sb_decompress_values.argtypes = [P, I32, P, U64, U64, P]
     L.sb_decompress_values.restype = I32
+    L.sb_decode_page_validity.argtypes = [P, P, U64, U64, P, U64, ctypes.POINTER(U64)]
+    L.sb_decode_page_validity.restype = I32
+    L.sb_decode_page_levels.argtypes = [P, P, U64, U64, ctypes.c_uint32, ctypes.c_uint32, P, P,
+                                        ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(U64)]
+    L.sb_decode_page_levels.restype = I32
     L.sb_read_meta.argtypes = [P, U64, P, P, U64, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]
     L.sb_read_meta.restype = I32
     PU8 = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))

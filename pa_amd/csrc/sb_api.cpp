@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
@@ -21,13 +22,13 @@ struct sb_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
-  void* scr[4] = {nullptr, nullptr, nullptr, nullptr};  // sb::ctx_scratch
-  size_t scr_bytes[4] = {0, 0, 0, 0};
+  void* scr[sb::kCtxScratchSlots] = {};  // sb::ctx_scratch
+  size_t scr_bytes[sb::kCtxScratchSlots] = {};
 };
 
 namespace sb {
 void* ctx_scratch(sb_ctx* c, size_t bytes, int slot) {
-  if (!c || slot < 0 || slot >= 4) return nullptr;
+  if (!c || slot < 0 || slot >= kCtxScratchSlots) return nullptr;
   if (c->scr_bytes[slot] < bytes) {
     if (c->scr[slot]) {
       (void)hipStreamSynchronize(c->stream);  // earlier work on the stream may still use it
@@ -91,6 +92,7 @@ struct sb_plan {
   uint64_t n_leaves = 0;
   int offset_width = 0;
   uint64_t* d_bin = nullptr;  // [sizes n | bases n | total 1 | UTF-8 flags 1] then BinLaunch::cls (u32)
+  uint64_t* d_lb = nullptr;   // binary, every page staged: the fused pass's look-back states + counter
   uint32_t bin_grid = 0;      // staged-pass workgroups: the plan pass's staged page count
   uint32_t bin_lds = 0;       // dynamic LDS of the binary kernels (the largest page need, from the plan pass)
   uint64_t values_bytes = 0;
@@ -168,7 +170,7 @@ sb_status sb_ctx_create(int device, sb_ctx** out) {
 void sb_ctx_destroy(sb_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < sb::kCtxScratchSlots; i++)
     if (ctx->scr[i]) {
       (void)hipStreamSynchronize(ctx->stream);
       (void)hipFree(ctx->scr[i]);
@@ -209,6 +211,7 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_spill) (void)hipFree(p->d_spill);
   if (p->d_spill_jobs) (void)hipFree(p->d_spill_jobs);
   if (p->d_bin) (void)hipFree(p->d_bin);
+  if (p->d_lb) (void)hipFree(p->d_lb);
   if (p->d_lc) (void)hipFree(p->d_lc);
   if (p->d_nest) (void)hipFree(p->d_nest);
   if (p->inner) sb_plan_destroy(p->inner);
@@ -512,6 +515,13 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "plan alloc: scratch");
     }
+    // every page staged (no header-only or big pages): one fused pass sizes,
+    // bases and decodes them (k_bin_fused)
+    if (n_staged == n_pages && !p->n_big && !p->n_bin_jobs && !getenv("SB_NO_BIN_FUSED") &&
+        hipMalloc(&p->d_lb, (n_pages + 1) * sizeof(uint64_t)) != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "plan alloc: look-back");
+    }
   }
   *out = p;
   return SB_OK;
@@ -532,6 +542,14 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   if (!p->n_pages) return SB_OK;
   if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
   const size_t np = p->n_pages;
+  if (p->d_lb) {  // every page staged: sizes, bases and rows in one pass
+    sb::BinLaunch F{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np,
+                    p->d_bin + 2 * np, (uint8_t*)out->d_offsets, out->d_values, out->values_capacity,
+                    (uint32_t*)out->d_validity, p->d_status, p->d_jobs, nullptr, p->d_scratch, p->bin_lds, nullptr,
+                    (uint32_t*)(p->d_bin + 2 * np + 2), p->bin_grid, p->d_region, nullptr, p->n_big, p->d_lb};
+    if (sb::launch_binary(3, p->offset_width, F, ctx->stream))
+      return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  } else {
   // Every decode sizes its pages again (values bytes -> bases, and the list of
   // LZ4 / Snappy streams): the plan-time pass only sized the caller's buffers.
   HIP_TRY(ctx, hipMemsetAsync(p->d_defer + 2, 0, sizeof(uint32_t), ctx->stream));
@@ -554,6 +572,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   }
   if (sb::launch_binary(1, p->offset_width, L, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
   if (p->desc.physical_type == SB_T_UTF8 || p->desc.physical_type == SB_T_LARGE_UTF8) {
     // Utf8Array::try_new (read/array/binary.rs:305-306): invalid UTF-8 or an
     // offset inside a character is OutOfSpec for the page that holds it

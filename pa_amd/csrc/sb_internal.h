@@ -11,8 +11,9 @@ struct sb_ctx;
 
 namespace sb {
 
-// Grow-only device scratch owned by a context (slot < 4), reused across calls
-// on its stream; nullptr if the allocation fails.
+// Grow-only device scratch owned by a context (slot < kCtxScratchSlots),
+// reused across calls on its stream; nullptr if the allocation fails.
+constexpr int kCtxScratchSlots = 5;
 void* ctx_scratch(sb_ctx* ctx, size_t bytes, int slot);
 // Records a failure message on the context (sb_last_error) and returns st.
 int ctx_fail(sb_ctx* ctx, int st, const char* what, int hip_error = -1);
@@ -174,8 +175,10 @@ struct BinLaunch {
   uint8_t* region;        // big Extend pages' tables (PageDesc.reserved = offset + 1), or nullptr
   uint64_t* rneed;        // stage 2 (plan time) out: region bytes per page; lds_need: LDS bytes per page
   uint32_t n_big;         // big pages of the plan (0: their kernels are not launched)
+  uint64_t* lb;           // stage 3: look-back states (n_pages) + page counter
 };
-// stage 2: plan-time probe (lds_need / rneed per page).
+// stage 2: plan-time probe (lds_need / rneed per page); stage 3: the fused
+// single pass when every page is staged (sizes, bases, offsets, values).
 int launch_binary(int stage, int offset_width, const BinLaunch& a, void* stream);
 
 // Utf8 / LargeUtf8 columns after the decode: the checks of Utf8Array::try_new

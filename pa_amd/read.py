@@ -315,3 +315,44 @@ def unpack_bitmap(bitmap, n: int):
     bits = torch.arange(8, device=bitmap.device, dtype=torch.uint8)
     b = (bitmap[: (n + 7) // 8].unsqueeze(1) >> bits) & 1
     return b.reshape(-1)[:n].bool()
+
+
+def read_validity(page, length: int, out=None, bit_offset: int = 0, ctx: Optional[Context] = None):
+    """read_validity (read/read_basic.rs:36-63) of one flat nullable page on
+    the GPU (sb_decode_page_validity): page = its bytes (host bytes or a
+    device uint8 tensor).  Writes `length` bits at bit_offset of out (a device
+    int32 bitmap tensor, allocated when None) and returns (out, bytes of the
+    prefix: the values stream starts there)."""
+    import torch
+
+    ctx = resolve_context(ctx, page)
+    d = _as_device_bytes(page, ctx.device)
+    if out is None:
+        out = torch.zeros(max((bit_offset + length + 31) // 32, 1), dtype=torch.int32, device=f"cuda:{ctx.device}")
+    used = ctypes.c_uint64()
+    st = N.lib().sb_decode_page_validity(ctx._h, ctypes.c_void_p(d.data_ptr()), d.numel(), length,
+                                         ctypes.c_void_p(out.data_ptr()), bit_offset, ctypes.byref(used))
+    if st:
+        raise N.StrawboatError(st, ctx.error())
+    return out, used.value
+
+
+def read_levels(page, num_levels: int, max_rep_level: int, max_def_level: int, ctx: Optional[Context] = None):
+    """The rep / def level streams of one nested page (read_validity_nested,
+    read/read_basic.rs:65-86) on the GPU (sb_decode_page_levels) -> (rep,
+    def device int16 tensors of num_levels levels, the page's row count, the
+    header + level bytes)."""
+    import torch
+
+    ctx = resolve_context(ctx, page)
+    d = _as_device_bytes(page, ctx.device)
+    dev = f"cuda:{ctx.device}"
+    rep = torch.empty(max(num_levels, 1), dtype=torch.int16, device=dev)
+    dfl = torch.empty(max(num_levels, 1), dtype=torch.int16, device=dev)
+    rows, used = ctypes.c_uint32(), ctypes.c_uint64()
+    st = N.lib().sb_decode_page_levels(ctx._h, ctypes.c_void_p(d.data_ptr()), d.numel(), num_levels, max_rep_level,
+                                       max_def_level, ctypes.c_void_p(rep.data_ptr()), ctypes.c_void_p(dfl.data_ptr()),
+                                       ctypes.byref(rows), ctypes.byref(used))
+    if st:
+        raise N.StrawboatError(st, ctx.error())
+    return rep[:num_levels], dfl[:num_levels], rows.value, used.value

@@ -117,6 +117,11 @@ extern "C" {
     pub fn sb_snappy_compress_host(src: *const u8, n: u64, dst: *mut u8) -> u64;
     pub fn sb_decompress_values(ctx: *mut sb_ctx, physical_type: i32, d_stream: *const u8, stream_len: u64,
                                 length: u64, d_out: *mut c_void) -> i32;
+    pub fn sb_decode_page_validity(ctx: *mut sb_ctx, d_page: *const u8, page_len: u64, length: u64,
+                                   d_validity: *mut u32, bit_offset: u64, consumed: *mut u64) -> i32;
+    pub fn sb_decode_page_levels(ctx: *mut sb_ctx, d_page: *const u8, page_len: u64, num_levels: u64,
+                                 max_rep_level: u32, max_def_level: u32, d_rep: *mut u16, d_def: *mut u16,
+                                 rows: *mut u32, consumed: *mut u64) -> i32;
     pub fn sb_ctx_device(ctx: *const sb_ctx) -> i32;
     pub fn sb_plan_enable_timing(plan: *mut sb_plan, on: i32) -> i32;
     pub fn sb_plan_last_kernel_ms(ctx: *mut sb_ctx, plan: *mut sb_plan, ms: *mut f32) -> i32;
