@@ -2532,6 +2532,7 @@ struct BinArgs {
   uint32_t* cls;  // staged list [n] | header-only list [n] | validity bitmap positions [n] | big list [n] | 3 lengths
   uint8_t* region;     // big pages' tables (PageDesc.reserved = region offset + 1)
   uint64_t* rneed;     // plan time (k_bin_probe): region bytes per page
+  uint64_t* lb;        // fused pass: look-back state per page, then the page counter (zeroed by the host)
 };
 
 enum : uint32_t { BIN_BASIC = 0, BIN_ONE = 12, BIN_DICT = 11, BIN_FREQ = 13 };
@@ -3388,21 +3389,96 @@ __global__ __launch_bounds__(NT) void k_bin_scan(BinArgs a) {
   if (threadIdx.x == 0) *a.total = carry;
 }
 
+// Rows longer than this are copied by the whole wave (bin_emit_wave).
+constexpr uint32_t kRowDirect = 64;
+
+// len bytes of a staged page at sp to global dst, one lane: the dwords the
+// row covers whole as dword stores, the bytes it shares with its neighbours'
+// dwords as byte stores (byte-granular, so no merge is needed).
+__device__ __forceinline__ void copy_row(const LdsSrc& src, uint32_t sp, uint32_t len, uint8_t* dst) {
+  const uint32_t head = min(len, (uint32_t)((4 - ((uintptr_t)dst & 3)) & 3));
+  for (uint32_t i = 0; i < head; i++) dst[i] = (uint8_t)src.u8(sp + i);
+  uint32_t k = head;
+  for (; k + 4 <= len; k += 4) *(uint32_t*)(dst + k) = src.u32(sp + k);
+  for (; k < len; k++) dst[k] = (uint8_t)src.u8(sp + k);
+}
+// The same for one long row, by the whole wave.
+__device__ __forceinline__ void wave_copy_row(const LdsSrc& src, uint32_t sp, uint32_t len, uint8_t* dst) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t head = min(len, (uint32_t)((4 - ((uintptr_t)dst & 3)) & 3));
+  if (lane < head) dst[lane] = (uint8_t)src.u8(sp + lane);
+  const uint32_t nw = (len - head) / 4;
+  for (uint32_t w = lane; w < nw; w += 64) *(uint32_t*)(dst + head + 4 * w) = src.u32(sp + head + 4 * w);
+  const uint32_t t0 = head + 4 * nw;
+  if (lane < len - t0) dst[t0 + lane] = (uint8_t)src.u8(sp + t0 + lane);
+}
+
+// Arrow offsets and values of rows [0, n) of a staged page, wave-parallel
+// with one block barrier: wave w takes rows [w q, (w + 1) q), its first byte
+// from the other waves' totals; then 64 rows a step, one a lane, placed by a
+// DPP scan, offsets as one coalesced store, each lane writing its row
+// dword-aligned (copy_row) -- no LDS window, no barrier per tile as in
+// bin_emit.  Rows over kRowDirect bytes are copied by the wave.
+template <int OW, class LenF, class SrcF>
+__device__ void bin_emit_wave(const LdsSrc& src, uint32_t n, uint64_t R, uint64_t V, const BinArgs& a, LenF len_of,
+                              SrcF src_of) {
+  __shared__ uint64_t qtot[NW];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t q = (n + NW - 1) / NW, r0 = min(n, wv * q), r1 = min(n, r0 + q);
+  uint64_t part = 0;
+  for (uint32_t r = r0 + lane; r < r1; r += 64) part += len_of(r);
+  part = wave_sum64(part);
+  if (lane == 0) qtot[wv] = part;
+  __syncthreads();
+  uint64_t base = V;
+  for (uint32_t k = 0; k < wv; k++) base += qtot[k];
+  __syncthreads();  // (qtot is the next page's)
+  for (uint32_t c0 = r0; c0 < r1; c0 += 64) {
+    const uint32_t r = c0 + lane;
+    const bool in = r < r1;
+    const uint32_t l = in ? len_of(r) : 0u, sp = in ? src_of(r) : 0u;
+    const uint32_t incl = wave_incl_scan(l);
+    const uint64_t d = base + incl - l;
+    if (in) bin_put_off(a.out_offsets, R + r + 1, d + l, OW);
+    if (in && l <= kRowDirect) copy_row(src, sp, l, a.out_values + d);
+    for (uint64_t big = __ballot(in && l > kRowDirect); big; big &= big - 1) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(big);
+      const uint64_t dj = ((uint64_t)__shfl((uint32_t)(d >> 32), j, 64) << 32) | __shfl((uint32_t)d, j, 64);
+      wave_copy_row(src, __shfl(sp, j, 64), __shfl(l, j, 64), a.out_values + dj);
+    }
+    base += __builtin_amdgcn_readlane(incl, 63);
+  }
+}
+
+// Offsets and values of rows [0, n) through bin_emit_wave (staged pages) or
+// bin_emit (pages whose tables live in HBM).
+template <int OW, class Src, class LenF, class SrcF>
+__device__ __forceinline__ void bin_emit_any(Shared& sh, const Src& src, lds_u32* ea, uint32_t n, uint64_t R, uint64_t V,
+                                             const BinArgs& a, LenF len_of, SrcF src_of) {
+#ifndef SB_BIN_EMIT_BLOCK
+  if constexpr (kLdsSrc<Src>) {
+    bin_emit_wave<OW>(src, n, R, V, a, len_of, src_of);
+    return;
+  }
+#endif
+  bin_emit<OW>(sh, src, ea, n, R, V, a, len_of, src_of);
+}
+
 // The Extend rows of a parsed page (OneValue / Dict / Freq) whose tables are
 // built (dict_tables / freq_tables + freq_rows): offsets and values through
-// bin_emit.  All NT threads.
+// bin_emit_any.  All NT threads.
 template <int OW, class Src>
 __device__ __forceinline__ void bin_emit_extend(Shared& sh, const Src& s, const BinInfo& bi, TabBase<kLdsSrc<Src>> tb, lds_u32* ea,
                                 uint32_t n, uint64_t R, uint64_t V, const BinArgs& a) {
   constexpr bool L = kLdsSrc<Src>;
   if (bi.codec == BIN_ONE) {
     const uint32_t len = bi.L, top = bi.top;
-    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t) { return len; }, [&](uint32_t) { return top; });
+    bin_emit_any<OW>(sh, s, ea, n, R, V, a, [&](uint32_t) { return len; }, [&](uint32_t) { return top; });
   } else if (bi.codec == BIN_DICT) {
     const mptr<L, uint32_t> xi = tb.template at<uint32_t>(0);
     const mptr<L, uint64_t> tab = tb.template at<uint64_t>(bi.otab);
     const uint32_t k = bi.k;
-    bin_emit<OW>(sh, s, ea, n, R, V, a,
+    bin_emit_any<OW>(sh, s, ea, n, R, V, a,
                  [&](uint32_t i) { const uint32_t x = xi[i]; return x < k ? (uint32_t)(tab[x] >> 32) : 0u; },
                  [&](uint32_t i) { const uint32_t x = xi[i]; return x < k ? (uint32_t)tab[x] : 0u; });
   } else {  // Freq: exception rows by the bitmap + prefix popcount rank
@@ -3413,41 +3489,121 @@ __device__ __forceinline__ void bin_emit_extend(Shared& sh, const Src& s, const 
     const uint32_t len = bi.L, top = bi.top;
     auto rank = [&](uint32_t i) { return pref[i >> 5] + __popc(bits[i >> 5] & ((1u << (i & 31)) - 1)); };
     auto exc = [&](uint32_t i) { return (bits[i >> 5] >> (i & 31)) & 1u; };
-    bin_emit<OW>(sh, s, ea, n, R, V, a, [&](uint32_t i) { return exc(i) ? (uint32_t)(tab[rank(i)] >> 32) : len; },
+    bin_emit_any<OW>(sh, s, ea, n, R, V, a, [&](uint32_t i) { return exc(i) ? (uint32_t)(tab[rank(i)] >> 32) : len; },
                  [&](uint32_t i) { return exc(i) ? (uint32_t)tab[rank(i)] : top; });
   }
 }
 
-template <int OW>
-__global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
+// Look-back state of a page in the fused pass: its values bytes (low 62
+// bits) and whether that is the page's own size (AGG) or the inclusive
+// prefix through it (INCL).
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 1ull << 63, kLbVal = kLbAgg - 1;
+
+// The values base of `page` from its predecessors' look-back states, wave 0
+// (the single-pass chained scan with a wave-wide look-back: 64 predecessor
+// states per probe; the nearest INCL ends the walk, AGGs before it add up; a
+// page waits only for lower pages, which resident workgroups claimed before
+// it, so every wait ends).  Returns the base in every lane.
+__device__ uint64_t lookback(uint64_t* lb, uint32_t page, uint64_t S) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (page == 0) {
+    if (lane == 0) __hip_atomic_store(&lb[0], kLbIncl | S, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&lb[page], kLbAgg | S, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t acc = 0;
+  for (int64_t top = (int64_t)page - 1;;) {
+    const int64_t j = top - (int64_t)lane;  // lane 0: the nearest predecessor
+    const uint64_t v = j >= 0 ? __hip_atomic_load(&lb[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+    const uint64_t incl = __ballot((v & kLbIncl) != 0);
+    const uint32_t k = incl ? (uint32_t)__builtin_ctzll(incl) : 63u;  // lanes 0..k decide this probe
+    const uint64_t upto = k == 63 ? ~0ull : ((2ull << k) - 1);
+    if (__ballot(!(v & (kLbAgg | kLbIncl))) & upto) {  // some needed state not published yet
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    acc += wave_sum64(lane <= k ? (v & kLbVal) : 0ull);
+    if (incl) break;
+    top -= 64;
+  }
+  if (lane == 0) __hip_atomic_store(&lb[page], kLbIncl | (acc + S), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return acc;
+}
+
+// Pass 2 over the staged pages (FUSED = false: bases from k_bin_size /
+// k_bin_scan), or the whole decode in one pass when every page of the plan
+// is staged (FUSED = true: pages claimed in order from a counter, each sized
+// from its own tables and based by lookback, so k_bin_size / k_bin_scan do
+// not run).
+template <int OW, bool FUSED>
+__device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
   extern __shared__ u32x4 stage[];
   __shared__ Shared sh;
   __shared__ BinInfo bi;
   __shared__ Stream idx;
+  __shared__ uint32_t claimed;
+  __shared__ uint64_t base_v;
   uint8_t* lds = (uint8_t*)stage;
   const uint32_t tid = threadIdx.x;
-  const uint32_t n_staged = a.cls[4 * a.n_pages];
-  for (uint32_t i = blockIdx.x; i < n_staged; i += gridDim.x) {
-    const uint32_t page = a.cls[i];
-    const PageDesc pd = a.pages[page];
-    if (pd.reserved) continue;  // k_bin_big's
-    const uint32_t n = pd.num_values;
-    const uint64_t R = pd.row_off, V = a.bases[page];
-    if (tid == 0) {
-      sh.err = a.status[page];  // sizing errors stand
-      if (!sh.err && V + a.sizes[page] > a.values_cap) sh.err = ST_OUT_OF_SPEC;
+  const uint32_t n_staged = FUSED ? a.n_pages : a.cls[4 * a.n_pages];
+  for (uint32_t i = blockIdx.x;; i += gridDim.x) {
+    if (FUSED) {
+      if (tid == 0) claimed = atomicAdd((uint32_t*)(a.lb + a.n_pages), 1u);
+      __syncthreads();
+      i = claimed;
+      __syncthreads();
     }
+    if (i >= n_staged) break;
+    const uint32_t page = FUSED ? i : a.cls[i];
+    const PageDesc pd = a.pages[page];
+    if (!FUSED && pd.reserved) continue;  // k_bin_big's
+    const uint32_t n = pd.num_values;
+    const uint64_t R = pd.row_off;
     const uint32_t stage_end = ((pd.byte_len + 15 + kStagePad) + 15) & ~15u;
+    if (tid == 0) {
+      sh.err = FUSED ? (pd.reserved || stage_end + 64 > a.lds_bytes ? ST_NYI : ST_OK) : a.status[page];  // sizing errors stand
+      if (!FUSED && !sh.err && a.bases[page] + a.sizes[page] > a.values_cap) sh.err = ST_OUT_OF_SPEC;
+    }
     __syncthreads();
-    if (sh.err || stage_end + 64 > a.lds_bytes) {
+    if (!FUSED && (sh.err || stage_end + 64 > a.lds_bytes)) {
       __syncthreads();
       if (tid == 0 && sh.err && !a.status[page]) a.status[page] = sh.err;
       continue;
     }
-    const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
+    uint32_t base = 0;
+    if (!sh.err) {
+      base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
+      if (tid == 0) bin_parse<OW>(LdsSrc{(const uint32_t*)stage, base}, sh, bi, pd, a.nullable, true, stage_end,
+                                  a.lds_bytes, &idx);
+      __syncthreads();
+    }
     LdsSrc s{(const uint32_t*)stage, base};
-    if (tid == 0) bin_parse<OW>(s, sh, bi, pd, a.nullable, true, stage_end, a.lds_bytes, &idx);
-    __syncthreads();
+    const TabBase<true> tb{(lds_u8*)stage + bi.tb};
+    if (FUSED) {  // tables (and so the size), then the base
+      if (!sh.err) {
+        if (bi.codec == BIN_DICT) {
+          dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, true);
+        } else if (bi.codec == BIN_FREQ) {
+          freq_tables(s, sh, bi, tb, pd, nullptr);
+          if (!sh.err) freq_rows(s, sh, bi, tb, n);
+        } else if (bi.codec == 1 || bi.codec == 3) {
+          set_err(sh, ST_NYI);  // (a plan with Basic LZ4 / Snappy pages is not fused)
+        }
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const uint64_t S = sh.err ? 0 : bi.S;
+        const uint64_t v = lookback(a.lb, page, S);
+        if (tid == 0) {
+          base_v = v;
+          a.bases[page] = v;
+          a.sizes[page] = S;
+          if (!sh.err && v + S > a.values_cap) sh.err = ST_OUT_OF_SPEC;
+        }
+      }
+      __syncthreads();
+    }
+    const uint64_t V = FUSED ? base_v : a.bases[page];
     if (!sh.err) {
       if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
       if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);  // Extend codecs push 0 first
@@ -3503,12 +3659,13 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
           }
         }
       } else {
-        const TabBase<true> tb{(lds_u8*)stage + bi.tb};
-        if (bi.codec == BIN_DICT) {
-          dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, false);
-        } else if (bi.codec == BIN_FREQ) {
-          freq_tables(s, sh, bi, tb, pd, nullptr);
-          if (!sh.err) freq_rows(s, sh, bi, tb, n);
+        if (!FUSED) {
+          if (bi.codec == BIN_DICT) {
+            dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, false);
+          } else if (bi.codec == BIN_FREQ) {
+            freq_tables(s, sh, bi, tb, pd, nullptr);
+            if (!sh.err) freq_rows(s, sh, bi, tb, n);
+          }
         }
         if (!sh.err) bin_emit_extend<OW>(sh, s, bi, tb, (lds_u32*)((lds_u8*)stage + bi.emit), n, R, V, a);
       }
@@ -3517,6 +3674,15 @@ __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
     if (tid == 0) a.status[page] = sh.err;
     __syncthreads();
   }
+}
+
+template <int OW>
+__global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
+  bin_decode_pages<OW, false>(a);
+}
+template <int OW>
+__global__ __launch_bounds__(NT) void k_bin_fused(BinArgs a) {
+  bin_decode_pages<OW, true>(a);
 }
 
 // Big Extend pages (OneValue / Dict / Freq pages whose tables do not fit one
@@ -4710,7 +4876,7 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
   const uint32_t lds = L.lds_bytes ? std::min(L.lds_bytes, kDeferredLds) : kDeferredLds;
   sbk::BinArgs a{L.chunk, L.pages, L.n_pages, L.nullable, L.sizes, L.bases, L.total, L.out_offsets, L.out_values,
                  L.values_cap, L.out_validity, L.status, lds, L.jobs, L.job_count, L.scratch, L.lds_need, L.cls,
-                 L.region, L.rneed};
+                 L.region, L.rneed, L.lb};
   hipStream_t st = (hipStream_t)stream;
   const dim3 block(sbk::NT);
   // staged passes: one workgroup per listed page (grid-stride), as many
@@ -4725,6 +4891,8 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
   ensure_lds_attr(sbk::k_bin_size<8>, (int)kDeferredLds);
   ensure_lds_attr(sbk::k_bin_decode<4>, (int)kDeferredLds);
   ensure_lds_attr(sbk::k_bin_decode<8>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_fused<4>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_fused<8>, (int)kDeferredLds);
   if (stage == 2) {  // plan time: per-page LDS / region needs
     if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_probe<8>, cgrid, block, 0, st, a);
     else hipLaunchKernelGGL(sbk::k_bin_probe<4>, cgrid, block, 0, st, a);
@@ -4740,6 +4908,10 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
       if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<4, 0>), bgrid, block, sbk::kBigLds, st, a);
     }
     hipLaunchKernelGGL(sbk::k_bin_scan, dim3(1), block, 0, st, a);
+  } else if (stage == 3) {  // every page staged: size, base and decode in one pass
+    if (hipMemsetAsync(L.lb, 0, (L.n_pages + 1) * sizeof(uint64_t), st) != hipSuccess) return -1;
+    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_fused<8>, grid, block, lds, st, a);
+    else hipLaunchKernelGGL(sbk::k_bin_fused<4>, grid, block, lds, st, a);
   } else {
     if (offset_width == 8) {
       hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, lds, st, a);

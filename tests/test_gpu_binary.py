@@ -168,3 +168,16 @@ def test_binary_ragged_pages(ctx, page_rows):
     for opts in (O.WriteOptions.make(), O.WriteOptions.make(default_codec=O.LZ4), O.WriteOptions.make(ratio=2.0)):
         check(ctx, s, v, True, page_rows, opts, 13)
         check(ctx, s, None, False, page_rows, opts, 13)
+
+
+@pytest.mark.parametrize("opt", ["plain", "dict", "freq", "adaptive", "zstd"])
+def test_binary_two_pass_path(ctx, opt, monkeypatch):
+    """The two-pass decode (k_bin_size -> k_bin_scan -> k_bin_decode) that a
+    plan with header-only or big pages takes, forced on an all-staged column
+    (SB_NO_BIN_FUSED): the same bytes as the fused pass."""
+    monkeypatch.setenv("SB_NO_BIN_FUSED", "1")
+    rng = np.random.default_rng(9)
+    s = strings("freq" if opt == "freq" else "rand", 5000, rng)
+    v = rng.random(5000) > 0.2
+    assert check(ctx, s, v, True, 1000, O.WriteOptions.make(**OPTS[opt]), 13)
+    assert check(ctx, s, None, False, 777, O.WriteOptions.make(**OPTS[opt]), 12)

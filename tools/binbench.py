@@ -1,4 +1,4 @@
-"""Utf8 column decode time per C5 string kind: python tools/binbench.py [rows]"""
+"""Utf8 column decode time per C5 string kind: python tools/binbench.py [rows] [kind,kind...]"""
 import os
 import sys
 
@@ -16,7 +16,8 @@ def main():
 
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 8 * 1024 * 1024
     rng = np.random.default_rng(5)
-    for kind in ["dict", "freq", "one", "lz4"]:
+    kinds = sys.argv[2].split(",") if len(sys.argv) > 2 else ["dict", "freq", "one", "lz4"]
+    for kind in kinds:
         svals, soffs = bench.WorkloadC5._strings(kind, rows, rng)
         opts = pa_amd.WriteOptions(default_compression=1 if kind == "lz4" else 0,
                                    default_compress_ratio=None if kind == "lz4" else 2.0, max_page_size=8192, seed=3)

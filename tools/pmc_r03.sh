@@ -2,7 +2,7 @@
 # --pmc passes) and a kernel trace of the C2 headline, C3, C4 and C5 decodes
 # of this tree.  Outputs: gpurun_out/r03pmc/ (summaries: <wl>_traffic.json).
 set -o pipefail
-out=gpurun_out/r03pmc
+out=${OUT:-gpurun_out/r03pmc}
 mkdir -p $out
 commit=${COMMIT:-unknown}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
