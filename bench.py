@@ -289,7 +289,15 @@ def cpu_info() -> dict:
                     break
     except OSError:
         pass
-    return {"cpu_model": model, "nproc": os.cpu_count()}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count()
+    th = cpu_threads()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": aff,
+            "cores_note": f"the 'all cores' leg uses {th} threads: this GPU's CPU allotment on the box "
+                          f"(OMP_NUM_THREADS = {os.environ.get('OMP_NUM_THREADS', 'unset')}; {os.cpu_count()} CPUs "
+                          f"serve 8 GPUs), not the whole node"}
 
 
 def cpu_threads() -> int:
@@ -800,7 +808,7 @@ class WorkloadC5:
             t0 = time.perf_counter()
             cols = [pa.DeviceColumn(t[0], None, False, opts, t[1], pa.UTF8) if dt == "utf8" else
                     pa.DeviceColumn(t[0], t[1], nullable, opts) for dt, opts, nullable, t in enc]
-            chunks = pa.encode_table_device(cols, n_streams=4, device=device)
+            chunks = pa.encode_table_device(cols, n_streams=int(os.environ.get("SB_ENC_STREAMS", "4")), device=device)
             torch.cuda.synchronize()
             dt_s = time.perf_counter() - t0
             if rep:
