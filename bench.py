@@ -786,17 +786,45 @@ class WorkloadC5:
         # device encode of every column (values in HBM): a warm-up pass (context
         # scratch), then a timed pass; byte-identical to the host writer
         self.encode_gpu_s, self.byte_identical = self._encode_device(torch, pa, enc, device)
-        # decoders over the device-encoded chunks, columns over 4 streams (LZ4 ones first)
-        order = sorted(range(len(specs)), key=lambda i: specs[i][1] != "lz4")
-        home = {ci: self.ss.ctxs[j % 4] for j, ci in enumerate(order)}
+        # decoders over the device-encoded chunks: the fixed-width and Boolean
+        # leaves of one type and nullability as one plan each
+        # (pa_amd.ColumnGroupDecoder: their chunks back to back, as in a file),
+        # the Utf8 leaves one plan each; then longest first onto the least
+        # loaded of the 4 streams (each unit's cost from one timed decode)
+        groups = {}
         for ci, col in enumerate(self.cols):
-            dt, chunk_d, metas = col[0], self.dev_chunks[ci], col[5]
-            if dt == "utf8":
-                dec = pa.BinaryColumnDecoder(chunk_d, metas, pa.UTF8, False, ctx=home[ci])
-            else:
-                dec = pa.ColumnDecoder(chunk_d, metas, dt, col[6], ctx=home[ci])
-            col[1], col[2] = dec, dec.alloc_outputs()
+            if col[0] != "utf8":
+                groups.setdefault((np.dtype(col[0]).str, col[6]), []).append(ci)
+        self.units = []
+        for cis in groups.values():
+            g = pa.ColumnGroupDecoder([(self.dev_chunks[ci], self.cols[ci][5]) for ci in cis], self.cols[cis[0]][0],
+                                      self.cols[cis[0]][6], ctx=self.ss.ctxs[0])
+            outs = g.alloc_outputs()
+            for i, ci in enumerate(cis):
+                self.cols[ci][1], self.cols[ci][2] = g, g.column(i, *outs)
+            self.units.append([g, outs])
+        for ci, col in enumerate(self.cols):
+            if col[0] == "utf8":
+                dec = pa.BinaryColumnDecoder(self.dev_chunks[ci], col[5], pa.UTF8, False, ctx=self.ss.ctxs[0])
+                col[1], col[2] = dec, dec.alloc_outputs()
+                self.units.append([dec, col[2]])
         del self.dev_chunks
+        cost = []
+        for u in self.units:
+            u[0].decode_async(*u[1])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            u[0].decode_async(*u[1])
+            torch.cuda.synchronize()
+            cost.append(time.perf_counter() - t0)
+        load = [0.0] * len(self.ss.ctxs)
+        order = sorted(range(len(self.units)), key=lambda i: -cost[i])
+        for i in order:
+            s_ = min(range(len(load)), key=lambda j: load[j])
+            load[s_] += cost[i]
+            self.units[i][0].ctx = self.ss.ctxs[s_]
+        self.units = [self.units[i] for i in order]
+        self.n_launch_units = len(self.units)
         torch.cuda.synchronize()
 
     def _encode_device(self, torch, pa, enc, device):
@@ -872,12 +900,12 @@ class WorkloadC5:
 
     @property
     def decs(self):
-        return [c[1] for c in self.cols]
+        return [u[0] for u in self.units]
 
     def step(self, k):
         self.ss.fork()
-        for col in self.cols:
-            col[1].decode_async(*col[2])
+        for dec, outs in self.units:
+            dec.decode_async(*outs)
         self.ss.join()
 
     def verify(self, torch) -> bool:
@@ -1147,6 +1175,8 @@ def main():
             "bit_exact": bool(ok5),
             "scaling": "strong",
             "parallelism": f"columns round-robin over {world} rank(s) (column ci on rank ci % {world})",
+            "decode_units": f"{wl5.n_launch_units} plans per step: fixed-width / Boolean leaves grouped by type and "
+                            f"nullability (pa_amd.ColumnGroupDecoder), one per Utf8 leaf; longest first over 4 streams",
             "traffic": load_traffic("c5_mixed_64col"),
         }
         if do_cpu:

@@ -134,6 +134,16 @@ const char* sb_status_str(int status);
 sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk,
                          uint64_t chunk_len, const sb_page_meta* h_metas, uint64_t n_pages,
                          sb_plan** out);
+/* The same over pages placed at caller-chosen rows: page i decodes into
+ * rows [h_row_offsets[i], + num_values) of the outputs (non-decreasing, no
+ * overlap; rows in gaps are not written).  Several columns of one type and
+ * nullability whose chunks lie back to back in d_chunk (as the columns of a
+ * file do) become one plan and one launch sequence, each column at its own
+ * row base (a multiple of 32 keeps its validity word-aligned).  Fixed-width
+ * and Boolean columns only. */
+sb_status sb_plan_column_at(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                            const sb_page_meta* h_metas, uint64_t n_pages, const uint64_t* h_row_offsets,
+                            sb_plan** out);
 void sb_plan_destroy(sb_plan* plan);
 uint64_t sb_plan_num_rows(const sb_plan* plan);
 uint64_t sb_plan_num_pages(const sb_plan* plan);

@@ -23,3 +23,4 @@ from .binary import (  # noqa: F401,E402
 )
 from .nested import ListColumnDecoder, NestedColumnDecoder, batch_read_list, encode_list_column  # noqa: F401,E402
 from .file import Leaf, StrawboatFile, parse_schema  # noqa: F401,E402
+from .table import ColumnGroupDecoder  # noqa: F401,E402

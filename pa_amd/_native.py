@@ -31,7 +31,7 @@ EXPORTED = [
     "sb_encode_binary_device_bound", "sb_encode_binary_column_device", "sb_plan_nested_column",
     "sb_plan_nested_count", "sb_decode_nested_planned", "sb_parse_schema", "sb_file_open", "sb_file_close",
     "sb_file_last_error", "sb_file_num_columns", "sb_file_column", "sb_file_schema", "sb_file_upload",
-    "sb_decode_page_validity", "sb_decode_page_levels",
+    "sb_decode_page_validity", "sb_decode_page_levels", "sb_plan_column_at",
 ]
 
 MAX_NEST = 4
@@ -112,6 +112,8 @@ def lib():
     L.sb_status_str.restype = ctypes.c_char_p
     L.sb_plan_column.argtypes = [P, ctypes.POINTER(ColumnDescC), P, U64, ctypes.POINTER(PageMetaC), U64, PP]
     L.sb_plan_column.restype = I32
+    L.sb_plan_column_at.argtypes = [P, ctypes.POINTER(ColumnDescC), P, U64, ctypes.POINTER(PageMetaC), U64, P, PP]
+    L.sb_plan_column_at.restype = I32
     L.sb_plan_destroy.argtypes = [P]
     L.sb_plan_destroy.restype = None
     L.sb_plan_num_rows.argtypes = [P]

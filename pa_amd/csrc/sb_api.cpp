@@ -244,6 +244,27 @@ sb_status sb_plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t*
   return plan_column(ctx, desc, d_chunk, chunk_len, h_metas, n_pages, out, kRegionsProbe);
 }
 
+sb_status sb_plan_column_at(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
+                            const sb_page_meta* h_metas, uint64_t n_pages, const uint64_t* h_row_offsets,
+                            sb_plan** out) {
+  if (!ctx || !desc || !out || (n_pages && (!h_metas || !h_row_offsets))) return fail(ctx, SB_E_ARG, "null argument");
+  if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
+  if (desc->physical_type >= SB_T_BINARY && desc->physical_type <= SB_T_LARGE_UTF8)
+    return fail(ctx, SB_E_ARG, "binary columns are planned with sb_plan_column");
+  std::vector<sb::PageDesc> pages(n_pages);
+  uint64_t off = 0, end = 0;
+  for (uint64_t i = 0; i < n_pages; i++) {
+    const sb_page_meta& m = h_metas[i];
+    if (m.length > 0xFFFFFFFFull || m.num_values > 0xFFFFFFFFull)
+      return fail(ctx, SB_E_ARG, "page %llu exceeds u32 sizes", (unsigned long long)i);
+    if (h_row_offsets[i] < end) return fail(ctx, SB_E_ARG, "page %llu overlaps the rows before it", (unsigned long long)i);
+    pages[i] = sb::PageDesc{off, h_row_offsets[i], (uint32_t)m.length, (uint32_t)m.num_values, 0};
+    off += m.length;
+    end = h_row_offsets[i] + m.num_values;
+  }
+  return plan_pages(ctx, desc, d_chunk, chunk_len, std::move(pages), out, kRegionsProbe);
+}
+
 static sb_status plan_column(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
                              const sb_page_meta* h_metas, uint64_t n_pages, sb_plan** out, int regions) {
   if (!ctx || !desc || !out || (!h_metas && n_pages)) return fail(ctx, SB_E_ARG, "null argument");

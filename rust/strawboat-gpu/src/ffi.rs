@@ -64,6 +64,9 @@ extern "C" {
                           out: *mut *mut sb_plan) -> i32;
     pub fn sb_decode_planned(ctx: *mut sb_ctx, plan: *mut sb_plan, out: *const sb_primitive_out) -> i32;
     pub fn sb_plan_status(ctx: *mut sb_ctx, plan: *mut sb_plan, bad_page: *mut i64) -> i32;
+    pub fn sb_plan_column_at(ctx: *mut sb_ctx, desc: *const sb_column_desc, d_chunk: *const u8, chunk_len: u64,
+                             metas: *const sb_page_meta, n_pages: u64, row_offsets: *const u64,
+                             out: *mut *mut sb_plan) -> i32;
     pub fn sb_plan_destroy(plan: *mut sb_plan);
     pub fn sb_plan_num_rows(plan: *const sb_plan) -> u64;
     pub fn sb_plan_values_bytes(plan: *const sb_plan) -> u64;
