@@ -2715,7 +2715,11 @@ __device__ bool bin_parse(const Src& s, Shared& sh, BinInfo& bi, const PageDesc&
   if (lds) {
     const uint64_t zt = align16(stage_end + L.end);
     const uint64_t em = zt + (zstd ? kZTablesBytes : 0);
+#ifdef SB_BIN_EMIT_BLOCK
     const uint64_t need = em + kEmitBytes + kStagePad;
+#else
+    const uint64_t need = em + kStagePad;  // (staged pages emit through bin_emit_wave: no LDS window)
+#endif
     if (need > lds_bytes) { set_err(sh, ST_NYI); return false; }  // (the plan made it a big page)
     bi.ztab = (uint32_t)zt;
     bi.emit = (uint32_t)em;
@@ -3535,6 +3539,13 @@ __device__ uint64_t lookback(uint64_t* lb, uint32_t page, uint64_t S) {
 // is staged (FUSED = true: pages claimed in order from a counter, each sized
 // from its own tables and based by lookback, so k_bin_size / k_bin_scan do
 // not run).
+#ifdef SB_BIN_PHASES  // A/B instrumentation: per fused page, s_memrealtime at each phase boundary
+__device__ uint64_t sb_dbg_phase[4096 * 6];
+#define SB_PHASE(k) do { if (FUSED && threadIdx.x == 0 && page < 4096) sb_dbg_phase[page * 6 + (k)] = wall_clock64(); } while (0)
+#else
+#define SB_PHASE(k) do { } while (0)
+#endif
+
 template <int OW, bool FUSED>
 __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
   extern __shared__ u32x4 stage[];
@@ -3557,6 +3568,7 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
     const uint32_t page = FUSED ? i : a.cls[i];
     const PageDesc pd = a.pages[page];
     if (!FUSED && pd.reserved) continue;  // k_bin_big's
+    SB_PHASE(0);
     const uint32_t n = pd.num_values;
     const uint64_t R = pd.row_off;
     const uint32_t stage_end = ((pd.byte_len + 15 + kStagePad) + 15) & ~15u;
@@ -3579,6 +3591,7 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
     }
     LdsSrc s{(const uint32_t*)stage, base};
     const TabBase<true> tb{(lds_u8*)stage + bi.tb};
+    SB_PHASE(1);
     if (FUSED) {  // tables (and so the size), then the base
       if (!sh.err) {
         if (bi.codec == BIN_DICT) {
@@ -3591,6 +3604,7 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
         }
       }
       __syncthreads();
+      SB_PHASE(2);
       if (tid < 64) {
         const uint64_t S = sh.err ? 0 : bi.S;
         const uint64_t v = lookback(a.lb, page, S);
@@ -3604,6 +3618,7 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
       __syncthreads();
     }
     const uint64_t V = FUSED ? base_v : a.bases[page];
+    SB_PHASE(3);
     if (!sh.err) {
       if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
       if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);  // Extend codecs push 0 first
@@ -3671,6 +3686,7 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
       }
     }
     __syncthreads();
+    SB_PHASE(4);
     if (tid == 0) a.status[page] = sh.err;
     __syncthreads();
   }
@@ -4940,6 +4956,12 @@ int launch_utf8_check(int offset_width, const Utf8Launch& a, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb
+
+#ifdef SB_BIN_PHASES
+extern "C" int sb_debug_bin_phases(uint64_t* host, uint64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(sbk::sb_dbg_phase), std::min<uint64_t>(n, 4096 * 6) * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 namespace sb {
 int launch_inflate(const InflateLaunch& a, void* stream) {
