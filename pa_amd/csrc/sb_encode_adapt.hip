@@ -41,7 +41,7 @@ namespace sba {
 
 constexpr int NT = 256, NW = NT / 64;
 constexpr uint32_t kMaxRows = 16384;      // pages whose statistics' tables fit the LDS work area
-constexpr uint32_t kMaxBigRows = 65535;   // pages with statistics, tables in HBM (16-bit rows in the table words)
+constexpr uint32_t kMaxNarrowRows = 65535;  // table words with 16-bit rows; larger pages use 64-bit words
 constexpr uint32_t SC = 10, SS = 64, kSample = SC * SS;
 
 enum : int { C_NONE = 0, C_LZ4 = 1, C_ZSTD = 2, C_SNAPPY = 3, C_RLE = 10, C_DICT = 11, C_ONE = 12, C_FREQ = 13, C_BP = 14,
@@ -138,6 +138,7 @@ struct Sh {
 };
 
 struct Ctx {
+  bool wide;        // pages over 65535 rows: 64-bit table words (count << 32 | row + 1), multi-container roaring
   uint32_t* work;   // work area: hash tables, run starts, bitmaps, the Snappy table (LDS, or HBM for big pages)
   uint8_t* lz4;     // LDS: the wave LZ4 compressor's tables (sbc::kLz4WaveLds bytes)
   uint32_t work_bytes;
@@ -288,16 +289,62 @@ __device__ __forceinline__ bool room(const Ctx& c, Sh& sh, uint64_t end) {
 }
 
 // ---------------------------------------------------------------------------
-// LDS hash table: word = count << 16 | (first row + 1); S slots (pow2)
+// Open-addressing hash table, S slots (pow2): word = count << 16 | (first row
+// + 1) in LDS, or for pages over 65535 rows (HBM) count << 32 | (row + 1);
+// after the ids are assigned, count is replaced by the id.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t tab_slots(uint32_t n) {
   uint32_t s = 64;
   while (s < 2 * n) s <<= 1;
   return s;
 }
+struct Tab {
+  uint32_t* w;
+  bool wide;
+  __device__ __forceinline__ uint64_t* w64() const { return (uint64_t*)w; }
+  __device__ __forceinline__ uint32_t row1(uint32_t h) const {  // first row + 1, 0 = empty
+    return wide ? (uint32_t)w64()[h] : (w[h] & 0xFFFFu);
+  }
+  __device__ __forceinline__ uint32_t hi(uint32_t h) const {  // count, or the id after set()
+    return wide ? (uint32_t)(w64()[h] >> 32) : (w[h] >> 16);
+  }
+  __device__ __forceinline__ void set(uint32_t h, uint32_t hi_v, uint32_t row1_v) const {
+    if (wide) w64()[h] = ((uint64_t)hi_v << 32) | row1_v;
+    else w[h] = (hi_v << 16) | row1_v;
+  }
+  __device__ void clear(uint32_t S) const {
+    for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) {
+      if (wide) w64()[i] = 0;
+      else w[i] = 0;
+    }
+  }
+};
 template <class Same>
-__device__ __forceinline__ uint32_t tab_insert_h(uint32_t* tab, uint32_t S, uint32_t r, uint64_t hv, Same same) {
+__device__ __forceinline__ uint32_t tab_insert_h(const Tab& t, uint32_t S, uint32_t r, uint64_t hv, Same same) {
   uint32_t h = (uint32_t)(hv >> 32) & (S - 1);
+  if (t.wide) {
+    uint64_t* tab = t.w64();
+    for (;;) {
+      uint64_t e = tab[h];
+      if (e == 0) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&tab[h], 0ull, (1ull << 32) | (r + 1));
+        if (prev == 0) return h;
+        e = prev;
+      }
+      const uint32_t o = (uint32_t)e - 1;
+      if (same(o)) {
+        uint64_t old = atomicAdd((unsigned long long*)&tab[h], 1ull << 32) + (1ull << 32);
+        while ((uint32_t)old > r + 1) {  // keep the smallest row
+          const uint64_t prev = atomicCAS((unsigned long long*)&tab[h], old, (old & ~0xFFFFFFFFull) | (r + 1));
+          if (prev == old) break;
+          old = prev;
+        }
+        return h;
+      }
+      h = (h + 1) & (S - 1);
+    }
+  }
+  uint32_t* tab = t.w;
   for (;;) {
     uint32_t e = tab[h];
     if (e == 0) {
@@ -319,8 +366,8 @@ __device__ __forceinline__ uint32_t tab_insert_h(uint32_t* tab, uint32_t S, uint
   }
 }
 template <class KeyF>
-__device__ __forceinline__ uint32_t tab_insert(uint32_t* tab, uint32_t S, uint32_t r, uint64_t k, KeyF key) {
-  return tab_insert_h(tab, S, r, mix64(k), [&](uint32_t o) { return key(o) == k; });
+__device__ __forceinline__ uint32_t tab_insert(const Tab& t, uint32_t S, uint32_t r, uint64_t k, KeyF key) {
+  return tab_insert_h(t, S, r, mix64(k), [&](uint32_t o) { return key(o) == k; });
 }
 
 // ---------------------------------------------------------------------------
@@ -364,8 +411,8 @@ __device__ void gen_stats(Ctx& c, Sh& sh, const Av& a) {
   const uint64_t s_first = bmin(sh, firstv ? firstv : 0xFFFFFFFFu);
   // distinct values over every slot (nulls included)
   const uint32_t S = tab_slots(n);
-  uint32_t* tab = c.work;
-  for (uint32_t i = tid; i < S; i += NT) tab[i] = 0;
+  const Tab tab{c.work, c.wide};
+  tab.clear(S);
   __syncthreads();
   auto key = [&](uint32_t r) { return key_of<W, FLT, SGN>(ld<W>(a.p, r)); };
   for (uint32_t r = tid; r < n; r += NT) tab_insert(tab, S, r, key(r), key);
@@ -373,10 +420,10 @@ __device__ void gen_stats(Ctx& c, Sh& sh, const Av& a) {
   uint32_t uniq = 0;
   uint64_t best = 0;
   for (uint32_t i = tid; i < S; i += NT) {
-    const uint32_t e = tab[i];
-    if (e) {
+    const uint32_t r1 = tab.row1(i);
+    if (r1) {
       uniq++;
-      best = max(best, ((uint64_t)(e >> 16) << 32) | (0xFFFFFFFFu - ((e & 0xFFFFu) - 1)));
+      best = max(best, ((uint64_t)tab.hi(i) << 32) | (0xFFFFFFFFu - (r1 - 1)));
     }
   }
   const uint64_t s_uniq = bsum(sh, uniq);
@@ -749,8 +796,8 @@ __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
   auto dv = [&](uint32_t r) -> uint64_t { return (r == 0 && !v0) ? 0ull : ld<W>(a.p, r); };
   auto ins = [&](uint32_t r) { return r == 0 || valid_at(a, r); };
   const uint32_t S = tab_slots(n);
-  uint32_t* tab = c.work;
-  for (uint32_t i = tid; i < S; i += NT) tab[i] = 0;
+  const Tab tab{c.work, c.wide};
+  tab.clear(S);
   __syncthreads();
   for (uint32_t r = tid; r < n; r += NT)
     if (ins(r)) idx[r] = tab_insert(tab, S, r, dv(r), dv);  // the slot, for now
@@ -763,7 +810,7 @@ __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
     uint32_t slot = 0;
     if (r < n && ins(r)) {
       slot = idx[r];
-      f = (tab[slot] & 0xFFFFu) == r + 1;
+      f = tab.row1(slot) == r + 1;
     }
     uint32_t tot;
     const uint32_t ex = bscan(sh, f ? 1u : 0u, &tot);
@@ -775,11 +822,11 @@ __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
   for (uint32_t j = tid; j < k; j += NT) {
     const uint32_t r = row_of[j];
     const uint32_t slot = idx[r];
-    tab[slot] = (j << 16) | (r + 1);
+    tab.set(slot, j, r + 1);
   }
   __syncthreads();
   for (uint32_t r = tid; r < n; r += NT)
-    if (ins(r)) idx[r] = tab[idx[r]] >> 16;
+    if (ins(r)) idx[r] = tab.hi(idx[r]);
   __syncthreads();
   // null rows take the id of the last inserted row before them
   uint32_t carry_last = 0;
@@ -804,6 +851,75 @@ __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
   return p2 + 4 + k * W;
 }
 
+// roaring 0.10.1 serialize_into (sb_encode.cpp roaring_serialize) of e
+// ascending rows (rows[j] < n) for pages over 65536 rows: cookie 12346, the
+// containers' (key, card - 1), their offsets, then array (<= 4096) or bitmap
+// containers (bitmaps from bm, the rows' n-bit bitmap).  tmp: 4 ceil(n /
+// 65536) words of scratch.  All NT threads.  Returns the bytes written at
+// c.out + rpos (0 when out of room).
+__device__ uint32_t roaring_multi(Ctx& c, Sh& sh, const uint32_t* bm, const uint32_t* rows, uint32_t e, uint32_t n,
+                                  uint32_t rpos, uint32_t* tmp) {
+  const uint32_t tid = threadIdx.x, nk = (n + 65535) >> 16;
+  uint32_t* first = tmp;
+  uint32_t* card = tmp + nk;
+  uint32_t* doff = tmp + 2 * nk;  // data offset of each present container; tmp[3 nk + k]: its index
+  auto lower = [&](uint32_t x) {  // first j with rows[j] >= x
+    uint32_t lo = 0, hi = e;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (rows[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  for (uint32_t k = tid; k < nk; k += NT) {
+    const uint32_t a = lower(k << 16), b = k + 1 < nk ? lower((k + 1) << 16) : e;
+    first[k] = a;
+    card[k] = b - a;
+  }
+  __syncthreads();
+  uint32_t nc = 0, dsz = 0;  // present containers and data bytes before the tile
+  for (uint32_t k0 = 0; k0 < nk; k0 += NT) {
+    const uint32_t k = k0 + tid;
+    const uint32_t cd = k < nk ? card[k] : 0u;
+    const uint32_t sz = cd == 0 ? 0u : cd <= 4096 ? 2 * cd : 8192u;
+    uint32_t tc, ts;
+    const uint32_t ic = bscan(sh, cd ? 1u : 0u, &tc), is = bscan(sh, sz, &ts);
+    if (k < nk) doff[k] = cd ? dsz + is : 0u;
+    if (k < nk && cd) tmp[3 * nk + k] = nc + ic;  // compact index
+    nc += tc;
+    dsz += ts;
+  }
+  __syncthreads();
+  const uint32_t hdr = 8 + 8 * nc, total = hdr + dsz;
+  if (!room(c, sh, (uint64_t)rpos + total)) return 0;
+  if (tid == 0) {
+    put8(c.out + rpos, 12346, 4);  // SERIAL_COOKIE_NO_RUNCONTAINER
+    put8(c.out + rpos + 4, nc, 4);
+  }
+  for (uint32_t k = tid; k < nk; k += NT) {
+    const uint32_t cd = card[k];
+    if (!cd) continue;
+    const uint32_t i = tmp[3 * nk + k];
+    put8(c.out + rpos + 8 + 4 * i, k, 2);
+    put8(c.out + rpos + 10 + 4 * i, cd - 1, 2);
+    put8(c.out + rpos + 8 + 4 * nc + 4 * i, hdr + doff[k], 4);
+  }
+  for (uint32_t j = tid; j < e; j += NT) {  // array containers
+    const uint32_t r = rows[j], k = r >> 16;
+    if (card[k] <= 4096) put8(c.out + rpos + hdr + doff[k] + 2 * (j - first[k]), r & 0xFFFF, 2);
+  }
+  for (uint32_t k = 0; k < nk; k++) {  // bitmap containers (uniform)
+    if (card[k] <= 4096) continue;
+    for (uint32_t w = tid; w < 2048; w += NT) {
+      const uint32_t g = k * 2048 + w;  // the container's words; none past the page's last row
+      put8(c.out + rpos + hdr + doff[k] + 4 * w, g < (n + 31) / 32 ? bm[g] : 0u, 4);
+    }
+  }
+  __syncthreads();
+  return total;
+}
+
 // Freq (freq.rs:34-86): top value (the most frequent, first occurrence on
 // ties; T::default() when >= 90 % nulls), roaring bitmap of the valid rows
 // that differ from it, their values as a cascaded stream (Freq forbidden).
@@ -814,8 +930,11 @@ __device__ uint32_t freq_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
   const uint64_t top = top_null ? 0ull : ld<W>(a.p, sh.top_row);
   const uint64_t tk = key_of<W, FLT, SGN>(top);
   uint8_t* exc = c.scratch + (uint64_t)D * c.nmax * 8;
-  uint32_t* bm = c.work;  // bitmap container (1024 x u64) when card > 4096
-  for (uint32_t i = tid; i < 2048; i += NT) bm[i] = 0;
+  uint32_t* bm = c.work;  // the exceptions' row bitmap (bitmap containers)
+  const bool multi = n > 65536;  // (a wide page: several roaring containers)
+  uint32_t* rows = (uint32_t*)(c.scratch + (uint64_t)2 * c.nmax * 8);
+  const uint32_t bmw = multi ? (n + 31) / 32 : 2048;
+  for (uint32_t i = tid; i < bmw; i += NT) bm[i] = 0;
   __syncthreads();
   // exceptions in row order; positions written as an array container after the header
   const uint32_t rpos = pos + W + 4;  // roaring start
@@ -838,12 +957,24 @@ __device__ uint32_t freq_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
       else if constexpr (W == 2) ((uint16_t*)exc)[j] = (uint16_t)v;
       else exc[j] = (uint8_t)v;
       atomicOr(&bm[r >> 5], 1u << (r & 31));
-      if ((uint64_t)data + 2ull * (j + 1) <= c.cap) put8(c.out + data + 2 * j, r & 0xFFFF, 2);
+      if (multi) rows[j] = r;
+      else if ((uint64_t)data + 2ull * (j + 1) <= c.cap) put8(c.out + data + 2 * j, r & 0xFFFF, 2);
     }
     carry += tot;
   }
   const uint32_t e = carry;
   __syncthreads();
+  if (multi) {
+    const uint32_t bytes = roaring_multi(c, sh, bm, rows, e, n, rpos, rows + c.nmax);
+    if (!bytes) return pos;
+    if (tid == 0) {
+      put8(c.out + pos, top, W);
+      put8(c.out + pos + W, bytes, 4);
+    }
+    __syncthreads();
+    const Av ea{exc, nullptr, 0, e};
+    return enc_stream<W, FLT, SGN, D + 1>(c, sh, ea, fm | (1u << C_FREQ), rpos + bytes);
+  }
   const uint32_t bytes = e == 0 ? 8u : (e <= 4096 ? 16 + 2 * e : 16 + 8192u);
   if (!room(c, sh, (uint64_t)rpos + bytes)) return pos;
   if (tid == 0) {
@@ -1001,6 +1132,7 @@ __device__ uint32_t write_prefix(Ctx& c, const AdArgs& A, uint64_t r0, uint32_t 
 // the LDS then holding the LZ4 tables and the sample.
 __device__ __forceinline__ void set_work(Ctx& c, const AdArgs& A, uint32_t* lds) {
   c.lz4 = (uint8_t*)lds;
+  c.wide = A.P > 65535;  // (only with an HBM work area)
   if (A.gwork) {
     c.work = (uint32_t*)(A.gwork + (uint64_t)blockIdx.x * A.gwork_bytes);
     c.samp = (uint8_t*)lds + sbc::kLz4WaveLds;
@@ -1012,6 +1144,7 @@ __device__ __forceinline__ void set_work(Ctx& c, const AdArgs& A, uint32_t* lds)
 
 __device__ void ctx_init(Ctx& c, Sh& sh, const AdArgs& A, uint32_t p) {
   c.work = nullptr;
+  c.wide = false;
   c.work_bytes = A.work_bytes;
   c.scratch = A.scratch + (uint64_t)blockIdx.x * A.scratch_bytes;
   c.nmax = A.P;
@@ -1244,11 +1377,11 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
   uint32_t NU = 0, U = 0, maxc = 0, top_row = 0;
   uint64_t TU = 0;
   const uint32_t Sl = tab_slots(n);
-  uint32_t* tab = c.work;
+  const Tab tab{c.work, c.wide};
   if (needs_stats(A.o, A.o.forbidden)) {
     for (uint32_t r = tid; r < n; r += NT) hsh[r] = str_hash(sptr(r), slen(r));
     __syncthreads();
-    for (uint32_t i = tid; i < Sl; i += NT) tab[i] = 0;
+    tab.clear(Sl);
     __syncthreads();
     uint32_t nulls = 0;
     for (uint32_t r = tid; r < n; r += NT) {
@@ -1259,11 +1392,11 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
     uint32_t uniq = 0;
     uint64_t best = 0, tu = 0;
     for (uint32_t i = tid; i < Sl; i += NT) {
-      const uint32_t e = tab[i];
-      if (e) {
+      const uint32_t r1 = tab.row1(i);
+      if (r1) {
         uniq++;
-        tu += slen((e & 0xFFFFu) - 1) + 8;
-        best = max(best, ((uint64_t)(e >> 16) << 32) | (0xFFFFFFFFu - ((e & 0xFFFFu) - 1)));
+        tu += slen(r1 - 1) + 8;
+        best = max(best, ((uint64_t)tab.hi(i) << 32) | (0xFFFFFFFFu - (r1 - 1)));
       }
     }
     NU = (uint32_t)bsum(sh, nulls), U = (uint32_t)bsum(sh, uniq);
@@ -1347,7 +1480,7 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
     }
   } else if (codec == C_DICT) {
     auto ins = [&](uint32_t r) { return r == 0 || valid_at(va, r); };
-    for (uint32_t i = tid; i < Sl; i += NT) tab[i] = 0;
+    tab.clear(Sl);
     __syncthreads();
     for (uint32_t r = tid; r < n; r += NT)
       if (ins(r)) idx[r] = tab_insert_h(tab, Sl, r, hsh[r], [&](uint32_t o) { return same(o, r); });
@@ -1355,7 +1488,7 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
     uint32_t carry = 0;
     for (uint32_t t0 = 0; t0 < n; t0 += NT) {
       const uint32_t r = t0 + tid;
-      const bool f = r < n && ins(r) && (tab[idx[r]] & 0xFFFFu) == r + 1;
+      const bool f = r < n && ins(r) && tab.row1(idx[r]) == r + 1;
       uint32_t tot;
       const uint32_t ex = bscan(sh, f ? 1u : 0u, &tot);
       if (f) row_of[carry + ex] = r;
@@ -1363,10 +1496,10 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
     }
     const uint32_t k = carry;
     __syncthreads();
-    for (uint32_t j = tid; j < k; j += NT) tab[idx[row_of[j]]] = (j << 16) | (row_of[j] + 1);
+    for (uint32_t j = tid; j < k; j += NT) tab.set(idx[row_of[j]], j, row_of[j] + 1);
     __syncthreads();
     for (uint32_t r = tid; r < n; r += NT)
-      if (ins(r)) idx[r] = tab[idx[r]] >> 16;
+      if (ins(r)) idx[r] = tab.hi(idx[r]);
     __syncthreads();
     uint32_t carry_last = 0;
     for (uint32_t t0 = 0; t0 < n; t0 += NT) {
@@ -1391,8 +1524,9 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
     const bool top_null = (double)NU / (double)n >= 0.9;
     const uint32_t tl = top_null ? 0u : slen(top_row);
     uint32_t* bm = c.work;
+    const bool multi = n > 65536;  // (a wide page: several roaring containers)
     __syncthreads();
-    for (uint32_t i = tid; i < 2048; i += NT) bm[i] = 0;
+    for (uint32_t i = tid; i < (multi ? (n + 31) / 32 : 2048u); i += NT) bm[i] = 0;
     __syncthreads();
     const uint32_t rpos = body + 8 + tl + 4;
     const uint32_t data = rpos + 16;
@@ -1406,27 +1540,30 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
         const uint32_t j = carry + ex;
         row_of[j] = r;
         atomicOr(&bm[r >> 5], 1u << (r & 31));
-        if ((uint64_t)data + 2ull * (j + 1) <= c.cap) put8(c.out + data + 2 * j, r & 0xFFFF, 2);
+        if (!multi && (uint64_t)data + 2ull * (j + 1) <= c.cap) put8(c.out + data + 2 * j, r & 0xFFFF, 2);
       }
       carry += tot;
     }
     const uint32_t e = carry;
     __syncthreads();
-    const uint32_t bytes = e == 0 ? 8u : (e <= 4096 ? 16 + 2 * e : 16 + 8192u);
-    if (room(c, sh, (uint64_t)rpos + bytes)) {
+    uint32_t bytes = e == 0 ? 8u : (e <= 4096 ? 16 + 2 * e : 16 + 8192u);
+    if (multi) bytes = roaring_multi(c, sh, bm, row_of, e, n, rpos, (uint32_t*)(c.scratch + (uint64_t)4 * A.P * 8 + 64));
+    if ((!multi || bytes) && room(c, sh, (uint64_t)rpos + bytes)) {
       if (tid == 0) {
         put8(c.out + body, tl, 8);
         put8(c.out + body + 8 + tl, bytes, 4);
-        put8(c.out + rpos, 12346, 4);
-        put8(c.out + rpos + 4, e ? 1u : 0u, 4);
-        if (e) {
-          put8(c.out + rpos + 8, 0, 2);
-          put8(c.out + rpos + 10, e - 1, 2);
-          put8(c.out + rpos + 12, 16, 4);
+        if (!multi) {
+          put8(c.out + rpos, 12346, 4);
+          put8(c.out + rpos + 4, e ? 1u : 0u, 4);
+          if (e) {
+            put8(c.out + rpos + 8, 0, 2);
+            put8(c.out + rpos + 10, e - 1, 2);
+            put8(c.out + rpos + 12, 16, 4);
+          }
         }
       }
       for (uint32_t i = tid; i < tl; i += NT) c.out[body + 8 + i] = sptr(top_row)[i];
-      if (e > 4096)
+      if (!multi && e > 4096)
         for (uint32_t i = tid; i < 2048; i += NT) put8(c.out + data + 4 * i, bm[i], 4);
       __syncthreads();
       const Strs SS2{A.values, A.offsets + r0, hsh};
@@ -1516,7 +1653,8 @@ static uint64_t stream_bound(uint64_t n, uint64_t w, int depth) {
   const uint64_t leaf = 9 + std::max({n * (4 + w), n * w + n * w / 255 + 32, (n / 128) * 513, w + n * (2 + w)});
   if (depth == 0) return leaf;
   const uint64_t dict = 9 + stream_bound(n, 4, depth - 1) + 4 + n * w;
-  const uint64_t freq = 9 + w + 4 + 16 + std::max<uint64_t>(2 * n, 8192) + stream_bound(n, w, depth - 1);
+  const uint64_t freq = 9 + w + 4 + 16 + 8 * ((n + 65535) / 65536) + std::max<uint64_t>(2 * n, 8192) +
+                        stream_bound(n, w, depth - 1);
   return std::max({leaf, dict, freq});
 }
 
@@ -1542,7 +1680,8 @@ uint32_t adaptive_work_bytes(uint64_t P, const sba::Opts& o) {
 uint64_t big_work_bytes(uint64_t P, bool stats) {
   uint64_t s = 64;
   while (s < 2 * P) s <<= 1;
-  return stats ? std::max<uint64_t>(4 * s, sbc::kSnappyTableBytes) : sbc::kSnappyTableBytes;
+  const uint64_t word = P > 65535 ? 8 : 4;  // (wide table words)
+  return stats ? std::max<uint64_t>(word * s, sbc::kSnappyTableBytes) : sbc::kSnappyTableBytes;
 }
 
 // Pages of a batch: at most 2048, and at most ~2 GiB of slots + scratch + work.
@@ -1578,14 +1717,14 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
     default: return SB_E_NYI;
   }
   const bool is_bool = phys == SB_T_BOOLEAN;
-  // Pages over kMaxRows rows keep their work area in HBM: any size for a
-  // Basic(default) page, up to kMaxBigRows when the statistics are needed;
+  // Pages over kMaxRows rows keep their work area in HBM (any size; over
+  // kMaxNarrowRows with 64-bit table words and several roaring containers);
   // Boolean pages stage their bits in LDS (kMaxRows)
   const bool stats = sba::needs_stats(o, o.forbidden);
   const bool big = P > sba::kMaxRows;
-  if (big && (is_bool || (stats && P > sba::kMaxBigRows) || P * w > 0xFFFFFFF0ull)) return SB_E_NYI;
+  if (big && (is_bool || P * w > 0xFFFFFFF0ull || P > 0x7FFFFFFFull)) return SB_E_NYI;
   const uint64_t slot = adaptive_slot_bytes(P, w, nullable);
-  const uint64_t scr = (2 * P * 8 + 255) & ~255ull;
+  const uint64_t scr = ((P > 65535 ? 3 : 2) * P * 8 + 255) & ~255ull;  // (wide pages: roaring rows, level 2)
   const uint64_t gwb = big ? big_work_bytes(P, stats) : 0;
   const uint32_t batch = batch_pages(np, slot + scr + gwb);
   sba::Opts wo = o;
@@ -1672,7 +1811,7 @@ int encode_binary_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, uint6
   const sba::Opts o{opts->default_codec, opts->has_ratio, opts->ratio, opts->forbidden_mask, opts->forced_codec};
   const bool stats = sba::needs_stats(o, o.forbidden);
   const bool big = P > sba::kMaxRows;  // (work area in HBM, as encode_adaptive's)
-  if (big && stats && P > sba::kMaxBigRows) return SB_E_NYI;
+  if (big && P > 0x7FFFFFFFull) return SB_E_NYI;
   const uint64_t scr = (32 * P + 64 + 255) & ~255ull;
   const uint64_t gwb = big ? big_work_bytes(P, stats) : 0;
   const uint64_t maxpp = batch_pages(np, scr + gwb);

@@ -98,14 +98,12 @@ def test_config1_int64_none(ctx):
 
 def test_unsupported_options_are_nyi(ctx):
     """Zstd as the default codec (libzstd's compressor is not restated on the
-    device), pages with statistics over 65535 rows (the 16-bit rows of the
-    table words) and Boolean pages over 16384 rows report NotYetImplemented."""
+    device) and Boolean pages over 16384 rows report NotYetImplemented."""
     import pa_amd
 
     tv = torch.arange(70000, dtype=torch.int32, device="cuda")
     for opts in (pa_amd.WriteOptions(default_compression=2), pa_amd.WriteOptions(default_compression=2,
-                                                                                  default_compress_ratio=1.2),
-                 pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=65536)):
+                                                                                  default_compress_ratio=1.2)):
         with pytest.raises(pa_amd.StrawboatError) as e:
             pa_amd.encode_column_device(tv, None, False, opts, ctx=ctx)
         assert e.value.status == 2
@@ -115,12 +113,13 @@ def test_unsupported_options_are_nyi(ctx):
     assert e.value.status == 2
 
 
-@pytest.mark.parametrize("P", [20000, 40000, 65535])
+@pytest.mark.parametrize("P", [20000, 65535, 65537, 300_000])
 @pytest.mark.parametrize("kind", ["int32_mix", "f64_mix", "int64_freq", "int32_dict"])
 @pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
 def test_big_adaptive_pages(ctx, P, kind, nullable):
     """Pages over 16384 rows with the adaptive cascade (their statistics'
-    tables in HBM): byte-identical to the host writer, decoded back."""
+    tables in HBM; over 65535 rows 64-bit table words and roaring bitmaps of
+    several containers): byte-identical to the host writer, decoded back."""
     import pa_amd
 
     rng = np.random.default_rng(P + len(kind))
@@ -165,12 +164,12 @@ def test_big_basic_pages(ctx, codec, P):
 
 @pytest.mark.parametrize("opt", ["lz4", "dict", "freq", "adaptive"])
 def test_big_binary_pages(ctx, opt):
-    """Utf8 pages over 16384 rows: Basic LZ4 of any size, Dict / Freq /
-    adaptive up to 65535 rows, byte-identical to the host writer."""
+    """Utf8 pages over 16384 rows: Basic LZ4, Dict, Freq (several roaring
+    containers) and adaptive pages, byte-identical to the host writer."""
     import pa_amd
 
     rng = np.random.default_rng(5)
-    P = 300_000 if opt == "lz4" else 50_000
+    P = 300_000 if opt in ("lz4", "freq", "adaptive") else 50_000
     n = 2 * P + 11
     pool = [f"v{i}".encode() for i in range(700)]
     strs = [pool[i] if r < 0.95 else str(x).encode()
