@@ -4254,12 +4254,32 @@ __device__ __forceinline__ void wave_put_bits(const uint32_t* bm, uint32_t n, ui
 constexpr uint32_t kLvStage = 4160;      // page bytes staged per wave (header + level streams)
 constexpr uint32_t kLvStep = 64 * kLvK;  // levels per wave step (2048)
 
+#ifndef SB_LV_ACC_BITS
+#define SB_LV_ACC_BITS 8192
+#endif
+#ifdef SB_LV_STEPBITS
+constexpr uint32_t kLvBitsW = kLvStep / 32 + 4;  // a step's bits, written out every step
+#else
+// The page's validity bits accumulate over its steps and go out once per
+// kLvAccBits (a C4 page: once), as whole words with two edge merges,
+// instead of a short partial-line write and two atomics every step.
+constexpr uint32_t kLvAccBits = SB_LV_ACC_BITS;
+constexpr uint32_t kLvBitsW = kLvAccBits / 32 + 2;
+#endif
+
 struct ListWave {
   ListShared ls;
   uint32_t err;
   alignas(16) uint16_t obuf[kLvStep + 8];  // step-relative leaf offset of each row start, at row + (g0 & 3)
-  uint32_t lbits[kLvStep / 32 + 4];   // [0] = 0, then the list-validity bits of the step's rows
-  uint32_t fbits[kLvStep / 32 + 4];   // [0] = 0, then the leaf-validity bits of the step's leaves
+  uint32_t lbits[kLvBitsW];   // [0] = 0, then the list-validity bits held (rows)
+  uint32_t fbits[kLvBitsW];   // [0] = 0, then the leaf-validity bits held (leaves)
+};
+
+// Validity bits held in ListWave.lbits / fbits: r / l bits from global bit
+// positions g0 / v0 (uniform over the wave).
+struct LvAcc {
+  uint32_t r, l;
+  uint64_t g0, v0;
 };
 
 // Page bytes: the staged prefix from LDS, the rest from HBM.
@@ -4293,6 +4313,24 @@ __device__ __forceinline__ uint32_t compress32(uint32_t x, uint32_t m) {
   return x;
 }
 
+// The held validity bits to the bitmaps; the buffers zeroed again.
+__device__ __forceinline__ void lv_flush(ListWave& w, const ListArgs& a, LvAcc& acc) {
+#ifndef SB_LV_STEPBITS
+  const uint32_t lane = threadIdx.x & 63;
+#ifndef SB_V_LV_NOBITS
+  if (a.nl) wave_put_bits(w.lbits + 1, acc.r, acc.g0, a.out_list_validity);
+  if (a.ni) wave_put_bits(w.fbits + 1, acc.l, acc.v0, a.out_leaf_validity);
+#endif
+  wave_sync();
+  const uint32_t nw = (max(acc.r, acc.l) + 31) / 32 + 2;
+  for (uint32_t i = lane; i < nw; i += 64) w.lbits[i] = w.fbits[i] = 0;
+  wave_sync();
+  acc.g0 += acc.r;
+  acc.v0 += acc.l;
+  acc.r = acc.l = 0;
+#endif
+}
+
 // One step of kLvStep levels [t0, t0 + kLvStep) of a page, one wave, rows
 // and leaves before it = (carry_r, carry_l).  *step_r / *step_l: the step's
 // row starts and leaves (all levels); the return value: leaves consumed
@@ -4301,7 +4339,8 @@ __device__ __forceinline__ uint32_t compress32(uint32_t x, uint32_t m) {
 // (m: this lane's masks of levels t0 + 32 lane ..; rows: the page's rows.)
 template <bool WRITE, class WV>
 __device__ uint32_t lv_step_m(const LvMasks m, WV& w, uint32_t rows, const ListArgs& a, uint32_t t0, uint64_t rbase,
-                              uint64_t lbase, uint32_t carry_r, uint32_t carry_l, uint32_t* step_r, uint32_t* step_l) {
+                              uint64_t lbase, uint32_t carry_r, uint32_t carry_l, uint32_t* step_r, uint32_t* step_l,
+                              LvAcc& acc) {
   const uint32_t lane = threadIdx.x & 63;
   if (t0 == 0 && lane == 0 && !(m.rsm & 1)) put_err(&w.err, ST_OUT_OF_SPEC);  // level 0 starts no row
   const uint32_t pk = ((uint32_t)__popc(m.rsm) << 16) | (uint32_t)__popc(m.lfm);
@@ -4321,8 +4360,14 @@ __device__ uint32_t lv_step_m(const LvMasks m, WV& w, uint32_t rows, const ListA
     const uint32_t s_r0 = carry_r, s_l0 = carry_l;
     const uint64_t g0 = rbase + s_r0, v0 = lbase + s_l0;
     const uint32_t al = a.ow == 4 ? (uint32_t)(g0 & 3) : (uint32_t)(g0 & 1);  // obuf index of row 0
-    for (uint32_t i = lane; i < kLvStep / 32 + 4; i += 64) w.lbits[i] = w.fbits[i] = 0;
+#ifdef SB_LV_STEPBITS
+    for (uint32_t i = lane; i < kLvBitsW; i += 64) w.lbits[i] = w.fbits[i] = 0;
     wave_sync();
+    const uint32_t pr = rb - s_r0, pf = lb - s_l0;
+#else
+    if (acc.r + (tot >> 16) > kLvAccBits || acc.l + (tot & 0xFFFFu) > kLvAccBits) lv_flush(w, a, acc);
+    const uint32_t pr = acc.r + rb - s_r0, pf = acc.l + lb - s_l0;
+#endif
     const uint32_t nr = __popc(rsm), nf = __popc(lfm);
     uint16_t* ob = w.obuf + al + (rb - s_r0);
     const uint32_t lrel = lb - s_l0;
@@ -4330,8 +4375,8 @@ __device__ uint32_t lv_step_m(const LvMasks m, WV& w, uint32_t rows, const ListA
 #ifndef SB_V_LV_NOOB
     for (uint32_t x = rsm; x; x &= x - 1, j++) ob[j] = (uint16_t)(lrel + __popc(m.lfm & ((x & (0u - x)) - 1)));
 #endif
-    if (a.nl) lds_or_bits(w.lbits + 1, rb - s_r0, compress32(m.lvm, rsm), nr);
-    if (a.ni) lds_or_bits(w.fbits + 1, lrel, compress32(m.fvm, lfm), nf);
+    if (a.nl) lds_or_bits(w.lbits + 1, pr, compress32(m.lvm, rsm), nr);
+    if (a.ni) lds_or_bits(w.fbits + 1, pf, compress32(m.fvm, lfm), nf);
     const uint32_t cpk = (nr << 16) | nf;
     const uint32_t ctot = __builtin_amdgcn_readlane(wave_incl_scan(cpk), 63);
     const uint32_t tr = ctot >> 16, tl = ctot & 0xFFFFu;
@@ -4373,23 +4418,26 @@ __device__ uint32_t lv_step_m(const LvMasks m, WV& w, uint32_t rows, const ListA
         }
       }
     }
-#ifndef SB_V_LV_NOBITS
+#ifdef SB_LV_STEPBITS
     if (a.nl) wave_put_bits(w.lbits + 1, tr, g0, a.out_list_validity);
     if (a.ni) wave_put_bits(w.fbits + 1, tl, v0, a.out_leaf_validity);
+#else
+    acc.r += tr;
+    acc.l += tl;
 #endif
     wave_sync();
   }
   *step_r = tot >> 16;
   *step_l = tot & 0xFFFFu;
-  return (uint32_t)wave_sum64(__popc(lfm));
+  return __builtin_amdgcn_readlane(wave_incl_scan(__popc(lfm)), 63);  // DPP, not a permute chain
 }
 
 template <bool WRITE, class Src>
 __device__ __forceinline__ uint32_t lv_step(const Src& s, ListWave& w, const ListShared& ls, const ListArgs& a,
                                             uint32_t t0, uint32_t L, uint64_t rbase, uint64_t lbase, uint32_t carry_r,
-                                            uint32_t carry_l, uint32_t* step_r, uint32_t* step_l) {
+                                            uint32_t carry_l, uint32_t* step_r, uint32_t* step_l, LvAcc& acc) {
   const LvMasks m = level_masks(s, ls, t0 + (threadIdx.x & 63) * kLvK, L, a.nl + 1);
-  return lv_step_m<WRITE>(m, w, ls.rows, a, t0, rbase, lbase, carry_r, carry_l, step_r, step_l);
+  return lv_step_m<WRITE>(m, w, ls.rows, a, t0, rbase, lbase, carry_r, carry_l, step_r, step_l, acc);
 }
 
 // One wave walks its page's levels a step at a time (the sizing pass).
@@ -4398,13 +4446,23 @@ __device__ void wave_levels(const Src& s, ListWave& w, const ListArgs& a, uint32
                             uint32_t* rows_c, uint32_t* leaves_c) {
   const uint32_t lane = threadIdx.x & 63, rows = w.ls.rows;
   uint32_t carry_r = 0, carry_l = 0, leaves = 0;
+  LvAcc acc{0, 0, rbase, lbase};
+#ifndef SB_LV_STEPBITS
+  if constexpr (WRITE) {
+    for (uint32_t i = lane; i < kLvBitsW; i += 64) w.lbits[i] = w.fbits[i] = 0;
+    wave_sync();
+  }
+#endif
   for (uint32_t t0 = 0; t0 < L; t0 += kLvStep) {
     uint32_t sr, sl;
-    leaves += lv_step<WRITE>(s, w, w.ls, a, t0, L, rbase, lbase, carry_r, carry_l, &sr, &sl);
+    leaves += lv_step<WRITE>(s, w, w.ls, a, t0, L, rbase, lbase, carry_r, carry_l, &sr, &sl, acc);
     carry_r += sr;
     carry_l += sl;
     if (carry_r > rows) break;  // uniform: every later level is past the last row
   }
+#ifndef SB_LV_STEPBITS
+  if constexpr (WRITE) lv_flush(w, a, acc);
+#endif
   const uint32_t rc = min(carry_r, rows);
   if (lane == 0 && rc != rows) put_err(&w.err, ST_OUT_OF_SPEC);  // levels ended before `rows` rows
   *rows_c = rc;
@@ -4416,7 +4474,7 @@ template <class Src>
 __device__ __forceinline__ uint32_t lv_count(const Src& s, const ListShared& ls, uint32_t t0, uint32_t L, uint32_t cs1) {
   const LvMasks m = level_masks(s, ls, t0 + (threadIdx.x & 63) * kLvK, L, cs1);
   const uint32_t pk = ((uint32_t)__popc(m.rsm) << 16) | (uint32_t)__popc(m.lfm);
-  return (uint32_t)wave_sum64(pk);  // rows < 2^16 per 2048-level step
+  return __builtin_amdgcn_readlane(wave_incl_scan(pk), 63);  // rows < 2^16 per 2048-level step
 }
 
 // Per page setup of one wave: the page's first kLvStage bytes staged in LDS
