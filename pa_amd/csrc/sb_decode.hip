@@ -4495,8 +4495,19 @@ __device__ bool wave_page_setup(ListWave& w, uint32_t* stage, const ListArgs& a,
     d0 = a.lvdesc[2 * page];
     d1 = a.lvdesc[2 * page + 1];
   }
-  if (stage)
-    for (uint32_t d = lane; d < ndw; d += 64) stage[d] = __builtin_nontemporal_load((const uint32_t*)a0 + d);
+  if (stage) {  // every load issued before the first LDS store (one round trip, not one per 64 dwords)
+    typedef const __attribute__((address_space(1))) uint32_t g32;
+    constexpr uint32_t kIt = (kLvStage / 4 + 2 + 63) / 64;
+    uint32_t v[kIt];
+#pragma unroll
+    for (uint32_t k = 0; k < kIt; k++) {
+      const uint32_t d = lane + 64 * k;
+      v[k] = d < ndw ? __builtin_nontemporal_load((g32*)a0 + d) : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kIt; k++)
+      if (lane + 64 * k < ndw) stage[lane + 64 * k] = v[k];
+  }
   if (lane == 0) w.err = 0;
   wave_sync();
   *mis_out = mis;
