@@ -43,8 +43,6 @@ namespace sba {
 #define SB_ENC_NT 256
 #endif
 constexpr int NT = SB_ENC_NT, NW = NT / 64;
-constexpr uint32_t kPre = 32;  // rows a thread holds (pages up to kPre * NT rows)
-constexpr uint32_t kLd = 16;   // rows a thread loads ahead at a time
 constexpr uint32_t kMaxRows = 16384;      // pages whose statistics' tables fit the LDS work area
 constexpr uint32_t kMaxNarrowRows = 65535;  // table words with 16-bit rows; larger pages use 64-bit words
 constexpr uint32_t SC = 10, SS = 64, kSample = SC * SS;
@@ -389,7 +387,8 @@ __device__ void gen_stats(Ctx& c, Sh& sh, const Av& a) {
   bool sorted = true;
   uint64_t kmin = ~0ull, kmax = 0, prevk = 0;
   bool have = false;
-  auto visit = [&](uint32_t r, uint64_t k) {
+  for (uint32_t r = r0; r < r1; r++) {
+    const uint64_t k = key_of<W, FLT, SGN>(ld<W>(a.p, r));
     kmin = min(kmin, k);
     kmax = max(kmax, k);
     if (valid_at(a, r)) {
@@ -401,19 +400,6 @@ __device__ void gen_stats(Ctx& c, Sh& sh, const Av& a) {
     } else {
       nulls++;
     }
-  };
-  if (ch <= kPre) {  // kLd loads issued before their first use
-#pragma unroll 1
-    for (uint32_t j0 = 0; j0 < ch; j0 += kLd) {
-      uint64_t kv[kLd];
-#pragma unroll
-      for (uint32_t j = 0; j < kLd; j++) kv[j] = r0 + j0 + j < r1 ? ld<W>(a.p, r0 + j0 + j) : 0ull;
-#pragma unroll
-      for (uint32_t j = 0; j < kLd; j++)
-        if (r0 + j0 + j < r1) visit(r0 + j0 + j, key_of<W, FLT, SGN>(kv[j]));
-    }
-  } else {
-    for (uint32_t r = r0; r < r1; r++) visit(r, key_of<W, FLT, SGN>(ld<W>(a.p, r)));
   }
   uint32_t tot;
   const uint32_t prev_row = bexcl_max(sh, lastv, &tot);  // last valid row (+1) before this chunk
@@ -432,24 +418,7 @@ __device__ void gen_stats(Ctx& c, Sh& sh, const Av& a) {
   tab.clear(S);
   __syncthreads();
   auto key = [&](uint32_t r) { return key_of<W, FLT, SGN>(ld<W>(a.p, r)); };
-  if (n <= kPre * NT) {  // keys loaded ahead, kLd at a time, then inserted
-#pragma unroll 1
-    for (uint32_t j0 = 0; j0 < kPre; j0 += kLd) {
-      uint64_t kv[kLd];
-#pragma unroll
-      for (uint32_t j = 0; j < kLd; j++) {
-        const uint32_t r = tid + (j0 + j) * NT;
-        kv[j] = r < n ? ld<W>(a.p, r) : 0ull;
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < kLd; j++) {
-        const uint32_t r = tid + (j0 + j) * NT;
-        if (r < n) tab_insert(tab, S, r, key_of<W, FLT, SGN>(kv[j]), key);
-      }
-    }
-  } else {
-    for (uint32_t r = tid; r < n; r += NT) tab_insert(tab, S, r, key(r), key);
-  }
+  for (uint32_t r = tid; r < n; r += NT) tab_insert(tab, S, r, key(r), key);
   __syncthreads();
   uint32_t uniq = 0;
   uint64_t best = 0;
@@ -833,110 +802,48 @@ __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
   const Tab tab{c.work, c.wide};
   tab.clear(S);
   __syncthreads();
-  const uint32_t ch = (n + NT - 1) / NT;
-  uint32_t k;
-  if (ch <= kPre) {
-    // Every thread owns the rows [r0, r1) (values and slots in registers):
-    // one block scan orders the first occurrences, one max-scan carries ids
-    // over null rows, instead of a block scan per NT rows for each.
-    const uint32_t r0 = min(n, tid * ch), r1 = min(n, r0 + ch);
-    uint32_t sl[kPre];
-    uint32_t insm = 0;  // rows of the chunk that are inserted
-#pragma unroll
-    for (uint32_t j0 = 0; j0 < kPre; j0 += kLd) {
-      uint64_t kv[kLd];
-#pragma unroll
-      for (uint32_t j = 0; j < kLd; j++) kv[j] = r0 + j0 + j < r1 ? dv(r0 + j0 + j) : 0ull;
-#pragma unroll
-      for (uint32_t j = 0; j < kLd; j++) {
-        const uint32_t r = r0 + j0 + j;
-        sl[j0 + j] = 0;
-        if (r < r1 && ins(r)) {
-          insm |= 1u << (j0 + j);
-          sl[j0 + j] = tab_insert(tab, S, r, kv[j], dv);
-        }
-      }
+  for (uint32_t r = tid; r < n; r += NT)
+    if (ins(r)) idx[r] = tab_insert(tab, S, r, dv(r), dv);  // the slot, for now
+  __syncthreads();
+  // ids: first rows in row order
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+    const uint32_t r = t0 + tid;
+    bool f = false;
+    uint32_t slot = 0;
+    if (r < n && ins(r)) {
+      slot = idx[r];
+      f = tab.row1(slot) == r + 1;
     }
-    __syncthreads();
-    uint32_t fom = 0;  // first occurrences
-#pragma unroll
-    for (uint32_t j = 0; j < kPre; j++)
-      if ((insm >> j) & 1) fom |= (uint32_t)(tab.row1(sl[j]) == r0 + j + 1) << j;
-    uint32_t id = bscan(sh, (uint32_t)__popc(fom), &k);  // (bscan ends with a barrier)
-#pragma unroll
-    for (uint32_t j = 0; j < kPre; j++)
-      if ((fom >> j) & 1) {
-        row_of[id] = r0 + j;
-        tab.set(sl[j], id++, r0 + j + 1);
-      }
-    __syncthreads();
-    uint32_t ids[kPre];
-#pragma unroll
-    for (uint32_t j = 0; j < kPre; j++) ids[j] = ((insm >> j) & 1) ? tab.hi(sl[j]) : 0u;
-    if (a.vb) {  // null rows take the id of the last inserted row before them
-      const uint32_t last = insm ? r0 + 32 - __clz(insm) : 0u;  // last inserted row + 1
-      uint32_t tmax;
-      const uint32_t prev = bexcl_max(sh, last, &tmax);
-#pragma unroll
-      for (uint32_t j = 0; j < kPre; j++)
-        if ((insm >> j) & 1) idx[r0 + j] = ids[j];
-      __syncthreads();
-      uint32_t cur = prev ? idx[prev - 1] : 0u;  // (row 0 is always inserted)
-#pragma unroll
-      for (uint32_t j = 0; j < kPre; j++) {
-        if ((insm >> j) & 1) cur = ids[j];
-        else if (r0 + j < r1) idx[r0 + j] = cur;
-      }
-    } else {
-#pragma unroll
-      for (uint32_t j = 0; j < kPre; j++)
-        if (r0 + j < r1) idx[r0 + j] = ids[j];
-    }
-    __syncthreads();
-  } else {
-    for (uint32_t r = tid; r < n; r += NT)
-      if (ins(r)) idx[r] = tab_insert(tab, S, r, dv(r), dv);  // the slot, for now
-    __syncthreads();
-    // ids: first rows in row order
-    uint32_t carry = 0;
-    for (uint32_t t0 = 0; t0 < n; t0 += NT) {
-      const uint32_t r = t0 + tid;
-      bool f = false;
-      uint32_t slot = 0;
-      if (r < n && ins(r)) {
-        slot = idx[r];
-        f = tab.row1(slot) == r + 1;
-      }
-      uint32_t tot;
-      const uint32_t ex = bscan(sh, f ? 1u : 0u, &tot);
-      if (f) row_of[carry + ex] = r;
-      carry += tot;
-    }
-    k = carry;
-    __syncthreads();
-    for (uint32_t j = tid; j < k; j += NT) {
-      const uint32_t r = row_of[j];
-      const uint32_t slot = idx[r];
-      tab.set(slot, j, r + 1);
-    }
-    __syncthreads();
-    for (uint32_t r = tid; r < n; r += NT)
-      if (ins(r)) idx[r] = tab.hi(idx[r]);
-    __syncthreads();
-    // null rows take the id of the last inserted row before them
-    uint32_t carry_last = 0;
-    for (uint32_t t0 = 0; t0 < n; t0 += NT) {
-      const uint32_t r = t0 + tid;
-      const bool in = r < n && ins(r);
-      uint32_t tmax;
-      const uint32_t incl = bscan_max(sh, in ? r + 1 : 0u, &tmax);
-      const uint32_t last = max(incl, carry_last);
-      if (r < n && !in) idx[r] = idx[last - 1];
-      carry_last = max(carry_last, tmax);
-      __syncthreads();
-    }
+    uint32_t tot;
+    const uint32_t ex = bscan(sh, f ? 1u : 0u, &tot);
+    if (f) row_of[carry + ex] = r;
+    carry += tot;
+  }
+  const uint32_t k = carry;
+  __syncthreads();
+  for (uint32_t j = tid; j < k; j += NT) {
+    const uint32_t r = row_of[j];
+    const uint32_t slot = idx[r];
+    tab.set(slot, j, r + 1);
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += NT)
+    if (ins(r)) idx[r] = tab.hi(idx[r]);
+  __syncthreads();
+  // null rows take the id of the last inserted row before them
+  uint32_t carry_last = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
+    const uint32_t r = t0 + tid;
+    const bool in = r < n && ins(r);
+    uint32_t tmax;
+    const uint32_t incl = bscan_max(sh, in ? r + 1 : 0u, &tmax);
+    const uint32_t last = max(incl, carry_last);
+    if (r < n && !in) idx[r] = idx[last - 1];
+    carry_last = max(carry_last, tmax);
     __syncthreads();
   }
+  __syncthreads();
   const Av ia{(const uint8_t*)idx, nullptr, 0, n};
   const uint32_t p2 = enc_stream<4, false, false, D + 1>(c, sh, ia, fm | (1u << C_DICT), pos);
   if (sh.err) return pos;
@@ -1091,7 +998,7 @@ __device__ uint32_t freq_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
   return enc_stream<W, FLT, SGN, D + 1>(c, sh, ea, fm | (1u << C_FREQ), rpos + bytes);
 }
 
-#ifdef SB_ENC_PHASES  // A/B instrumentation: per workgroup, s_memrealtime at each phase of the top stream
+#ifdef SB_ENC_PHASES  // A/B instrumentation: per workgroup, s_memrealtime at each phase of the top two streams
 __device__ uint64_t sb_enc_phase[4096 * 12];
 #define SB_EPHASE(k, v) do { if (D < 2 && threadIdx.x == 0 && blockIdx.x < 4096) sb_enc_phase[blockIdx.x * 12 + ((k) == 5 ? 8 + D : 4 * D + (k))] = (v); } while (0)
 #else
@@ -1359,7 +1266,7 @@ __global__ __launch_bounds__(NT) void k_enc_bool(AdArgs A) {
 }
 
 template <int W, bool FLT, bool SGN>
-__global__ __launch_bounds__(NT, 2) void k_enc_adaptive(AdArgs A) {
+__global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
   extern __shared__ uint32_t lds[];
   __shared__ Sh sh;
   const uint32_t tid = threadIdx.x;
@@ -1450,7 +1357,7 @@ __device__ uint32_t put_records(Ctx& c, Sh& sh, const Strs& S, uint32_t cnt, Row
 }
 
 template <int OW>
-__global__ __launch_bounds__(NT, 2) void k_enc_binary(AdArgs A) {
+__global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
   extern __shared__ uint32_t lds[];
   __shared__ Sh sh;
   const uint32_t tid = threadIdx.x;
