@@ -4251,7 +4251,13 @@ __device__ __forceinline__ void wave_put_bits(const uint32_t* bm, uint32_t n, ui
   }
 }
 
-constexpr uint32_t kLvStage = 4160;      // page bytes staged per wave (header + level streams)
+#ifndef SB_LV_STAGE
+#define SB_LV_STAGE 4160
+#endif
+#ifndef SB_LV_STAGE_PAD
+#define SB_LV_STAGE_PAD 16  // (>= 3 dwords: LdsSrc::u64 reads two words past the last staged one)
+#endif
+constexpr uint32_t kLvStage = SB_LV_STAGE;  // page bytes staged per wave (header + level streams)
 constexpr uint32_t kLvStep = 64 * kLvK;  // levels per wave step (2048)
 
 #ifndef SB_LV_ACC_BITS
@@ -4538,7 +4544,7 @@ __device__ bool wave_page_setup(ListWave& w, uint32_t* stage, const ListArgs& a,
 // consumed rows / leaves, and the parse results for the levels pass.
 __global__ __launch_bounds__(NT) void k_list_size(ListArgs a) {
   __shared__ ListWave waves[NW];
-  __shared__ uint32_t stages[NW][kLvStage / 4 + 16];  // the page's first bytes at byte `mis` (+ pad)
+  __shared__ uint32_t stages[NW][kLvStage / 4 + SB_LV_STAGE_PAD];  // the page's first bytes at byte `mis` (+ pad)
   const uint32_t lane = threadIdx.x & 63;
   ListWave& w = waves[threadIdx.x >> 6];
   uint32_t* stage = stages[threadIdx.x >> 6];
@@ -4661,7 +4667,7 @@ __global__ __launch_bounds__(NT) void k_list_vbase(ListArgs a) {
 // the last page also the totals and the final offset.
 __global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
   __shared__ ListWave waves[NW];
-  __shared__ uint32_t stages[NW][kLvStage / 4 + 16];  // the page's first bytes at byte `mis` (+ pad)
+  __shared__ uint32_t stages[NW][kLvStage / 4 + SB_LV_STAGE_PAD];  // the page's first bytes at byte `mis` (+ pad)
   const uint32_t lane = threadIdx.x & 63;
   ListWave& w = waves[threadIdx.x >> 6];
   uint32_t* stage = stages[threadIdx.x >> 6];
