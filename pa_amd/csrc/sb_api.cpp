@@ -345,6 +345,32 @@ static hipError_t plan_regions(sb_ctx* ctx, sb_plan* p, std::vector<sb::PageDesc
   return e;
 }
 
+// LDS a staged Boolean page takes in k_bool_decode: the page, its expanded
+// bitmap and the Zstd decoder's tables.
+static uint64_t bool_lds_need(uint64_t len, uint64_t n) {
+  return ((len + 15 + sb::kStagePad + 15) & ~15ull) + (((n + 7) / 8 + 15) & ~15ull) + sb::kStagePad +
+         sb::kZTablesBytes;
+}
+
+// Boolean pages too large for that (max_page_size = None: one page per
+// chunk) decode from HBM (k_bool_decode's big-page path) and expand RLE /
+// general-codec bitmaps into a region of their own: the page's bitmap words
+// plus 16 bytes of over-read slack.
+static hipError_t plan_bool_regions(sb_ctx* ctx, sb_plan* p, std::vector<sb::PageDesc>& pages) {
+  uint64_t off = 0;
+  for (sb::PageDesc& pd : pages) {
+    if (bool_lds_need(pd.byte_len, pd.num_values) <= sb::kDeferredLds) continue;
+    pd.reserved = off | sb::kRegionSpill;
+    off += sb::align16(4 * (((uint64_t)pd.num_values + 31) / 32)) + 16;
+  }
+  if (!off) return hipSuccess;
+  hipError_t e = hipMalloc(&p->d_region, off);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(p->d_pages, pages.data(), pages.size() * sizeof(sb::PageDesc), hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  return e;
+}
+
 static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8_t* d_chunk, uint64_t chunk_len,
                             std::vector<sb::PageDesc> pages, sb_plan** out, int regions) {
   const uint64_t n_pages = pages.size();
@@ -369,11 +395,9 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
       return fail(ctx, SB_E_ARG, "page %llu overruns the column chunk", (unsigned long long)i);
     // a 32-bit validity word shared by two pages is merged with atomics
     if ((pd.row_off & 31) || (m.num_values & 31)) needs_zero = true;
-    if (is_bool) {  // page + its expanded bitmap, as k_bool_decode lays them out in LDS
-      const uint64_t need = ((m.length + 15 + sb::kStagePad + 15) & ~15ull) + (((m.num_values + 7) / 8 + 15) & ~15ull) +
-                            sb::kStagePad + sb::kZTablesBytes;  // (+ the Zstd decoder's tables)
-      max_bool = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(max_bool, need), sb::kDeferredLds);
-    }
+    if (is_bool)  // page + its expanded bitmap, as k_bool_decode lays them out in LDS (big pages: all of it)
+      max_bool = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(max_bool, bool_lds_need(m.length, m.num_values)),
+                                              sb::kDeferredLds);
     if (m.length + 16 <= sb::kStageMaxBytes) {
       staged.push_back((uint32_t)i);
       max_stage = std::max<uint32_t>(max_stage, (uint32_t)m.length);
@@ -422,6 +446,13 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
   if (e != hipSuccess) {
     sb_plan_destroy(p);
     return fail(ctx, SB_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
+  }
+  if (is_bool && n_pages) {
+    e = plan_bool_regions(ctx, p, pages);
+    if (e != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "boolean plan regions: %s", hipGetErrorString(e));
+    }
   }
   if (regions != kRegionsNone && !owidth && !is_bool && n_pages) {
     e = plan_regions(ctx, p, pages, regions);

@@ -505,7 +505,7 @@ __device__ __forceinline__ void run_leaf(const Src& s, Shared& sh, const Stream 
     }
     case 1:
     case 2:
-    case 3:   // LZ4 / Zstd / Snappy general codecs: not yet on device
+    case 3:   // LZ4 / Zstd / Snappy: expanded first by the deferred / inflate passes, never a leaf here
     case 11:  // Dict / Freq nested below another Dict / Freq
     case 13:
     case 16:  // Patas (float streams)
@@ -3869,7 +3869,7 @@ __global__ __launch_bounds__(NT) void k_utf8_bytes(Utf8Args a) {
     }
     if (bad) {
       const uint32_t pg = utf8_page(a.n_pages, (uint64_t)bad_pos, [&](uint32_t i) { return a.bases[i]; });
-      a.status[pg] = ST_OUT_OF_SPEC;
+      atomicCAS(&a.status[pg], (uint32_t)ST_OK, (uint32_t)ST_OUT_OF_SPEC);  // (a page's earlier failure stands)
     }
   }
 }
@@ -3888,7 +3888,7 @@ __global__ __launch_bounds__(NT) void k_utf8_bounds(Utf8Args a) {
     if (in && utf8_trail(a.values[o])) {
       const uint64_t row = j < a.n_rows ? j : a.n_rows - 1;
       const uint32_t pg = utf8_page(a.n_pages, row, [&](uint32_t i) { return a.pages[i].row_off; });
-      a.status[pg] = ST_OUT_OF_SPEC;
+      atomicCAS(&a.status[pg], (uint32_t)ST_OK, (uint32_t)ST_OUT_OF_SPEC);
     }
   }
 }
@@ -3915,6 +3915,90 @@ __device__ void fill_bits(uint32_t n, uint64_t row_off, bool v, uint32_t* out) {
   }
 }
 
+// Page-relative bits [b, e) set in a zeroed word bitmap: whole words stored,
+// the two edge words OR-ed (a neighbouring run owns their other bits).
+__device__ __forceinline__ void set_bit_range(uint32_t* bm, uint64_t b, uint64_t e) {
+  if (b >= e) return;
+  const uint64_t fw = b >> 5, lw = (e - 1) >> 5;
+  for (uint64_t w = fw; w <= lw; w++) {
+    const uint32_t lo = w == fw ? (uint32_t)(b & 31) : 0u;
+    const uint32_t hi = w == lw ? (uint32_t)((e - 1) & 31) : 31u;
+    const uint32_t m = (hi == 31 ? 0xFFFFFFFFu : ((2u << hi) - 1)) & (0xFFFFFFFFu << lo);
+    if (m == 0xFFFFFFFFu) bm[w] = m;
+    else atomicOr(&bm[w], m);
+  }
+}
+
+// A Boolean page whose bytes plus expanded bitmap exceed the LDS
+// (max_page_size = None writes one page per column chunk,
+// write/common.rs:54-58): parsed from HBM; None pages funnel-shift their
+// bitmap bytes from the page, OneValue fills; RLE runs (each thread walks its
+// own chunk of runs, rle_prepare's starts) and LZ4 / Snappy / Zstd streams
+// (wave 0, expand_to_hbm) expand into the page's HBM region, which is then
+// funnel-shifted to the page's first row.  `lds` = the dynamic LDS
+// (expand_to_hbm's kBig* layout).
+__device__ void bool_big_page(const LaunchArgs& a, uint32_t page, const PageDesc& pd, Shared& sh, Stream& bs,
+                              uint8_t* lds) {
+  const uint32_t tid = threadIdx.x, n = pd.num_values, len = pd.byte_len, nb = (n + 7) / 8;
+  const GlbSrc s{a.chunk + pd.byte_off};
+  uint8_t* rg = a.region + (pd.reserved & kRegionOffMask);
+  uint32_t* rw = (uint32_t*)rg;
+  if (tid == 0) {
+    uint32_t p = 0;
+    sh.has_valid = 0;
+    do {
+      if (a.nullable && !parse_validity(s, sh, len, n, &p)) break;
+      if (!parse_stream(s, p, len, n, &bs)) { set_err(sh, ST_IO); break; }
+    } while (0);
+  }
+  __syncthreads();
+  if (sh.err) return;
+  if (sh.has_valid) write_validity(s, sh.vb_pos, n, pd.row_off, a.out_validity);
+  const Stream st = bs;
+  switch (st.codec) {
+    case 0:  // the page's bitmap bytes (basic.rs:68-71)
+      if (st.csize != nb) { if (tid == 0) set_err(sh, ST_OUT_OF_SPEC); }
+      else write_validity(s, st.body, n, pd.row_off, (uint32_t*)a.out_values);
+      return;
+    case 12:  // OneValue (boolean/one_value.rs:54-61)
+      if (st.body >= len) { if (tid == 0) set_err(sh, ST_IO); }
+      else fill_bits(n, pd.row_off, s.u8(st.body) != 0, (uint32_t*)a.out_values);
+      return;
+    case 10: {  // RLE (boolean/rle.rs:41-55): (u32 count, u8 value) runs over the rest of the page
+      for (uint32_t w = tid; w < (n + 31) / 32; w += NT) rw[w] = 0;
+      __threadfence();  // (the zeroes reach L2 before any run's atomics)
+      const Stream rs{10u, st.body, len - st.body, n};
+      rle_prepare<1>(s, sh, rs);  // run sums, chunk starts, overshoot / short checks (syncs)
+      if (sh.err) return;
+      const uint32_t R = sh.rle_R, c = sh.rle_c;
+      const uint32_t r0 = min(R, tid * c), r1 = min(R, r0 + c);
+      uint64_t b = sh.rle_start[tid];
+      for (uint32_t r = r0; r < r1 && b < n; r++) {
+        const uint32_t cnt = s.u32(rs.body + 5 * r);
+        const uint64_t e = min<uint64_t>(b + cnt, n);
+        if (s.u8(rs.body + 5 * r + 4) != 0) set_bit_range(rw, b, e);
+        b += cnt;
+      }
+      break;
+    }
+    case 1:
+    case 2:
+    case 3:  // LZ4 / Zstd / Snappy over the bitmap bytes
+      if (tid < 64) {
+        const uint32_t r = expand_to_hbm(st.codec, a.chunk + pd.byte_off + st.body, st.csize, rg, nb, lds);
+        if (r && tid == 0) set_err(sh, r);
+      }
+      break;
+    default:
+      if (tid == 0) set_err(sh, ST_OUT_OF_SPEC);  // Compression::from_codec / from_compression
+      return;
+  }
+  __threadfence();  // release the region's bytes ...
+  __syncthreads();
+  __threadfence();  // ... and drop stale L1 lines before reading them back
+  if (!sh.err) write_validity(GlbSrc{rg}, 0, n, pd.row_off, (uint32_t*)a.out_values);
+}
+
 __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
   extern __shared__ u32x4 stage[];
   __shared__ Shared sh;
@@ -3927,6 +4011,14 @@ __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
     const uint32_t need = (len + 15 + kStagePad + 15) & ~15u;
     const uint32_t xb = ((n + 7) / 8 + 15) & ~15u;
     if (tid == 0) sh.err = 0;
+    if (a.region && pd.reserved) {  // planned as a big page (sb_api plan_bool_regions)
+      __syncthreads();
+      bool_big_page(a, page, pd, sh, bs, (uint8_t*)stage);
+      __syncthreads();
+      if (tid == 0) a.status[page] = sh.err;
+      __syncthreads();
+      continue;
+    }
     if (need + xb + kStagePad > a.stage_bytes) {  // page + bitmap larger than the LDS budget
       __syncthreads();
       if (tid == 0) a.status[page] = ST_NYI;

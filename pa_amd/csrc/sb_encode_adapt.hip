@@ -46,6 +46,14 @@ constexpr int NT = SB_ENC_NT, NW = NT / 64;
 constexpr uint32_t kMaxRows = 16384;      // pages whose statistics' tables fit the LDS work area
 constexpr uint32_t kMaxNarrowRows = 65535;  // table words with 16-bit rows; larger pages use 64-bit words
 constexpr uint32_t SC = 10, SS = 64, kSample = SC * SS;
+// A big Boolean page's HBM work area: the RLE run starts (or the Snappy
+// table), then the page's bits one byte a row, then its rebuilt bitmap.
+__host__ __device__ constexpr uint64_t bool_work_head(uint64_t P) {
+  return (std::max<uint64_t>(4 * (P + 1), sbc::kSnappyTableBytes) + 15) & ~15ull;
+}
+__host__ __device__ constexpr uint64_t bool_work_bytes(uint64_t P) {
+  return bool_work_head(P) + ((P + 15) & ~15ull) + (((P + 7) / 8 + 16 + 15) & ~15ull);
+}
 
 enum : int { C_NONE = 0, C_LZ4 = 1, C_ZSTD = 2, C_SNAPPY = 3, C_RLE = 10, C_DICT = 11, C_ONE = 12, C_FREQ = 13, C_BP = 14,
              C_DBP = 15, C_PATAS = 16 };
@@ -1190,10 +1198,18 @@ __global__ __launch_bounds__(NT) void k_enc_bool(AdArgs A) {
   const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
   Ctx c;
   ctx_init(c, sh, A, p);
-  c.work = lds;
-  c.lz4 = (uint8_t*)lds;
-  c.samp = (uint8_t*)lds + A.work_bytes;
-  uint8_t* vals = c.samp + kSample * 8 + kSample / 8 + 16;
+  uint8_t* vals;
+  if (A.gwork) {  // a big page: run starts / Snappy table, staged bits and rebuilt bitmap in its HBM work area
+    c.work = (uint32_t*)(A.gwork + (uint64_t)blockIdx.x * A.gwork_bytes);
+    c.lz4 = (uint8_t*)lds;
+    c.samp = (uint8_t*)lds + sbc::kLz4WaveLds;
+    vals = (uint8_t*)c.work + bool_work_head(A.P);
+  } else {
+    c.work = lds;
+    c.lz4 = (uint8_t*)lds;
+    c.samp = (uint8_t*)lds + A.work_bytes;
+    vals = c.samp + kSample * 8 + kSample / 8 + 16;
+  }
   uint8_t* rebuilt = vals + ((A.P + 15) & ~15u);
   const uint32_t nb = (n + 7) / 8;
   for (uint32_t i = tid; i < n; i += NT) vals[i] = (A.values[(r0 + i) >> 3] >> ((r0 + i) & 7)) & 1;
@@ -1734,19 +1750,19 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
   const bool is_bool = phys == SB_T_BOOLEAN;
   // Pages over kMaxRows rows keep their work area in HBM (any size; over
   // kMaxNarrowRows with 64-bit table words and several roaring containers);
-  // Boolean pages stage their bits in LDS (kMaxRows)
+  // Boolean pages stage their bits in LDS up to kMaxRows, in HBM past it
   const bool stats = sba::needs_stats(o, o.forbidden);
   const bool big = P > sba::kMaxRows;
-  if (big && (is_bool || P * w > 0xFFFFFFF0ull || P > 0x7FFFFFFFull)) return SB_E_NYI;
+  if (big && (P * w > 0xFFFFFFF0ull || P > 0x7FFFFFFFull)) return SB_E_NYI;
   const uint64_t slot = adaptive_slot_bytes(P, w, nullable);
-  const uint64_t scr = ((P > 65535 ? 3 : 2) * P * 8 + 255) & ~255ull;  // (wide pages: roaring rows, level 2)
-  const uint64_t gwb = big ? big_work_bytes(P, stats) : 0;
+  const uint64_t scr = is_bool ? 256 : ((P > 65535 ? 3 : 2) * P * 8 + 255) & ~255ull;  // (wide: roaring rows, level 2)
+  const uint64_t gwb = !big ? 0 : is_bool ? sba::bool_work_bytes(P) : big_work_bytes(P, stats);
   const uint32_t batch = batch_pages(np, slot + scr + gwb);
   sba::Opts wo = o;
   if (is_bool) wo.has_ratio = 1;  // (k_enc_bool stages its bits after the full work area)
   const uint32_t work = big ? 0u : adaptive_work_bytes(P, wo);
   uint32_t lds = (big ? sbc::kLz4WaveLds : work) + sba::kSample * 8 + sba::kSample / 8 + 16;
-  if (is_bool) lds += (uint32_t)(((P + 15) & ~15ull) + (P + 7) / 8 + 16);  // staged bits + rebuilt bitmap
+  if (is_bool && !big) lds += (uint32_t)(((P + 15) & ~15ull) + (P + 7) / 8 + 16);  // staged bits + rebuilt bitmap
   uint8_t* slots = (uint8_t*)ctx_scratch(ctx, batch * slot + 256, 0);
   uint8_t* scratch = (uint8_t*)ctx_scratch(ctx, batch * scr, 1);
   uint64_t* meta = (uint64_t*)ctx_scratch(ctx, (2 * np + 2) * 8 + np * 4, 2);
@@ -1827,7 +1843,8 @@ int encode_binary_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, uint6
   const bool stats = sba::needs_stats(o, o.forbidden);
   const bool big = P > sba::kMaxRows;  // (work area in HBM, as encode_adaptive's)
   if (big && P > 0x7FFFFFFFull) return SB_E_NYI;
-  const uint64_t scr = (32 * P + 64 + 255) & ~255ull;
+  // rows / ids (32 P + 64 bytes), then roaring_multi's 4 u32 per container key
+  const uint64_t scr = (32 * P + 64 + 16 * ((P + 65535) >> 16) + 255) & ~255ull;
   const uint64_t gwb = big ? big_work_bytes(P, stats) : 0;
   const uint64_t maxpp = batch_pages(np, scr + gwb);
   hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);

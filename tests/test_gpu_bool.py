@@ -99,6 +99,82 @@ def test_bool_ragged_and_large_pages(ctx, n):
         assert (gv == ov).all() and (gm == om).all()
 
 
+BIG_OPTS = {
+    "none": dict(),
+    "lz4": dict(default_codec=O.LZ4),
+    "zstd": dict(default_codec=O.ZSTD),
+    "snappy": dict(default_codec=O.SNAPPY),
+    "rle": dict(forced=O.RLE),
+    "onevalue": dict(ratio=1.2),
+}
+
+
+@pytest.mark.parametrize("rows", [1 << 20, 3_000_000])
+@pytest.mark.parametrize("opt", list(BIG_OPTS))
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+def test_bool_single_page_columns(ctx, rows, opt, nullable):
+    """max_page_size = None writes one page per chunk (write/common.rs:54-58):
+    a Boolean page of 1M / 3M rows exceeds one workgroup's LDS and decodes
+    from HBM, its RLE / general-codec bitmap expanded into the page's region
+    (boolean/mod.rs:63-102).  Bit-exact against read_bool_column, both
+    nullabilities, every codec the writer can pick."""
+    rng = np.random.default_rng(rows + len(opt))
+    if opt == "onevalue":
+        v = np.ones(rows, bool)
+    elif opt == "rle":
+        v = np.repeat(rng.random(rows // 37 + 1) > 0.5, rng.integers(1, 75, rows // 37 + 1))[:rows]
+        v = np.resize(v, rows)
+    else:
+        v = np.repeat(rng.random(rows // 8 + 1) > 0.3, 8)[:rows] ^ (rng.random(rows) < 0.02)
+    valid = rng.random(rows) > 0.1
+    chunk, metas = oracle_chunk(v, valid, nullable, rows, O.WriteOptions.make(seed=5, **BIG_OPTS[opt]))
+    assert len(metas) == 1
+    ov, om = O.read_bool_column(chunk, metas, nullable)
+    gv, gm = gpu_bool(ctx, chunk, metas, nullable)
+    bad = np.flatnonzero(gv != ov)
+    assert len(bad) == 0, f"{len(bad)} values differ, first at {bad[:5]}"
+    if nullable:
+        assert (gm == om).all(), "validity differs"
+
+
+def test_bool_big_pages_beside_small_pages(ctx):
+    """Big and small pages in one column, at row offsets that are not
+    multiples of 32 (shared bitmap words on both sides of a big page)."""
+    rng = np.random.default_rng(4)
+    parts, metas, chunks, row = [], [], [], 0
+    for rows, opt in [(1001, "rle"), (700_003, "lz4"), (77, "none"), (900_001, "rle"), (5, "zstd"),
+                      (650_000, "none"), (800_000, "snappy")]:
+        v = np.repeat(rng.random(rows // 5 + 1) > 0.5, 5)[:rows]
+        valid = rng.random(rows) > 0.2
+        c, m = oracle_chunk(v, valid, True, rows, O.WriteOptions.make(**BIG_OPTS[opt]))
+        chunks.append(c)
+        metas += m
+    chunk = b"".join(chunks)
+    ov, om = O.read_bool_column(chunk, metas, True)
+    gv, gm = gpu_bool(ctx, chunk, metas, True)
+    assert (gv == ov).all() and (gm == om).all()
+
+
+def test_bool_big_malformed_pages(ctx):
+    """The big-page path reports the small path's statuses."""
+    import pa_amd
+
+    n = 1_500_000
+    good = O.write_bool_page(np.ones(n, bool), None, False, O.WriteOptions.make(forced=O.RLE))
+    nb = (n + 7) // 8
+    cases = {
+        "rle short": good[:9] + (n - 1).to_bytes(4, "little") + b"\x01",
+        "rle overshoot": good[:9] + (n + 1).to_bytes(4, "little") + b"\x01",
+        "none size": bytes([0]) + (nb - 1).to_bytes(4, "little") + n.to_bytes(4, "little") + b"\xff" * (nb - 1),
+        "lz4 garbage": bytes([1]) + (nb).to_bytes(4, "little") + n.to_bytes(4, "little") + b"\xf0" * nb,
+    }
+    for name, page in cases.items():
+        with pytest.raises(pa_amd.StrawboatError):
+            gpu_bool(ctx, page, [(len(page), n)], False)
+        with pytest.raises(O.OracleError):
+            O.read_bool_column(page, [(len(page), n)], False)
+
+
 def test_bool_product_encoder_roundtrip(ctx):
     import pa_amd
 
