@@ -49,6 +49,7 @@ constexpr uint32_t kMaxBitmapConts = 4;  // of which bitmap containers (card > 4
 constexpr uint32_t kRleFastRows = 8192;  // RLE pages up to this many rows use the run-start bitmap
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <int W> struct VT { using T = uint32_t; };
 template <> struct VT<8> { using T = uint64_t; };
@@ -1158,7 +1159,7 @@ __device__ uint32_t snappy_wave(WaveWin& w, uint32_t p, uint32_t pend, WaveOut<R
 //     source ends before the batch's first match byte are copied
 //     lane-parallel and the rest in sequence order, wave-wide.
 // The compressed stream is staged into a per-wave kIb ring (LDS-DMA at a
-// seek, then a KiB at a time from registers loaded a KiB ahead).
+// seek, then half a ring at a time from registers loaded half a ring ahead).
 // ---------------------------------------------------------------------------
 // Record chains through a window, wave-parallel.  Variable-length records
 // whose size follows from their own header (Patas records, LZ4 sequences)
@@ -1198,9 +1199,10 @@ __device__ __forceinline__ uint32_t wave_chain(uint32_t t1) {
   return x;
 }
 
-// wave_chain through LDS byte tables: T1..T32 at tab + 256 j (T1 byte 255
-// must be 0xFF, so every table maps 0xFF to itself and no lookup needs a
-// guard); one byte read per lookup instead of a permute and a byte extract.
+// wave_chain through LDS byte tables: T1..T32 at tab + 256 j (T1 bytes 254
+// and 255 must be 0xFE and 0xFF, so every table maps both sentinels to
+// themselves and no lookup needs a guard); one byte read per lookup instead
+// of a permute and a byte extract.
 __device__ __forceinline__ uint32_t lds_chain(lds_u8* tab, uint32_t t1) {
   typedef __attribute__((address_space(3))) uint32_t l32;
   const uint32_t lane = threadIdx.x & 63;
@@ -1224,51 +1226,51 @@ __device__ __forceinline__ uint32_t lds_chain(lds_u8* tab, uint32_t t1) {
   return x;
 }
 
-constexpr uint32_t kIb = 2048, kLitFast = 64, kMatchFast = 32;
+constexpr uint32_t kIb = 1024, kIbHalf = kIb / 2, kLitFast = 64, kMatchFast = 32;
+constexpr uint32_t kChainTabs = 6;  // T1..T32: batches of up to 64 sequences
+constexpr uint32_t kChainEnd = 0xFE, kChainStop = 0xFF;  // chain sentinels (see cand_steps)
 
 struct InRing {
   gmem_u32* g;   // dword-aligned stream base
   uint32_t nd;   // stream dwords
-  lds_u8* ib;    // kIb (2 KiB) bytes: stream byte x at ib[x % kIb]
-  lds_u8* ct;    // 7 x 256 bytes: the chain tables T1..T32 and the candidates' accept table
-  uint32_t base; // [base, base + 2 KiB) staged and complete; base % 1 KiB == 0
-  u32x4 pf;      // [base + 2 KiB, base + 3 KiB), 16 bytes a lane, loaded ahead in registers
-  // (a 2 KiB ring keeps the wave at 7.75 KiB of LDS: five waves per SIMD)
+  lds_u8* ib;    // kIb (1 KiB) bytes: stream byte x at ib[x % kIb]
+  lds_u8* ct;    // kChainTabs x 256 bytes: the chain tables T1..T32
+  uint32_t base; // [base, base + kIb) staged and complete; base % kIbHalf == 0
+  u32x2 pf;      // [base + kIb, base + kIb + kIbHalf), 8 bytes a lane, loaded ahead in registers
+  // (a 1 KiB ring and six chain tables keep the wave at 6.5 KiB of LDS: six waves per SIMD)
 
-  __device__ __forceinline__ void dma(uint32_t b) {  // [b, b + 1 KiB) -> ib
+  __device__ __forceinline__ void dma(uint32_t b) {  // [b, b + kIbHalf) -> ib
     const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
+    for (uint32_t k = 0; k < kIbHalf / 256; k++) {
       const uint32_t dw = min((b >> 2) + 64 * k + lane, nd - 1);
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g + dw),
                                        (__attribute__((address_space(3))) void*)(ib + (b & (kIb - 1)) + 256 * k), 4,
                                        0, 0);
     }
   }
-  __device__ __forceinline__ void prefetch(uint32_t b) {  // [b, b + 1 KiB) -> pf
-    const uint32_t i = (b >> 2) + 4 * (threadIdx.x & 63);
+  __device__ __forceinline__ void prefetch(uint32_t b) {  // [b, b + kIbHalf) -> pf
+    const uint32_t i = (b >> 2) + 2 * (threadIdx.x & 63);
     pf.x = g[min(i, nd - 1)];
     pf.y = g[min(i + 1, nd - 1)];
-    pf.z = g[min(i + 2, nd - 1)];
-    pf.w = g[min(i + 3, nd - 1)];
   }
   __device__ void seek(uint32_t x) {
-    base = x & ~1023u;
+    base = x & ~(kIbHalf - 1);
     dma(base);
-    dma(base + 1024);
+    dma(base + kIbHalf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    prefetch(base + 2048);
+    prefetch(base + kIb);
   }
   __device__ __forceinline__ void slide(uint32_t p) {
-    if (p - base < 1024) return;
-    if (p - base >= 2048) { seek(p); return; }
-    // the prefetched KiB into the slot of base, then the next one
-    *(__attribute__((address_space(3))) u32x4*)(ib + (base & (kIb - 1)) + 16 * (threadIdx.x & 63)) = pf;
-    base += 1024;
-    prefetch(base + 2048);
+    if (p - base < kIbHalf) return;
+    if (p - base >= kIb) { seek(p); return; }
+    // the prefetched half into the slot of base, then the next one
+    *(__attribute__((address_space(3))) u32x2*)(ib + (base & (kIb - 1)) + 8 * (threadIdx.x & 63)) = pf;
+    base += kIbHalf;
+    prefetch(base + kIb);
   }
   __device__ __forceinline__ uint32_t ubyte(uint32_t x) const {  // uniform
-    if (x - base < 2048) return ib[x & (kIb - 1)];
+    if (x - base < kIb) return ib[x & (kIb - 1)];
     return ((gmem_u8*)g)[x];
   }
 };
@@ -1346,13 +1348,18 @@ __device__ __forceinline__ uint32_t lane_mod(uint32_t lane, uint32_t o) {
   return lane - q * o;
 }
 
-// Successor table of the 256 candidate starts p + r (r = 4 lane + k): byte k
-// = r + d for a sequence of d bytes that batch decoding takes (literal <=
-// kLitFast, each length with at most one extension byte, not the final
-// sequence, staged below lim), else 0xFF (the chain stops); byte k of *okt
-// is 1 for such a sequence (the chain's last one may end past the window).
-__device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uint32_t lim, uint32_t pend,
-                                               uint32_t* okt) {
+// Successor table of the candidate starts p + r (r = 4 lane + k < 254):
+// byte k = r + d for a sequence of d bytes that batch decoding takes (literal
+// <= kLitFast, each length with at most one extension byte, not the final
+// sequence, staged below lim), kChainEnd when such a sequence's successor
+// lies past position 253 (the batch ends after it), else kChainStop (the
+// sequence is not taken); entries 254 and 255 are the sentinels themselves.
+// A chain position x is a taken sequence iff x < kChainEnd and T1[x] !=
+// kChainStop.
+__device__ __forceinline__ uint32_t succ_byte(bool ok, uint32_t nr) {
+  return !ok ? kChainStop : nr < kChainEnd ? nr : kChainEnd;
+}
+__device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uint32_t lim, uint32_t pend) {
   typedef __attribute__((address_space(3))) uint32_t l32;
   const l32* ib32 = (const l32*)ib;
   const uint32_t lane = threadIdx.x & 63;
@@ -1362,7 +1369,7 @@ __device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uin
   const uint32_t tok = __builtin_amdgcn_alignbyte(w1, w0, sh);   // bytes x0 .. x0 + 3
   const uint32_t nxt = __builtin_amdgcn_alignbyte(w2, w1, sh);   // bytes x0 + 4 .. x0 + 7
   const uint32_t ext = __builtin_amdgcn_alignbyte(nxt, tok, 1);  // bytes x0 + 1 .. x0 + 4
-  uint32_t t1 = 0, ov = 0;
+  uint32_t t1 = 0;
   if (lim - p >= 325) {  // every candidate's bytes (<= p + 324) are staged: no bounds checks
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
@@ -1373,11 +1380,9 @@ __device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uin
       const uint32_t e2 = ib[y & (kIb - 1)], mx = (t & 15) == 15;
       const bool ok = lit <= kLitFast && !(mx && e2 == 255);
       const uint32_t r = 4 * lane + k, nr = r + (y + mx - x);
-      t1 |= (ok && nr < 255 ? nr : 0xFFu) << (8 * k);
-      ov |= (uint32_t)ok << (8 * k);
+      t1 |= succ_byte(ok, nr) << (8 * k);
     }
-    *okt = ov;
-    return t1;
+    return lane == 63 ? (t1 & 0xFFFFu) | (kChainEnd << 16) | (kChainStop << 24) : t1;
   }
 #pragma unroll
   for (uint32_t k = 0; k < 4; k++) {
@@ -1394,11 +1399,9 @@ __device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uin
       y++;
     }
     const uint32_t r = 4 * lane + k, nr = r + (y - x);
-    t1 |= (ok && nr < 255 ? nr : 0xFFu) << (8 * k);
-    ov |= (uint32_t)ok << (8 * k);
+    t1 |= succ_byte(ok, nr) << (8 * k);
   }
-  *okt = ov;
-  return t1;
+  return lane == 63 ? (t1 & 0xFFFFu) | (kChainEnd << 16) | (kChainStop << 24) : t1;
 }
 
 // The sequence at x, which cand_steps accepted (no checks left to make).
@@ -1470,25 +1473,47 @@ __device__ uint32_t lz4_one(InRing& in, uint32_t* pp, uint32_t pend, WaveOut<tru
   return ST_OK;
 }
 
+#ifdef SB_INF_PHASES  // A/B instrumentation: shader cycles per phase of the batch loop, summed over waves
+// [0] slide [1] candidates [2] chain [3] parse + place [4] literals [5] free matches [6] hazards [7] flush
+// [8] serial path; counts: [9] batches [10] sequences [11] hazards [12] serial sequences [13] jobs
+__device__ unsigned long long sb_dbg_inf[16];
+#define INF_T(k)                                                         \
+  do {                                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                    \
+    ph[k] += t_ - tph;                                                   \
+    tph = t_;                                                            \
+  } while (0)
+#define INF_N(k, v) ph[k] += (v)
+#else
+#define INF_T(k) do { } while (0)
+#define INF_N(k, v) do { } while (0)
+#endif
+
 __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<true>& o) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t olen = o.olen;
   if (p == pend) return olen == 0 ? ST_OK : ST_CODEC;
   bool ended = false;
+#ifdef SB_INF_PHASES
+  uint64_t ph[16] = {0};
+  uint64_t tph = __builtin_amdgcn_s_memtime();
+  INF_N(13, 1);
+#endif
   while (p < pend && !ended) {
     in.slide(p);
-    const uint32_t lim = min(in.base + 2048, pend);
+    INF_T(0);
+    const uint32_t lim = min(in.base + kIb, pend);
     // 1. successor distances of the candidate starts x = p + 4 lane + k, from
     //    the token and at most one extension byte per length: the tokens are
     //    one unaligned dword of the ring, the literal extensions the next
     //    bytes; only a match-length extension needs its own byte read
-    uint32_t okt;
-    const uint32_t t1 = cand_steps(in.ib, p, lim, pend, &okt);
+    const uint32_t t1 = cand_steps(in.ib, p, lim, pend);
+    INF_T(1);
     // 2. the chain of sequence starts from p, wave-parallel (wave_chain): a
     //    candidate that needs the serial path ends it
     const uint32_t cx = lds_chain(in.ct, t1);
-    ((__attribute__((address_space(3))) uint32_t*)in.ct)[64 * 6 + lane] = okt;
-    const uint32_t j = (uint32_t)__popcll(__ballot(cx != 0xFF && in.ct[256 * 6 + cx] == 1));
+    const uint32_t j = (uint32_t)__popcll(__ballot(cx < kChainEnd && in.ct[cx] != kChainStop));
+    INF_T(2);
     const uint32_t starts = p + cx;
     // 3. decode and place
     Seq s{0, 0, 0, 0, 0};
@@ -1502,11 +1527,16 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     const bool ok = v0 && incl <= cap && s.off != 0 && s.off <= dm;
     const uint64_t okm = __ballot(ok);
     const uint32_t k = okm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);
+    INF_T(3);
     if (k == 0) {  // the serial path takes one sequence (and reports errors)
       const uint32_t st = lz4_one(in, &p, pend, o, &ended);
       if (st) return st;
+      INF_T(8);
+      INF_N(12, 1);
       continue;
     }
+    INF_N(9, 1);
+    INF_N(10, k);
 #ifdef SB_V_NOCOPY
     const bool v = false;
 #else
@@ -1529,6 +1559,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
         ring_put<5>(o.ring, dl + c, n, sh, w);
       }
     }
+    INF_T(4);
     const uint32_t d_first = __builtin_amdgcn_readfirstlane(dm);
     const uint32_t src = dm - s.off;
 #ifdef SB_V_NOHAZ
@@ -1570,6 +1601,8 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
         o.ring[(dm + i) & (kRing - 1)] = (uint8_t)b;
       }
     }
+    INF_T(5);
+    INF_N(11, __popcll(__ballot(hazard)));
     for (uint64_t hm = __ballot(hazard); hm; hm &= hm - 1) {
       const uint32_t l = (uint32_t)__builtin_ctzll(hm);
       const uint32_t D = __builtin_amdgcn_readlane(dm, l), O = __builtin_amdgcn_readlane(s.off, l),
@@ -1587,11 +1620,16 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
         }
       }
     }
+    INF_T(6);
     const uint32_t nop = o.op + __builtin_amdgcn_readlane(incl, k - 1);
     p = k == j ? q : __builtin_amdgcn_readlane(starts, k);
     if ((nop / kChunk) != (o.op / kChunk)) o.flush(o.op & ~(kChunk - 1), kChunk);
     o.op = nop;
+    INF_T(7);
   }
+#ifdef SB_INF_PHASES
+  if (lane < 14) atomicAdd(&sb_dbg_inf[lane], (unsigned long long)ph[lane]);
+#endif
   if (!ended || o.op != olen) return ST_CODEC;
   o.finish();
   return ST_OK;
@@ -2416,12 +2454,12 @@ static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
 // workgroup, so 8 waves per SIMD can be resident and the serial token streams
 // of many pages overlap.
 #ifndef SB_INF_BLOCKS
-#define SB_INF_BLOCKS 5  // 4-wave workgroups: 5 waves per SIMD (7.75 KiB of LDS and <= 96 VGPRs a wave)
+#define SB_INF_BLOCKS 6  // 4-wave workgroups: 6 waves per SIMD (6.5 KiB of LDS and <= 80 VGPRs a wave)
 #endif
 __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(InflateLaunch a) {
   __shared__ u32x4 rings[kInfWaves][kRing / 16];
   __shared__ u32x4 ibufs[kInfWaves][kIb / 16];
-  __shared__ u32x4 ctabs[kInfWaves][7 * 256 / 16];
+  __shared__ u32x4 ctabs[kInfWaves][kChainTabs * 256 / 16];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = a.count ? *a.count : a.n_jobs;
@@ -5124,6 +5162,15 @@ int launch_utf8_check(int offset_width, const Utf8Launch& a, void* stream) {
 }
 }  // namespace sb
 
+#ifdef SB_INF_PHASES
+extern "C" int sb_debug_inf_phases(uint64_t* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(sbk::sb_dbg_inf), 16 * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" int sb_debug_inf_reset() {
+  static const unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(sbk::sb_dbg_inf), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef SB_BIN_PHASES
 extern "C" int sb_debug_bin_phases(uint64_t* host, uint64_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(sbk::sb_dbg_phase), std::min<uint64_t>(n, 4096 * 6) * 8) == hipSuccess ? 0 : -1;

@@ -1,30 +1,72 @@
 //! The reference's own API shapes over the engine, so a
-//! `strawboat` (b41sh/pa 0.2.6) maintainer swaps the codec path without
-//! rewriting callers:
+//! `strawboat` (b41sh/pa 0.2.6) caller swaps the codec path without touching
+//! its call sites:
 //!
 //! | reference | here |
 //! |---|---|
+//! | `read::NativeReadBuf` (src/read/mod.rs:26-53) | [`NativeReadBuf`] |
 //! | `read::PageIterator` (src/read/mod.rs:55-57) | [`PageIterator`] |
 //! | `read::reader::NativeReader::{new, has_next, current_page, skip_page}` + `Iterator` (src/read/reader.rs:51-146) | [`NativeReader`] |
-//! | `read::deserialize::column_iter_to_arrays` (src/read/deserialize.rs:237-253) | [`column_iter_to_arrays`] |
+//! | `read::deserialize::{column_iter_to_arrays, ArrayIter}` (src/read/deserialize.rs:237-253) | [`column_iter_to_arrays`], [`ArrayIter`] |
 //! | `read::batch_read::batch_read_array` (src/read/batch_read.rs:190-209) | [`batch_read_array`] |
 //! | `write::writer::NativeWriter::{try_new, new, into_inner, start, write, finish, total_size}` (src/write/writer.rs:42-173) | [`NativeWriter`] |
+//! | `write::WriteOptions` (src/write/common.rs:37-45) | [`WriteOptions`] |
+//! | `compression::{Compression, CommonCompression}` (src/compression/mod.rs:37-108, basic.rs:23-60) | [`Compression`], [`CommonCompression`] |
 //!
-//! Every function keeps the reference's parameters in the reference's order
-//! and adds the engine [`Context`] (one device + one HIP stream) in front:
-//! that is where the pages are decoded.  arrow2 / parquet2 types are
-//! stood in for by the minimal [`Field`], [`DataType`], [`ColumnDescriptor`],
-//! [`Schema`] and [`Chunk`] below (this crate has no dependencies); the
-//! decoded [`Array`] holds Arrow buffers in HBM, which the caller wraps into
-//! arrow2 arrays.
-use std::io::{Read, Seek, SeekFrom, Write};
+//! Every entry point keeps the reference's parameters, in the reference's
+//! order, with the reference's bounds.  Pages are decoded on the calling
+//! thread's default engine context ([`default_context`]: one per thread and
+//! HIP device, created on first use, as `pa_amd.default_context` does), so no
+//! call site passes one.  arrow2 / parquet2 types are stood in for by the
+//! minimal [`Field`], [`DataType`], [`ColumnDescriptor`], [`Schema`],
+//! [`Chunk`] and [`Array`] below (this crate has no dependencies).  An
+//! [`Array`] is a row range of a decoded column whose Arrow buffers stay in
+//! HBM; the per-page arrays of [`column_iter_to_arrays`] share one decode of
+//! the whole chunk, as arrow2's sliced arrays share their buffers
+//! (INTEGRATION.md shows the arrow2 wrapping).
+use std::cell::RefCell;
+use std::collections::VecDeque;
+use std::io::{BufRead, BufReader, Cursor, Read, Seek, SeekFrom, Write};
 use std::os::raw::c_void;
 use std::ptr;
+use std::rc::Rc;
+use std::sync::Arc;
 
 use crate::{
     ffi, status, Binary, BinaryColumn, ColumnMeta, Context, DeviceBuffer, Error, List, ListColumn, Nested,
-    NestedColumn, PageMeta, PhysicalType, Primitive, PrimitiveColumn, Result, WriteOptions,
+    NestedColumn, PageMeta, PhysicalType, Primitive, PrimitiveColumn, Result,
 };
+
+/// `read::NativeReadBuf` (src/read/mod.rs:26-53): a buffered reader that
+/// lets the caller peek at its buffered bytes.
+pub trait NativeReadBuf: BufRead {
+    fn buffer_bytes(&self) -> &[u8];
+}
+
+impl<R: Read> NativeReadBuf for BufReader<R> {
+    fn buffer_bytes(&self) -> &[u8] {
+        self.buffer()
+    }
+}
+
+impl NativeReadBuf for &[u8] {
+    fn buffer_bytes(&self) -> &[u8] {
+        self
+    }
+}
+
+impl<T: AsRef<[u8]>> NativeReadBuf for Cursor<T> {
+    fn buffer_bytes(&self) -> &[u8] {
+        let len = self.position().min(self.get_ref().as_ref().len() as u64);
+        &self.get_ref().as_ref()[(len as usize)..]
+    }
+}
+
+impl<B: NativeReadBuf + ?Sized> NativeReadBuf for Box<B> {
+    fn buffer_bytes(&self) -> &[u8] {
+        (**self).buffer_bytes()
+    }
+}
 
 /// `read::PageIterator` (src/read/mod.rs:55-57): a page source that hands
 /// its read buffer back for reuse.
@@ -32,18 +74,43 @@ pub trait PageIterator {
     fn swap_buffer(&mut self, buffer: &mut Vec<u8>);
 }
 
+thread_local! {
+    static DEFAULT_CONTEXTS: RefCell<Vec<Rc<Context>>> = RefCell::new(Vec::new());
+}
+
+/// The calling thread's engine context on its current HIP device
+/// (`hipSetDevice` picks the device), created on first use and kept for the
+/// thread's lifetime.  An `sb_ctx` is one device + one HIP stream and is not
+/// shared between threads.
+pub fn default_context() -> Result<Rc<Context>> {
+    let mut dev = 0;
+    let e = unsafe { ffi::hipGetDevice(&mut dev) };
+    if e != 0 {
+        return Err(Error::Device(format!("hipGetDevice failed: {e}")));
+    }
+    DEFAULT_CONTEXTS.with(|c| {
+        let mut v = c.borrow_mut();
+        if let Some(x) = v.iter().find(|x| x.device() == dev) {
+            return Ok(x.clone());
+        }
+        let ctx = Rc::new(Context::new(dev)?);
+        v.push(ctx.clone());
+        Ok(ctx)
+    })
+}
+
 /// `read::reader::NativeReader` (src/read/reader.rs:51-146): the pages of
 /// one column chunk, read in order from `page_reader` (positioned at the
 /// chunk's first page, `ColumnMeta::offset`).
 #[derive(Debug)]
-pub struct NativeReader<R: Read + Seek> {
+pub struct NativeReader<R: NativeReadBuf> {
     page_reader: R,
     page_metas: Vec<PageMeta>,
     current_page: usize,
     scratch: Vec<u8>,
 }
 
-impl<R: Read + Seek> NativeReader<R> {
+impl<R: NativeReadBuf> NativeReader<R> {
     pub fn new(page_reader: R, page_metas: Vec<PageMeta>, scratch: Vec<u8>) -> Self {
         NativeReader { page_reader, page_metas, current_page: 0, scratch }
     }
@@ -56,41 +123,28 @@ impl<R: Read + Seek> NativeReader<R> {
     pub fn current_page(&self) -> usize {
         self.current_page
     }
+}
 
+impl<R: NativeReadBuf + Seek> NativeReader<R> {
     /// Skips the next page (reader.rs:134-145).
     pub fn skip_page(&mut self) -> Result<()> {
         if self.current_page == self.page_metas.len() {
             return Ok(());
         }
         let len = self.page_metas[self.current_page].length;
-        self.page_reader.seek(SeekFrom::Current(len as i64)).map_err(|e| Error::Io(e.to_string()))?;
+        self.page_reader.seek(SeekFrom::Current(len as i64)).map_err(io)?;
         self.current_page += 1;
         Ok(())
     }
-
-    /// The rest of the chunk's pages in one read (batch_read's read_simple
-    /// reads them page by page into one buffer).
-    fn read_rest(&mut self) -> Result<(Vec<u8>, Vec<PageMeta>)> {
-        let metas = self.page_metas[self.current_page..].to_vec();
-        let mut len = 0u64;
-        for m in &metas {
-            len = len.checked_add(m.length).ok_or_else(|| Error::OutOfSpec("chunk length overflows u64".into()))?;
-        }
-        let mut buf = std::mem::take(&mut self.scratch);
-        buf.resize(len as usize, 0);
-        self.page_reader.read_exact(&mut buf).map_err(|e| Error::Io(e.to_string()))?;
-        self.current_page = self.page_metas.len();
-        Ok((buf, metas))
-    }
 }
 
-impl<R: Read + Seek> PageIterator for NativeReader<R> {
+impl<R: NativeReadBuf> PageIterator for NativeReader<R> {
     fn swap_buffer(&mut self, scratch: &mut Vec<u8>) {
         std::mem::swap(&mut self.scratch, scratch)
     }
 }
 
-impl<R: Read + Seek> Iterator for NativeReader<R> {
+impl<R: NativeReadBuf + Seek> Iterator for NativeReader<R> {
     type Item = Result<(u64, Vec<u8>)>;
 
     /// The next page: (num_values, page bytes) (reader.rs:119-131).
@@ -102,7 +156,7 @@ impl<R: Read + Seek> Iterator for NativeReader<R> {
         let meta = self.page_metas[self.current_page];
         buffer.resize(meta.length as usize, 0);
         if let Err(e) = self.page_reader.read_exact(&mut buffer) {
-            return Some(Err(Error::Io(e.to_string())));
+            return Some(Err(io(e)));
         }
         self.current_page += 1;
         Some(Ok((meta.num_values, buffer)))
@@ -122,7 +176,7 @@ impl<R: Read + Seek> Iterator for NativeReader<R> {
         }
         if length > 0 {
             if let Err(e) = self.page_reader.seek(SeekFrom::Current(length as i64)) {
-                return Some(Err(Error::Io(e.to_string())));
+                return Some(Err(io(e)));
             }
         }
         self.next()
@@ -174,13 +228,65 @@ pub struct ColumnDescriptor {
     pub max_rep_level: i16,
 }
 
-/// A decoded column (or page): its Arrow buffers in HBM.
-pub enum Array {
+/// The Arrow buffers (in HBM) of one decoded column chunk.
+pub enum ColumnData {
     Primitive(Primitive),
     Binary(Binary),
     List(List),
     Nested(Nested),
 }
+
+impl ColumnData {
+    /// Top-level rows.
+    pub fn rows(&self) -> u64 {
+        match self {
+            ColumnData::Primitive(p) => p.len,
+            ColumnData::Binary(b) => b.len,
+            ColumnData::List(l) => l.rows,
+            ColumnData::Nested(n) => n.counts[0],
+        }
+    }
+}
+
+/// arrow2 `Box<dyn Array>`: rows [offset, offset + len) of a decoded column.
+/// Like arrow2's sliced arrays it is a view: the per-page arrays of one
+/// column share its buffers; `offset` is the first row's index into them
+/// (the bit offset of its validity and Boolean values, the index of its first
+/// offset).
+#[derive(Clone)]
+pub struct Array {
+    data_type: DataType,
+    data: Arc<ColumnData>,
+    offset: u64,
+    len: u64,
+}
+
+impl Array {
+    pub fn data_type(&self) -> &DataType {
+        &self.data_type
+    }
+    pub fn data(&self) -> &ColumnData {
+        &self.data
+    }
+    pub fn offset(&self) -> u64 {
+        self.offset
+    }
+    pub fn len(&self) -> usize {
+        self.len as usize
+    }
+    pub fn is_empty(&self) -> bool {
+        self.len == 0
+    }
+    /// arrow2 `Array::sliced`: rows [offset, offset + length) of this array.
+    pub fn sliced(&self, offset: usize, length: usize) -> Array {
+        assert!(offset as u64 + length as u64 <= self.len, "the offset of the new array cannot exceed the existing length");
+        Array { data_type: self.data_type.clone(), data: self.data.clone(), offset: self.offset + offset as u64, len: length as u64 }
+    }
+}
+
+/// `read::ArrayIter` (src/read/deserialize.rs): the arrays of a column, one
+/// per page.
+pub type ArrayIter<'a> = Box<dyn Iterator<Item = Result<Array>> + Send + Sync + 'a>;
 
 /// The leaf under a field: its physical type, per list level (outermost
 /// first) the level's nullability and whether it is a LargeList, and the
@@ -219,14 +325,15 @@ fn leaf_path(field: &Field) -> Result<(PhysicalType, Vec<bool>, Vec<bool>, bool)
 
 /// The read/deserialize.rs dispatch over one column chunk in HBM: flat
 /// primitive / Boolean, Binary / Utf8, List<primitive>, or any other list
-/// nesting (depth 1..=4, every leaf kind).
-fn decode_chunk(ctx: &Context, chunk: &DeviceBuffer, pages: &[PageMeta], field: &Field) -> Result<Array> {
+/// nesting (depth 1..=4, every leaf kind).  Returns once the decode has
+/// finished (the per-page statuses are read back).
+fn decode_chunk(ctx: &Context, chunk: &DeviceBuffer, pages: &[PageMeta], field: &Field) -> Result<ColumnData> {
     let (ty, lists, large, leaf_nullable) = leaf_path(field)?;
     if lists.is_empty() {
         return if ty.is_binary() {
-            Ok(Array::Binary(BinaryColumn::plan(ctx, chunk, pages, ty, leaf_nullable)?.decode()?))
+            Ok(ColumnData::Binary(BinaryColumn::plan(ctx, chunk, pages, ty, leaf_nullable)?.decode()?))
         } else {
-            Ok(Array::Primitive(PrimitiveColumn::plan(ctx, chunk, pages, ty, leaf_nullable)?.decode()?))
+            Ok(ColumnData::Primitive(PrimitiveColumn::plan(ctx, chunk, pages, ty, leaf_nullable)?.decode()?))
         };
     }
     if large.iter().any(|&l| l != large[0]) {
@@ -234,10 +341,17 @@ fn decode_chunk(ctx: &Context, chunk: &DeviceBuffer, pages: &[PageMeta], field: 
     }
     if lists.len() == 1 && !ty.is_binary() && ty != PhysicalType::Boolean {
         let c = ListColumn::plan(ctx, chunk, pages, ty, lists[0], leaf_nullable, large[0])?;
-        return Ok(Array::List(c.decode()?));
+        return Ok(ColumnData::List(c.decode()?));
     }
     let c = NestedColumn::plan(ctx, chunk, pages, ty, &lists, leaf_nullable, large[0])?;
-    Ok(Array::Nested(c.decode()?))
+    Ok(ColumnData::Nested(c.decode()?))
+}
+
+/// Column chunk bytes into HBM on the thread's default context, decoded.
+fn decode_host_chunk(bytes: &[u8], pages: &[PageMeta], field: &Field) -> Result<ColumnData> {
+    let ctx = default_context()?;
+    let chunk = ctx.upload(bytes)?;
+    decode_chunk(&ctx, &chunk, pages, field)
 }
 
 fn one_leaf(leaves: &[ColumnDescriptor], field: &Field) -> Result<()> {
@@ -251,78 +365,225 @@ fn one_leaf(leaves: &[ColumnDescriptor], field: &Field) -> Result<()> {
     Ok(())
 }
 
+fn check_nested(is_nested: bool, field: &Field) -> Result<()> {
+    if is_nested != matches!(field.data_type, DataType::List(_) | DataType::LargeList(_)) {
+        return Err(Error::Argument(format!("{}: is_nested {is_nested} against its data type", field.name)));
+    }
+    Ok(())
+}
+
 /// `batch_read_array` (src/read/batch_read.rs:190-209): every page of the
 /// column at once, one array.  The chunk's pages are read from the reader
-/// in one read, staged into HBM on the context's device and decoded there.
-pub fn batch_read_array<R: Read + Seek>(
-    ctx: &Context,
-    mut readers: Vec<NativeReader<R>>,
+/// in one read, staged into HBM with one copy and decoded there.
+pub fn batch_read_array<R: NativeReadBuf>(
+    mut readers: Vec<R>,
     leaves: Vec<ColumnDescriptor>,
     field: Field,
     is_nested: bool,
     mut page_metas: Vec<Vec<PageMeta>>,
 ) -> Result<Array> {
     one_leaf(&leaves, &field)?;
+    check_nested(is_nested, &field)?;
     let mut reader = readers.pop().ok_or_else(|| Error::Argument("no reader".into()))?;
     let metas = page_metas.pop().ok_or_else(|| Error::Argument("no page metas".into()))?;
-    if is_nested != matches!(field.data_type, DataType::List(_) | DataType::LargeList(_)) {
-        return Err(Error::Argument(format!("{}: is_nested {is_nested} against its data type", field.name)));
-    }
-    if metas.len() != reader.page_metas.len() - reader.current_page {
-        return Err(Error::Argument("page metas differ from the reader's".into()));
-    }
-    let (mut bytes, _) = reader.read_rest()?;
-    let out = ctx.upload(&bytes).and_then(|chunk| decode_chunk(ctx, &chunk, &metas, &field));
-    reader.swap_buffer(&mut bytes);  // the read buffer back to the reader for reuse
-    out
+    let len = ColumnMeta { offset: 0, pages: metas.clone() }.total_len()?;
+    let len = usize::try_from(len).map_err(|_| Error::OutOfSpec("column chunk larger than the address space".into()))?;
+    let mut bytes = vec![0u8; len];
+    reader.read_exact(&mut bytes).map_err(io)?;
+    let data = decode_host_chunk(&bytes, &metas, &field)?;
+    let len = data.rows();
+    Ok(Array { data_type: field.data_type, data: Arc::new(data), offset: 0, len })
 }
 
-/// The iterator `column_iter_to_arrays` returns: one array per page (the
-/// reference's streaming read yields one array per page).
-pub struct ArrayIter<'a, I> {
-    ctx: &'a Context,
-    reader: I,
+/// The rows of a nested page: its `u32 rows` header (write_nested_validity,
+/// serialize.rs:217-232; read_validity_nested, read_basic.rs:72).
+fn nested_page_rows(page: &[u8]) -> Result<u64> {
+    if page.len() < 4 {
+        return Err(Error::OutOfSpec("nested page shorter than its header".into()));
+    }
+    Ok(u32::from_le_bytes([page[0], page[1], page[2], page[3]]) as u64)
+}
+
+/// The iterator `column_iter_to_arrays` returns.  On the first call it
+/// drains the page reader (handing every page buffer back through
+/// `swap_buffer`), stages the chunk into HBM with one copy and plans and
+/// decodes it once; each page then becomes the row range of the decoded
+/// column it covers.  A read or decode error is returned by that first
+/// call.
+struct PageArrays<I> {
+    reader: Option<I>,
     field: Field,
+    is_nested: bool,
+    pages: VecDeque<(u64, u64)>,
+    data: Option<Arc<ColumnData>>,
 }
 
-impl<'a, I> Iterator for ArrayIter<'a, I>
+impl<I> PageArrays<I>
+where
+    I: Iterator<Item = Result<(u64, Vec<u8>)>> + PageIterator,
+{
+    fn load(&mut self, reader: &mut I) -> Result<()> {
+        let (mut bytes, mut metas, mut rows) = (Vec::new(), Vec::new(), Vec::new());
+        while let Some(page) = reader.next() {
+            let (num_values, mut buf) = page?;
+            rows.push(if self.is_nested { nested_page_rows(&buf)? } else { num_values });
+            metas.push(PageMeta { length: buf.len() as u64, num_values });
+            bytes.extend_from_slice(&buf);
+            reader.swap_buffer(&mut buf);  // the page buffer back to the reader for reuse
+        }
+        if metas.is_empty() {
+            return Ok(());
+        }
+        let data = decode_host_chunk(&bytes, &metas, &self.field)?;
+        let mut first = 0u64;
+        for r in rows {
+            self.pages.push_back((first, r));
+            first += r;
+        }
+        if first != data.rows() {
+            return Err(Error::OutOfSpec(format!("pages hold {first} rows, the decoded column {}", data.rows())));
+        }
+        self.data = Some(Arc::new(data));
+        Ok(())
+    }
+}
+
+impl<I> Iterator for PageArrays<I>
 where
     I: Iterator<Item = Result<(u64, Vec<u8>)>> + PageIterator,
 {
     type Item = Result<Array>;
 
     fn next(&mut self) -> Option<Self::Item> {
-        let (num_values, mut page) = match self.reader.next()? {
-            Ok(p) => p,
-            Err(e) => return Some(Err(e)),
-        };
-        let out = (|| {
-            let chunk = self.ctx.upload(&page)?;
-            let meta = PageMeta { length: page.len() as u64, num_values };
-            decode_chunk(self.ctx, &chunk, &[meta], &self.field)
-        })();
-        self.reader.swap_buffer(&mut page);  // the page buffer back to the reader for reuse
-        Some(out)
+        if let Some(mut reader) = self.reader.take() {
+            if let Err(e) = self.load(&mut reader) {
+                self.pages.clear();
+                return Some(Err(e));
+            }
+        }
+        let (offset, len) = self.pages.pop_front()?;
+        let data = self.data.as_ref()?.clone();
+        Some(Ok(Array { data_type: self.field.data_type.clone(), data, offset, len }))
     }
 }
 
-/// `column_iter_to_arrays` (src/read/deserialize.rs:237-253).
-pub fn column_iter_to_arrays<'a, I>(
-    ctx: &'a Context,
+/// `column_iter_to_arrays` (src/read/deserialize.rs:237-253): one array per
+/// page of the column.
+pub fn column_iter_to_arrays<'a, I: 'a>(
     mut readers: Vec<I>,
     leaves: Vec<ColumnDescriptor>,
     field: Field,
     is_nested: bool,
-) -> Result<ArrayIter<'a, I>>
+) -> Result<ArrayIter<'a>>
 where
-    I: Iterator<Item = Result<(u64, Vec<u8>)>> + PageIterator + 'a,
+    I: Iterator<Item = Result<(u64, Vec<u8>)>> + PageIterator + Send + Sync,
 {
     one_leaf(&leaves, &field)?;
-    if is_nested != matches!(field.data_type, DataType::List(_) | DataType::LargeList(_)) {
-        return Err(Error::Argument(format!("{}: is_nested {is_nested} against its data type", field.name)));
-    }
+    check_nested(is_nested, &field)?;
     let reader = readers.pop().ok_or_else(|| Error::Argument("no reader".into()))?;
-    Ok(ArrayIter { ctx, reader, field })
+    Ok(Box::new(PageArrays { reader: Some(reader), field, is_nested, pages: VecDeque::new(), data: None }))
+}
+
+/// `compression::Compression` (src/compression/mod.rs:37-108).
+#[derive(Debug, Clone, Copy, PartialEq, Eq, Hash, Default)]
+pub enum Compression {
+    #[default]
+    None,
+    Lz4,
+    Zstd,
+    Snappy,
+    Rle,
+    Dict,
+    OneValue,
+    Freq,
+    Bitpacking,
+    DeltaBitpacking,
+    Patas,
+}
+
+impl From<Compression> for u8 {
+    fn from(value: Compression) -> Self {
+        match value {
+            Compression::None => 0,
+            Compression::Lz4 => 1,
+            Compression::Zstd => 2,
+            Compression::Snappy => 3,
+            Compression::Rle => 10,
+            Compression::Dict => 11,
+            Compression::OneValue => 12,
+            Compression::Freq => 13,
+            Compression::Bitpacking => 14,
+            Compression::DeltaBitpacking => 15,
+            Compression::Patas => 16,
+        }
+    }
+}
+
+/// `compression::basic::CommonCompression` (src/compression/basic.rs:23-60).
+#[derive(Debug, Clone, Copy, PartialEq, Eq, Hash, Default)]
+pub enum CommonCompression {
+    #[default]
+    None,
+    Lz4,
+    Zstd,
+    Snappy,
+}
+
+impl CommonCompression {
+    pub fn to_compression(&self) -> Compression {
+        match self {
+            Self::None => Compression::None,
+            Self::Lz4 => Compression::Lz4,
+            Self::Zstd => Compression::Zstd,
+            Self::Snappy => Compression::Snappy,
+        }
+    }
+}
+
+/// `write::WriteOptions` (src/write/common.rs:37-45).
+#[derive(Debug, Clone, PartialEq, Default)]
+pub struct WriteOptions {
+    pub default_compression: CommonCompression,
+    pub default_compress_ratio: Option<f64>,
+    pub max_page_size: Option<usize>,
+    pub forbidden_compressions: Vec<Compression>,
+}
+
+/// util/env.rs's debug-build codec overrides, in choose_compressor's order
+/// (compression/integer/mod.rs:236-266, double/mod.rs:236-268): the first
+/// one set to "1" whose codec is not forbidden becomes the engine's forced
+/// codec (one per column; the reference re-checks them in each nested call).
+fn forced_from_env(forbidden: &[Compression]) -> Option<i32> {
+    if !cfg!(debug_assertions) {
+        return None;
+    }
+    const ENV: [(&str, Compression); 5] = [
+        ("STRAWBOAT_FREQ_COMPRESSION", Compression::Freq),
+        ("STRAWBOAT_DICT_COMPRESSION", Compression::Dict),
+        ("STRAWBOAT_RLE_COMPRESSION", Compression::Rle),
+        ("STRAWBOAT_BITPACK_COMPRESSION", Compression::Bitpacking),
+        ("STRAWBOAT_PATAS_COMPRESSION", Compression::Patas),
+    ];
+    ENV.iter()
+        .find(|(var, c)| std::env::var(var).map_or(false, |v| v == "1") && !forbidden.contains(c))
+        .map(|(_, c)| u8::from(*c) as i32)
+}
+
+impl WriteOptions {
+    fn engine(&self) -> crate::WriteOptions {
+        let mut forbidden_mask = 0u32;
+        for c in &self.forbidden_compressions {
+            forbidden_mask |= 1u32 << u8::from(*c);
+        }
+        crate::WriteOptions {
+            default_codec: u8::from(self.default_compression.to_compression()) as i32,
+            default_compress_ratio: self.default_compress_ratio,
+            max_page_size: self.max_page_size.map(|p| p as u64),
+            forbidden_mask,
+            forced_codec: forced_from_env(&self.forbidden_compressions),
+            seed: 0,
+        }
+    }
 }
 
 /// arrow2 `Schema` for the writer: the fields and arrow2's
@@ -352,6 +613,8 @@ enum State {
     Started,
     Written,
     Finished,
+    /// a write of the chunk's bytes failed part way: the file is unusable
+    Failed,
 }
 
 /// `write::writer::NativeWriter` (src/write/writer.rs:42-173): magic, one
@@ -387,13 +650,24 @@ impl<W: Write> NativeWriter<W> {
     }
 
     fn put(&mut self, b: &[u8]) -> Result<()> {
-        self.writer.write_all(b).map_err(io)?;
+        if let Err(e) = self.writer.write_all(b) {
+            self.state = State::Failed;
+            return Err(io(e));
+        }
         self.offset += b.len() as u64;
+        Ok(())
+    }
+
+    fn check_not_failed(&self) -> Result<()> {
+        if self.state == State::Failed {
+            return Err(Error::Io("an earlier write to the strawboat file failed".into()));
+        }
         Ok(())
     }
 
     /// "ARROW2" + two zero bytes (writer.rs:91-103); once only.
     pub fn start(&mut self) -> Result<()> {
+        self.check_not_failed()?;
         if self.state != State::None {
             return Err(Error::OutOfSpec("The strawboat file can only be started once".into()));
         }
@@ -404,7 +678,10 @@ impl<W: Write> NativeWriter<W> {
 
     /// The chunk's columns, each paged and encoded by the engine's writer
     /// (write/common.rs:49-119); one chunk per file (writer.rs:106-123).
+    /// Every column is encoded before any byte is written, so a column that
+    /// fails to encode leaves the writer as it was.
     pub fn write(&mut self, chunk: &Chunk) -> Result<()> {
+        self.check_not_failed()?;
         if self.state == State::Written {
             return Err(Error::OutOfSpec("The strawboat file can only accept one RowGroup in a single file".into()));
         }
@@ -416,9 +693,13 @@ impl<W: Write> NativeWriter<W> {
         if chunk.arrays.len() != self.schema.fields.len() {
             return Err(Error::Argument("the chunk's arrays differ from the schema's fields".into()));
         }
-        let fields = self.schema.fields.clone();
-        for (a, f) in chunk.arrays.iter().zip(fields.iter()) {
-            let (bytes, pages) = encode_array(a, f, &self.options)?;
+        let encoded = chunk
+            .arrays
+            .iter()
+            .zip(self.schema.fields.iter())
+            .map(|(a, f)| encode_array(a, f, &self.options))
+            .collect::<Result<Vec<_>>>()?;
+        for (bytes, pages) in encoded {
             let offset = self.offset;
             self.put(&bytes)?;
             self.metas.push(ColumnMeta { offset, pages });
@@ -429,6 +710,7 @@ impl<W: Write> NativeWriter<W> {
 
     /// Footer: schema, column metas, sizes, EOS (writer.rs:128-167).
     pub fn finish(&mut self) -> Result<()> {
+        self.check_not_failed()?;
         if self.state != State::Written {
             return Err(Error::OutOfSpec(
                 "The strawboat file must be written before it can be finished. Call `start` before `finish`".into(),
@@ -436,7 +718,10 @@ impl<W: Write> NativeWriter<W> {
         }
         let footer = crate::write_footer(&self.schema.ipc_bytes, &self.metas)?;
         self.put(&footer)?;
-        self.writer.flush().map_err(io)?;
+        if let Err(e) = self.writer.flush() {
+            self.state = State::Failed;
+            return Err(io(e));
+        }
         self.state = State::Finished;
         Ok(())
     }
@@ -446,33 +731,99 @@ impl<W: Write> NativeWriter<W> {
     }
 }
 
+fn bitmap_len(n: u64) -> u64 {
+    (n + 7) / 8
+}
+
+fn arg(msg: String) -> Error {
+    Error::Argument(msg)
+}
+
+/// An optional LSB bitmap must hold n bits.
+fn check_bitmap(b: &Option<Vec<u8>>, n: u64, what: &str) -> Result<()> {
+    match b {
+        Some(v) if (v.len() as u64) < bitmap_len(n) => {
+            Err(arg(format!("{what} bitmap holds {} bytes, {n} rows need {}", v.len(), bitmap_len(n))))
+        }
+        _ => Ok(()),
+    }
+}
+
+/// n values of `ty` (Boolean: an n-bit bitmap).
+fn check_values(v: &[u8], n: u64, ty: PhysicalType) -> Result<()> {
+    let need = if ty == PhysicalType::Boolean {
+        bitmap_len(n)
+    } else {
+        n.checked_mul(ty.width() as u64).ok_or_else(|| arg(format!("{n} rows overflow the values size")))?
+    };
+    if (v.len() as u64) < need {
+        return Err(arg(format!("values hold {} bytes, {n} rows of {ty:?} need {need}", v.len())));
+    }
+    Ok(())
+}
+
+/// n + 1 offsets, non-decreasing from >= 0, the last at most `limit`.
+fn check_offsets(offsets: &[i64], n: u64, limit: u64) -> Result<()> {
+    let want = n.checked_add(1).ok_or_else(|| arg("row count overflows".into()))?;
+    if offsets.len() as u64 != want {
+        return Err(arg(format!("{} offsets for {n} rows", offsets.len())));
+    }
+    if offsets[0] < 0 || offsets.windows(2).any(|w| w[1] < w[0]) {
+        return Err(arg("offsets must be non-negative and non-decreasing".into()));
+    }
+    let last = offsets[offsets.len() - 1] as u64;
+    if last > limit {
+        return Err(arg(format!("last offset {last} past the {limit} values")));
+    }
+    Ok(())
+}
+
 /// One column through sb_encode_column / sb_encode_binary_column /
 /// sb_encode_list_column (the host writer, every codec of the cascade).
+/// The buffers are checked against `len` first: the C encoder reads exactly
+/// what the lengths and offsets promise.
 fn encode_array(a: &HostArray, f: &Field, o: &WriteOptions) -> Result<(Vec<u8>, Vec<PageMeta>)> {
     let (ty, lists, _, leaf_nullable) = leaf_path(f)?;
-    let opts = o.raw();
-    let page = o.max_page_size.unwrap_or(0);
+    let eo = o.engine();
+    let opts = eo.raw();
+    let page = eo.max_page_size.unwrap_or(0);
     let mut out: *mut u8 = ptr::null_mut();
     let mut len = 0u64;
     let mut metas: *mut PageMeta = ptr::null_mut();
     let mut np = 0u64;
     let bm = |v: &Option<Vec<u8>>| v.as_ref().map_or(ptr::null(), |b| b.as_ptr());
     let st = match a {
-        HostArray::Primitive { values, validity, len: n } if lists.is_empty() && !ty.is_binary() => unsafe {
-            ffi::sb_encode_column(ty as i32, values.as_ptr() as *const c_void, bm(validity), *n, f.is_nullable as i32,
-                                  &opts, page, 0, &mut out, &mut len, &mut metas, &mut np)
-        },
-        HostArray::Binary { values, offsets, validity, len: n } if lists.is_empty() && ty.is_binary() => unsafe {
-            ffi::sb_encode_binary_column(ty as i32, values.as_ptr(), values.len() as u64, offsets.as_ptr(), bm(validity),
-                                         *n, f.is_nullable as i32, &opts, page, 0, &mut out, &mut len, &mut metas,
-                                         &mut np)
-        },
+        HostArray::Primitive { values, validity, len: n } if lists.is_empty() && !ty.is_binary() => {
+            check_values(values, *n, ty)?;
+            check_bitmap(validity, *n, "validity")?;
+            unsafe {
+                ffi::sb_encode_column(ty as i32, values.as_ptr() as *const c_void, bm(validity), *n,
+                                      f.is_nullable as i32, &opts, page, 0, &mut out, &mut len, &mut metas, &mut np)
+            }
+        }
+        HostArray::Binary { values, offsets, validity, len: n } if lists.is_empty() && ty.is_binary() => {
+            check_offsets(offsets, *n, values.len() as u64)?;
+            check_bitmap(validity, *n, "validity")?;
+            unsafe {
+                ffi::sb_encode_binary_column(ty as i32, values.as_ptr(), values.len() as u64, offsets.as_ptr(),
+                                             bm(validity), *n, f.is_nullable as i32, &opts, page, 0, &mut out,
+                                             &mut len, &mut metas, &mut np)
+            }
+        }
         HostArray::List { offsets, validity, values, child_validity, len: n }
-            if lists.len() == 1 && !ty.is_binary() && ty != PhysicalType::Boolean => unsafe {
-            ffi::sb_encode_list_column(ty as i32, offsets.as_ptr(), bm(validity), lists[0] as i32,
-                                       values.as_ptr() as *const c_void, bm(child_validity), leaf_nullable as i32, *n,
-                                       &opts, page, 0, &mut out, &mut len, &mut metas, &mut np)
-        },
+            if lists.len() == 1 && !ty.is_binary() && ty != PhysicalType::Boolean =>
+        {
+            let children = values.len() as u64 / ty.width() as u64;
+            check_offsets(offsets, *n, children)?;
+            check_bitmap(validity, *n, "list validity")?;
+            check_bitmap(child_validity, offsets[offsets.len() - 1] as u64, "item validity")?;
+            unsafe {
+                ffi::sb_encode_list_column(ty as i32, offsets.as_ptr(), bm(validity), lists[0] as i32,
+                                           values.as_ptr() as *const c_void, bm(child_validity),
+                                           leaf_nullable as i32, *n, &opts, page, 0, &mut out, &mut len, &mut metas,
+                                           &mut np)
+            }
+        }
         _ => return Err(Error::NotYetImplemented(format!("{}: no writer path for this array / field", f.name))),
     };
     status(st, || format!("encoding {}", f.name))?;
@@ -488,7 +839,6 @@ fn encode_array(a: &HostArray, f: &Field, o: &WriteOptions) -> Result<(Vec<u8>, 
 #[cfg(test)]
 mod tests {
     use super::*;
-    use std::io::Cursor;
 
     fn metas() -> Vec<PageMeta> {
         vec![PageMeta { length: 3, num_values: 10 }, PageMeta { length: 2, num_values: 7 }, PageMeta { length: 4, num_values: 1 }]
@@ -509,6 +859,15 @@ mod tests {
     }
 
     #[test]
+    fn native_read_buf_peeks() {
+        let mut c = Cursor::new(b"abcdef".to_vec());
+        c.set_position(2);
+        assert_eq!(c.buffer_bytes(), b"cdef");
+        let s: &[u8] = b"xyz";
+        assert_eq!(s.buffer_bytes(), b"xyz");
+    }
+
+    #[test]
     fn leaf_paths() {
         let f = Field::new("l", DataType::List(Box::new(Field::new("item", DataType::Int32, true))), false);
         assert_eq!(leaf_path(&f).unwrap(), (PhysicalType::Int32, vec![false], vec![false], true));
@@ -522,5 +881,42 @@ mod tests {
         w.start().unwrap();
         assert!(w.start().is_err());
         assert_eq!(w.total_size(), 8);
+    }
+
+    #[test]
+    fn malformed_host_arrays_are_argument_errors() {
+        let f = Field::new("x", DataType::Int32, true);
+        let o = WriteOptions::default();
+        let short = HostArray::Primitive { values: vec![0; 7], validity: None, len: 2 };
+        assert!(matches!(encode_array(&short, &f, &o), Err(Error::Argument(_))));
+        let bad_bitmap = HostArray::Primitive { values: vec![0; 40], validity: Some(vec![0xFF]), len: 10 };
+        assert!(matches!(encode_array(&bad_bitmap, &f, &o), Err(Error::Argument(_))));
+        let s = Field::new("s", DataType::Utf8, false);
+        let past = HostArray::Binary { values: b"ab".to_vec(), offsets: vec![0, 1, 3], validity: None, len: 2 };
+        assert!(matches!(encode_array(&past, &s, &o), Err(Error::Argument(_))));
+        let down = HostArray::Binary { values: b"ab".to_vec(), offsets: vec![0, 2, 1], validity: None, len: 2 };
+        assert!(matches!(encode_array(&down, &s, &o), Err(Error::Argument(_))));
+    }
+
+    #[test]
+    fn options_map_onto_the_engine() {
+        let o = WriteOptions {
+            default_compression: CommonCompression::Lz4,
+            default_compress_ratio: Some(2.0),
+            max_page_size: Some(8192),
+            forbidden_compressions: vec![Compression::Dict, Compression::Freq],
+        };
+        let e = o.engine();
+        assert_eq!(e.default_codec, 1);
+        assert_eq!(e.forbidden_mask, (1 << 11) | (1 << 13));
+        assert_eq!(e.max_page_size, Some(8192));
+    }
+
+    fn assert_send_sync<T: Send + Sync>() {}
+
+    #[test]
+    fn arrays_and_iterators_cross_threads() {
+        assert_send_sync::<Array>();
+        assert_send_sync::<ArrayIter<'static>>();
     }
 }

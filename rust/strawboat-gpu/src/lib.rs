@@ -183,6 +183,12 @@ impl Drop for DeviceBuffer {
     }
 }
 
+// A device allocation is a plain handle: any thread may read it through
+// `&self` (copies out) or free it (hipFree is not tied to a thread), so
+// decoded columns can be shared the way arrow2 shares its buffers.
+unsafe impl Send for DeviceBuffer {}
+unsafe impl Sync for DeviceBuffer {}
+
 /// One device + one HIP stream (`sb_ctx`); not `Sync`, like the reference's
 /// single-consumer readers (src/read/reader.rs:51).
 pub struct Context {

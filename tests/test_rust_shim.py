@@ -48,7 +48,8 @@ def test_rust_ffi_symbols_exported():
 COMPAT = os.path.join(ROOT, "rust", "strawboat-gpu", "src", "compat.rs")
 
 # The reference's signatures (b41sh/pa 0.2.6), parameter names in order:
-# the shim keeps them and puts the engine Context first.
+# the shim keeps them exactly (no engine context argument: the calling
+# thread's default context decodes).
 REFERENCE_SIGNATURES = {
     # src/read/reader.rs:60
     "new(page_reader": ["page_reader", "page_metas", "scratch"],
@@ -59,9 +60,22 @@ REFERENCE_SIGNATURES = {
     # src/write/writer.rs:59
     "try_new": ["writer", "schema", "options"],
 }
-# src/read/reader.rs:69-145, read/mod.rs:55-57, write/writer.rs:66-173
-REFERENCE_METHODS = ["has_next", "current_page", "skip_page", "swap_buffer", "next", "nth", "into_inner", "start",
-                     "write", "finish", "total_size"]
+# The generic bounds those functions carry in the reference.
+REFERENCE_BOUNDS = [
+    "pub fn batch_read_array<R: NativeReadBuf>(",                       # batch_read.rs:190
+    "pub fn column_iter_to_arrays<'a, I: 'a>(",                         # deserialize.rs:237
+    "I: Iterator<Item = Result<(u64, Vec<u8>)>> + PageIterator + Send + Sync,",  # deserialize.rs:243
+    "pub struct NativeReader<R: NativeReadBuf>",                        # reader.rs:51
+    "impl<R: NativeReadBuf + Seek> Iterator for NativeReader<R>",       # reader.rs:87
+    "pub trait NativeReadBuf: BufRead",                                 # read/mod.rs:26
+    "pub type ArrayIter<'a> = Box<dyn Iterator<Item = Result<Array>> + Send + Sync + 'a>;",
+]
+# src/write/common.rs:37-45
+WRITE_OPTIONS_FIELDS = ["default_compression: CommonCompression", "default_compress_ratio: Option<f64>",
+                        "max_page_size: Option<usize>", "forbidden_compressions: Vec<Compression>"]
+# src/read/reader.rs:69-145, read/mod.rs:26-57, write/writer.rs:66-173
+REFERENCE_METHODS = ["has_next", "current_page", "skip_page", "swap_buffer", "buffer_bytes", "next", "nth",
+                     "into_inner", "start", "write", "finish", "total_size"]
 
 
 def _params(src, head):
@@ -80,13 +94,26 @@ def _params(src, head):
 def test_rust_compat_keeps_the_reference_signatures():
     src = open(COMPAT).read()
     for head, names in REFERENCE_SIGNATURES.items():
-        got = _params(src, head)
-        if got and got[0] == "ctx":
-            got = got[1:]
-        assert got == names, (head, got)
+        assert _params(src, head) == names, (head, _params(src, head))
+    for b in REFERENCE_BOUNDS:
+        assert b in src, b
+    for f in WRITE_OPTIONS_FIELDS:
+        assert "pub " + f in src, f
     for m in REFERENCE_METHODS:
         assert re.search(r"\bfn %s\b" % m, src), m
-    assert "pub struct NativeReader<R: Read + Seek>" in src and "pub struct NativeWriter<W: Write>" in src
+    assert "pub struct NativeWriter<W: Write>" in src
     assert "pub trait PageIterator" in src
+    # no public entry point of the drop-in surface takes an engine context
+    assert not re.search(r"pub fn \w+[^(]*\([^)]*ctx\s*:", src)
     lib = open(os.path.join(ROOT, "rust", "strawboat-gpu", "src", "lib.rs")).read()
     assert "pub mod compat;" in lib
+
+
+def test_rust_compat_checks_host_buffers_before_ffi():
+    """encode_array validates lengths, bitmaps and offsets before the unsafe
+    calls into the C encoder."""
+    src = open(COMPAT).read()
+    body = src[src.index("fn encode_array"):]
+    for call in ("sb_encode_column(", "sb_encode_binary_column(", "sb_encode_list_column("):
+        head = body[:body.index(call)]
+        assert "check_" in head[head.rfind("=>"):], call
