@@ -71,6 +71,7 @@ struct sb_plan {
   uint8_t* d_scratch = nullptr;      // binary: expanded offsets streams
   uint8_t* d_region = nullptr;       // fixed width: the pages' HBM regions (PageDesc.reserved)
   uint32_t* d_spill = nullptr;       // [2] spilled-leaf job counts (by decode parity)
+  uint32_t* d_sched = nullptr;       // [2] k_inflate's job claim counters (zero between launches)
   sb::InflateJob* d_spill_jobs = nullptr;
   uint32_t n_spill = 0;              // pages with a spill area (bounds the spill launches)
   uint32_t n_big = 0;                // binary: big Extend pages (tables in d_region)
@@ -209,6 +210,7 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_scratch) (void)hipFree(p->d_scratch);
   if (p->d_region) (void)hipFree(p->d_region);
   if (p->d_spill) (void)hipFree(p->d_spill);
+  if (p->d_sched) (void)hipFree(p->d_sched);
   if (p->d_spill_jobs) (void)hipFree(p->d_spill_jobs);
   if (p->d_bin) (void)hipFree(p->d_bin);
   if (p->d_lb) (void)hipFree(p->d_lb);
@@ -432,6 +434,8 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
   if (e == hipSuccess) e = hipMalloc(&p->d_defer, (np + 4) * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemsetAsync(p->d_defer, 0, 4 * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipMalloc(&p->d_jobs, (owidth ? 2 : 1) * np * sizeof(sb::InflateJob));
+  if (e == hipSuccess) e = hipMalloc(&p->d_sched, 2 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(p->d_sched, 0, 2 * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipEventCreate(&p->ev0);
   if (e == hipSuccess) e = hipEventCreate(&p->ev1);
   if (e == hipSuccess && n_pages) {
@@ -616,7 +620,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
                   p->bin_grid, p->d_region, nullptr, p->n_big};
   if (p->n_bin_jobs) {  // Basic LZ4 / Snappy pages: streams expanded first, one wave each
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2, p->n_bin_jobs, out->d_values, p->d_scratch,
-                        p->d_bin + np, p->d_status, (uint8_t*)out->d_offsets};
+                        p->d_bin + np, p->d_status, (uint8_t*)out->d_offsets, p->d_sched};
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))
@@ -697,7 +701,7 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
   if (p->inflate_state != 0 && p->n_pages) {
     // CH_LEAF LZ4 / Snappy pages listed by the pass above: values straight into the column
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2 + a.parity, (uint32_t)p->n_pages,
-                        (uint8_t*)out->d_values, nullptr, nullptr, p->d_status};
+                        (uint8_t*)out->d_values, nullptr, nullptr, p->d_status, nullptr, p->d_sched};
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))
@@ -714,7 +718,7 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
       // leaves the deferred pass could not hold in LDS: expanded into the
       // pages' regions (one wave per stream), then the pages decoded from there
       sb::InflateLaunch I{p->d_chunk, p->d_spill_jobs, p->d_spill + a.parity, p->n_spill, nullptr, p->d_region,
-                          nullptr, p->d_status};
+                          nullptr, p->d_status, nullptr, p->d_sched};
       if (sb::launch_inflate(I, ctx->stream) || sb::launch_zinflate(I, ctx->stream))
         return fail(ctx, SB_E_DEVICE, "spill inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
       a.n_list = p->n_spill;

@@ -21,6 +21,9 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "sb_internal.h"
@@ -1579,19 +1582,19 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     // straddling farlim goes byte by byte.
     const bool mfar = src + s.ml <= farlim, mnear = src >= farlim;
     const bool fw = freel && (mfar || mnear);
+    const uint32_t fa = mfar ? src + o.dal : src, fsh = fa & 3, fa0 = fa - fsh, fneed = fw ? fsh + s.ml : 0u;
     if (__ballot(fw)) {
       constexpr uint32_t NW = kMatchFast / 4 + 1;
-      const uint32_t a = mfar ? src + o.dal : src, sh = a & 3, a0 = a - sh, need = fw ? sh + s.ml : 0u;
       uint32_t w[NW];
 #pragma unroll
       for (uint32_t t = 0; t < NW; t++) {
         w[t] = 0;
-        if (!__ballot(4 * t < need)) continue;
-        const uint32_t g = o.far32(a0 + 4 * t, mfar && 4 * t < need);
-        const uint32_t r = r32[((a0 + 4 * t) & (kRing - 1)) >> 2];
+        if (!__ballot(4 * t < fneed)) continue;
+        const uint32_t g = o.far32(fa0 + 4 * t, mfar && 4 * t < fneed);
+        const uint32_t r = r32[((fa0 + 4 * t) & (kRing - 1)) >> 2];
         w[t] = mfar ? g : r;
       }
-      if (fw) ring_put<NW>(o.ring, dm, s.ml, sh, w);
+      if (fw) ring_put<NW>(o.ring, dm, s.ml, fsh, w);
     }
     const bool fmix = freel && !mfar && !mnear;
     for (uint32_t i = 0; __ballot(fmix && i < s.ml); i++) {
@@ -2463,7 +2466,20 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = a.count ? *a.count : a.n_jobs;
-  for (uint32_t j = blockIdx.x * kInfWaves + wv; j < n; j += gridDim.x * kInfWaves) {
+  // Jobs are claimed from a counter (a.sched[0]) as waves free up, so the
+  // last wave slots do not idle behind a fixed job-to-wave assignment; the
+  // last wave out (a.sched[1] counts them) zeroes both words for the next
+  // launch on the stream.  Without a.sched: grid-strided.
+  uint32_t j = blockIdx.x * kInfWaves + wv;
+  for (bool first = true;; first = false) {
+    if (a.sched) {
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(&a.sched[0], 1u);
+      j = __builtin_amdgcn_readfirstlane(c);  // (every lane is active here: lane 0's claim, in an SGPR)
+    } else if (!first) {
+      j += gridDim.x * kInfWaves;
+    }
+    if (j >= n) break;
     const InflateJob jb = a.jobs[j];
     if (jb.codec == 2) continue;  // k_zinflate's
     const uint64_t kind = jb.dst >> 62, off = jb.dst & kDstMask;
@@ -2510,6 +2526,10 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
     }
 #endif
     if (st && lane == 0) a.status[jb.page] = st;
+  }
+  if (a.sched && lane == 0 && atomicAdd(&a.sched[1], 1u) == gridDim.x * kInfWaves - 1) {
+    a.sched[0] = 0;  // every wave has claimed its last job: reset for the next launch
+    a.sched[1] = 0;
   }
 }
 
@@ -5178,10 +5198,38 @@ extern "C" int sb_debug_bin_phases(uint64_t* host, uint64_t n) {
 #endif
 
 namespace sb {
+// Workgroups of k_inflate resident on the whole device at once (one query per device).
+static uint32_t inflate_resident() {
+  static std::mutex mu;
+  static std::map<int, uint32_t> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)sbk::k_inflate, 64 * sbk::kInfWaves, 0) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 || cus <= 0)
+    per_cu = 0;
+  // (the API has reported 8 a CU for this kernel; its launch bounds allow SB_INF_BLOCKS)
+  const uint32_t r = per_cu ? (uint32_t)(std::min(per_cu, SB_INF_BLOCKS) * cus) : kInflateGrid;
+  cache[dev] = r;
+  return r;
+}
+extern "C" uint32_t sb_debug_inflate_resident() { return inflate_resident(); }
 int launch_inflate(const InflateLaunch& a, void* stream) {
   if (a.n_jobs == 0) return 0;
-  const uint32_t grid = std::min<uint32_t>((a.n_jobs + sbk::kInfWaves - 1) / sbk::kInfWaves, kInflateGrid);
-  hipLaunchKernelGGL(sbk::k_inflate, dim3(grid), dim3(64 * sbk::kInfWaves), 0, (hipStream_t)stream, a);
+  // A/B switches: SB_INF_STATIC=1 grid-strides the jobs, SB_INF_GRID=n caps the grid
+  static const bool stat = getenv("SB_INF_STATIC") != nullptr;
+  static const uint32_t gcap = getenv("SB_INF_GRID") ? (uint32_t)atoi(getenv("SB_INF_GRID")) : 0u;
+  InflateLaunch b = a;
+  if (stat) b.sched = nullptr;
+  // claimed jobs: no more workgroups than fit at once (later ones would find none)
+  uint32_t cap = b.sched ? std::min<uint32_t>(inflate_resident(), kInflateGrid) : kInflateGrid;
+  if (gcap) cap = gcap;
+  const uint32_t grid = std::min<uint32_t>((a.n_jobs + sbk::kInfWaves - 1) / sbk::kInfWaves, cap);
+  hipLaunchKernelGGL(sbk::k_inflate, dim3(grid), dim3(64 * sbk::kInfWaves), 0, (hipStream_t)stream, b);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_zinflate(const InflateLaunch& a, void* stream) {

@@ -99,6 +99,7 @@ struct InflateLaunch {
   const uint64_t* bases;
   uint32_t* status;
   uint8_t* offs;  // kDstBinOffs jobs: the column's 32-bit offsets (dword-aligned)
+  uint32_t* sched;  // k_inflate's job claim counters [2], zero between launches (self-resetting), or nullptr
 };
 int launch_inflate(const InflateLaunch& a, void* stream);
 // Zstd jobs (codec 2) of the same list: one wave per frame, tables in LDS, output in HBM.

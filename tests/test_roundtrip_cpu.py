@@ -122,3 +122,56 @@ def test_encoder_matches_oracle_encoder():
                                                               seed=pa_amd.page_seed(11, i)))
                         assert chunk[pos:pos + m.length] == ob, (np.dtype(dt).name, kind, nullable, ratio, forced, i)
                         pos += m.length
+
+
+@pytest.mark.parametrize("P", [70_000, 300_000])
+def test_encoder_matches_oracle_encoder_big_pages(P):
+    """Pages past 65 535 rows: the product writer's 64-bit statistics table
+    words and multi-container roaring bitmaps (roaring 0.10.1 serialize_into)
+    against the oracle restatement, byte for byte.  The device encoder is
+    pinned to the product writer at these sizes (test_gpu_encode.py), so
+    this closes the chain to the restatement."""
+    from tests.colgen import gen_values
+
+    rng = np.random.default_rng(P)
+    n = P + P // 3  # a full page and a short one
+    cases = [(np.int32, "freq"), (np.int64, "freq"), (np.int32, "index"), (np.float64, "freq"), (np.uint32, "runs"),
+             (np.int32, "sorted"), (np.float64, "index")]
+    for dt, kind in cases:
+        v = gen_values(kind, n, dt, rng)
+        for nullable in (False, True):
+            val = rng.random(n) > 0.1 if nullable else None
+            for ratio, forced in [(1.2, -1), (2.0, O.FREQ), (2.0, O.DICT)]:
+                wo = pa_amd.WriteOptions(default_compress_ratio=ratio, max_page_size=P, forced_codec=forced, seed=5)
+                chunk, metas = pa_amd.encode_column(v, val, nullable, wo)
+                pos = 0
+                for i, m in enumerate(metas):
+                    sl = slice(i * P, i * P + m.num_values)
+                    ob = O.write_page(v[sl], None if val is None else val[sl], nullable,
+                                      O.WriteOptions.make(ratio=ratio, forced=forced, seed=pa_amd.page_seed(5, i)))
+                    assert chunk[pos:pos + m.length] == ob, (np.dtype(dt).name, kind, nullable, ratio, forced, i)
+                    pos += m.length
+
+
+def test_binary_encoder_matches_oracle_encoder_big_pages():
+    """Utf8 pages past 65 535 rows (Freq with several roaring containers,
+    Dict, adaptive) against the oracle's binary writer."""
+    rng = np.random.default_rng(9)
+    P = 140_000
+    n = P + 1000
+    pool = [f"v{i}".encode() for i in range(300)]
+    strs = [b"common" if r < 0.93 else pool[i] for r, i in zip(rng.random(n), rng.integers(0, 300, n))]
+    vals, offs = pa_amd.binary.strings_to_arrow(strs)
+    valid = rng.random(n) > 0.1
+    for ratio, forced in [(2.0, O.FREQ), (2.0, O.DICT), (1.2, -1)]:
+        wo = pa_amd.WriteOptions(default_compress_ratio=ratio, max_page_size=P, forced_codec=forced, seed=3)
+        chunk, metas = pa_amd.encode_binary_column(vals, offs, valid, True, wo, physical_type=pa_amd.UTF8)
+        pos = 0
+        for i, m in enumerate(metas):
+            r0, r1 = i * P, i * P + m.num_values
+            po = offs[r0:r1 + 1] - offs[r0]
+            ob = O.write_binary_page(vals[offs[r0]:offs[r1]], po, valid[r0:r1], True,
+                                     O.WriteOptions.make(ratio=ratio, forced=forced, seed=pa_amd.page_seed(3, i)),
+                                     parent_values_len=len(vals))
+            assert chunk[pos:pos + m.length] == ob, (ratio, forced, i)
+            pos += m.length

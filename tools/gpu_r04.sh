@@ -1,0 +1,20 @@
+# Round-4 GPU session steps: bash tools/gpu_r04.sh <step> ...
+#   tests "<pytest -k expr>" <files...>  : pytest subset (-m gpu), log under gpurun_out/
+#   c3ab "<lib ...>" [rows]              : tools/c3bench.py per library (PA_AMD_LIB)
+#   phases [rows]                        : tools/infphases.py on pa_amd/variants/libsb_phases.so
+set -o pipefail
+mkdir -p gpurun_out
+step=$1; shift
+case $step in
+  tests)
+    k=$1; shift
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -k "$k" "$@" > gpurun_out/r04_tests.log 2>&1
+    rc=$?; tail -4 gpurun_out/r04_tests.log; exit $rc ;;
+  c3ab)
+    for L in $1; do
+      echo "== $L"
+      PA_AMD_LIB=$L timeout -k 10 200 python tools/c3bench.py ${2:-100000000} 2>&1 | grep -v amdgpu.ids || exit 1
+    done ;;
+  phases)
+    PA_AMD_LIB=pa_amd/variants/libsb_phases.so timeout -k 10 200 python tools/infphases.py ${1:-10000000} 2>&1 | grep -v amdgpu.ids ;;
+esac
