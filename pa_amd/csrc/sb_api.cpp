@@ -83,6 +83,7 @@ struct sb_plan {
   bool boolean = false;  // SB_T_BOOLEAN: values are a bitmap (k_bool_decode)
   bool list = false;     // List<primitive>: levels kernels + `inner` (the values streams as flat pages)
   bool nested = false;   // general nesting (sb_nested_desc): k_nest_walk + `inner`
+  bool list_walk = false;  // a List plan served by the general walk (level streams k_list cannot take)
   sb_nested_desc ndesc{};
   uint64_t* d_nest = nullptr;        // [counts n(D+1) | bases n(D+1) | totals D+1]
   std::vector<uint64_t> nest_totals;  // entries per level
@@ -831,6 +832,26 @@ sb_status sb_plan_list_column(sb_ctx* ctx, const sb_list_desc* d, const uint8_t*
     std::vector<uint64_t> exact(n_pages), peek(n_pages);
     (void)hipMemcpy(stv.data(), p->d_status, n_pages * 4, hipMemcpyDeviceToHost);
     (void)hipMemcpy(exact.data(), p->d_lc, n_pages * 8, hipMemcpyDeviceToHost);
+    if (std::find(stv.begin(), stv.end(), (uint32_t)sb::ST_NYI) != stv.end()) {
+      // a level stream with more hybrid runs than k_list's run table holds
+      // (writers other than the reference's mix RLE and bit-packed runs
+      // freely; parquet2's HybridRleDecoder takes any number): the general
+      // level walk (k_nest_walk, depth 1) decodes the same List
+      sb_plan_destroy(p);
+      sb_nested_desc nd{};
+      nd.physical_type = d->physical_type;
+      nd.depth = 1;
+      nd.list_nullable[0] = d->list_nullable;
+      nd.item_nullable = d->item_nullable;
+      nd.offset_width = d->offset_width;
+      sb_plan* w = nullptr;
+      const sb_status wst = sb_plan_nested_column(ctx, &nd, d_chunk, chunk_len, h_metas, n_pages, &w);
+      if (wst) return wst;
+      w->list_walk = true;
+      w->ldesc = *d;
+      *out = w;
+      return SB_OK;
+    }
     for (uint64_t i = 0; i < n_pages; i++) {
       if (stv[i]) {
         sb_plan_destroy(p);
@@ -857,6 +878,14 @@ uint64_t sb_plan_num_leaves(const sb_plan* p) { return p ? p->n_leaves : 0; }
 
 sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* p, const sb_list_out* out) {
   if (!ctx || !p || !out) return fail(ctx, SB_E_ARG, "null argument");
+  if (p->list_walk) {  // planned on the general walk: the same buffers as level 0 + the leaf
+    sb_nested_out no{};
+    no.d_offsets[0] = out->d_offsets;
+    no.d_validity[0] = out->d_list_validity;
+    no.d_values = out->d_values;
+    no.d_leaf_validity = out->d_leaf_validity;
+    return sb_decode_nested_planned(ctx, p, &no);
+  }
   if (!p->list) return fail(ctx, SB_E_ARG, "not a list plan");
   if (!out->d_offsets || (p->n_leaves && !out->d_values)) return fail(ctx, SB_E_ARG, "list output buffers are null");
   if (p->ldesc.list_nullable && p->n_rows && !out->d_list_validity) return fail(ctx, SB_E_ARG, "list validity is null");

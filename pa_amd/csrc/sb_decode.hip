@@ -1230,6 +1230,10 @@ __device__ __forceinline__ uint32_t lds_chain(lds_u8* tab, uint32_t t1) {
 }
 
 constexpr uint32_t kIb = 1024, kIbHalf = kIb / 2, kLitFast = 64, kMatchFast = 32;
+#ifndef SB_HAZ_WORD
+#define SB_HAZ_WORD 16
+#endif
+constexpr uint32_t kHazWord = SB_HAZ_WORD;  // hazards copied word-wise in rounds: at most this long
 constexpr uint32_t kChainTabs = 6;  // T1..T32: batches of up to 64 sequences
 constexpr uint32_t kChainEnd = 0xFE, kChainStop = 0xFF;  // chain sentinels (see cand_steps)
 
@@ -1522,7 +1526,6 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     Seq s{0, 0, 0, 0, 0};
     const bool v0 = lane < j;
     if (v0) seq_parse(in.ib, starts, s);
-    const uint32_t q = j ? __builtin_amdgcn_readlane(s.next, j - 1) : p;
     const uint32_t len = v0 ? s.lit + s.ml : 0u;
     const uint32_t incl = wave_incl_scan(len), excl = incl - len;
     const uint32_t cap = min(kChunk, olen - o.op);
@@ -1540,6 +1543,9 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     }
     INF_N(9, 1);
     INF_N(10, k);
+    // the batch's end: where the k-th sequence resumes the stream, and the output length
+    const uint32_t pnext = __builtin_amdgcn_readlane(s.next, k - 1);
+    const uint32_t nop = o.op + __builtin_amdgcn_readlane(incl, k - 1);
 #ifdef SB_V_NOCOPY
     const bool v = false;
 #else
@@ -1606,10 +1612,42 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     }
     INF_T(5);
     INF_N(11, __popcll(__ballot(hazard)));
+#ifndef SB_HAZ_SERIAL
+    // Hazards in rounds: the first pending hazard (destination D) is ready,
+    // and so is every pending word-copyable hazard whose source ends at or
+    // before D (every byte below D is final once the hazards before it are
+    // done; the round's destinations all lie at or past D, so its copies are
+    // independent).  A batch of Float64 pages holds ~8 hazards in ~3 rounds.
+    // Self-overlapping, long (> kHazWord) and far-sourced hazards go one at
+    // a time, in order, when they are the first pending.
+    const bool hword = hazard && s.ml <= kHazWord && s.off >= s.ml && src >= farlim;
+    const uint64_t wordm = __ballot(hword);
+    for (uint64_t hm = __ballot(hazard); hm;) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(hm);
+      const uint32_t D = __builtin_amdgcn_readlane(dm, l);
+      if ((wordm >> l) & 1) {
+        const bool rd = ((hm >> lane) & 1) && hword && (src + s.ml <= D || lane == l);
+        constexpr uint32_t NW = kHazWord / 4 + 1;
+        const uint32_t sh = src & 3, a0 = src - sh, need = rd ? sh + s.ml : 0u;
+        uint32_t w[NW];
+#pragma unroll
+        for (uint32_t t = 0; t < NW; t++) {
+          w[t] = 0;
+          if (!__ballot(4 * t < need)) continue;
+          w[t] = r32[((a0 + 4 * t) & (kRing - 1)) >> 2];
+        }
+        if (rd) ring_put<NW>(o.ring, dm, s.ml, sh, w);
+        hm &= ~__ballot(rd);
+        continue;
+      }
+      hm &= hm - 1;
+      const uint32_t O = __builtin_amdgcn_readlane(s.off, l), M = __builtin_amdgcn_readlane(s.ml, l);
+#else
     for (uint64_t hm = __ballot(hazard); hm; hm &= hm - 1) {
       const uint32_t l = (uint32_t)__builtin_ctzll(hm);
       const uint32_t D = __builtin_amdgcn_readlane(dm, l), O = __builtin_amdgcn_readlane(s.off, l),
                      M = __builtin_amdgcn_readlane(s.ml, l);
+#endif
       if (M <= 64 && O >= M && D - O >= farlim) {  // no self-overlap, source in the ring: one byte a lane
         if (lane < M) o.ring[(D + lane) & (kRing - 1)] = o.ring[(D - O + lane) & (kRing - 1)];
         continue;
@@ -1624,8 +1662,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
       }
     }
     INF_T(6);
-    const uint32_t nop = o.op + __builtin_amdgcn_readlane(incl, k - 1);
-    p = k == j ? q : __builtin_amdgcn_readlane(starts, k);
+    p = pnext;
     if ((nop / kChunk) != (o.op / kChunk)) o.flush(o.op & ~(kChunk - 1), kChunk);
     o.op = nop;
     INF_T(7);

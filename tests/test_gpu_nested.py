@@ -47,10 +47,10 @@ def nested_values(rng, depth, nulls, leaf_null, n):
     return pa.table({"c": pa.array([build(0) for _ in range(n)], type=f.type)}, schema=pa.schema([f]))
 
 
-def chunk_of(tmp_path, t, depth, nulls, leaf_null, opts):
+def chunk_of(tmp_path, t, depth, nulls, leaf_null, opts, page_size=4096):
     path = str(tmp_path / "n.parquet")
-    pq.write_table(t, path, data_page_version="2.0", compression="NONE", use_dictionary=False, data_page_size=4096,
-                   write_statistics=False)
+    pq.write_table(t, path, data_page_version="2.0", compression="NONE", use_dictionary=False,
+                   data_page_size=page_size, write_statistics=False)
     leaf_def = sum(int(x) + 1 for x in nulls)
     max_def = leaf_def + int(leaf_null)
     bw = max_def.bit_length()
@@ -161,3 +161,67 @@ def test_nested_utf8_bool_leaves(ctx, tmp_path, leaf, depth, codec):
             if leaf_null:
                 assert (pa_amd.read.unpack_bitmap(gf, nleaf).cpu().numpy() == ef).all()
             dec.close()
+
+
+def hybrid_runs(stream: bytes, bw: int) -> int:
+    """Run headers of a parquet RLE / bit-packed hybrid stream."""
+    p, runs = 0, 0
+    while p < len(stream):
+        h, sh = 0, 0
+        while True:
+            c = stream[p]
+            p += 1
+            h |= (c & 0x7F) << sh
+            sh += 7
+            if not c & 0x80:
+                break
+        p += (h >> 1) * bw if h & 1 else (bw + 7) // 8
+        runs += 1
+    return runs
+
+
+@pytest.mark.parametrize("list_null", [False, True])
+@pytest.mark.parametrize("leaf_null", [False, True])
+def test_list_decoder_many_hybrid_runs(ctx, tmp_path, list_null, leaf_null):
+    """pyarrow's writer mixes RLE and bit-packed runs within a level stream;
+    a page whose rep / def streams hold more runs than the List kernels'
+    run table (64) is planned on the general level walk (k_nest_walk), as
+    parquet2's HybridRleDecoder takes any number of runs (read_basic.rs:
+    83-85).  ListColumnDecoder output == the oracle's reader."""
+    import pa_amd
+
+    rng = np.random.default_rng(31 + 2 * list_null + leaf_null)
+    rows = []
+    for seg in range(400):  # constant stretches (RLE runs) between random ones (bit-packed runs)
+        if seg % 2:
+            rows += [[int(x)] for x in rng.integers(0, 1000, 40)]
+        else:
+            for _ in range(25):
+                r = rng.random()
+                rows.append(None if list_null and r < 0.1 else [] if r < 0.25 else
+                            [None if leaf_null and rng.random() < 0.2 else int(x) for x in rng.integers(0, 1000, 2)])
+    f = pa.field("c", pa.list_(pa.field("item", pa.int64(), nullable=leaf_null)), nullable=list_null)
+    t = pa.table({"c": pa.array(rows, type=f.type)}, schema=pa.schema([f]))
+    chunk, metas = chunk_of(tmp_path, t, 1, (list_null,), leaf_null, O.WriteOptions.make(), page_size=1 << 20)
+    max_def = 2 + int(list_null) + int(leaf_null) - 1
+    pos, most = 0, 0
+    for length, nlev in metas:
+        rep_len = int.from_bytes(chunk[pos + 4:pos + 8], "little")
+        def_len = int.from_bytes(chunk[pos + 8:pos + 12], "little")
+        rep = chunk[pos + 12:pos + 12 + rep_len]
+        dfb = chunk[pos + 12 + rep_len:pos + 12 + rep_len + def_len]
+        most = max(most, hybrid_runs(rep, 1), hybrid_runs(dfb, max_def.bit_length()) if def_len else 0)
+        pos += length
+    assert most > 64, most
+    eo, eb, ev, ef = O.read_nested_column(chunk, metas, np.int64, (list_null,), leaf_null)
+    dec = pa_amd.ListColumnDecoder(chunk, [pa_amd.PageMeta(l, m) for l, m in metas], np.int64, list_null, leaf_null,
+                                   ctx)
+    assert dec.num_rows == len(eo[0]) - 1 and dec.num_leaves == len(ev)
+    go, gl, gv, gf = dec.decode()
+    assert (go.cpu().numpy().astype(np.int64) == eo[0]).all()
+    if list_null:
+        assert (pa_amd.read.unpack_bitmap(gl, dec.num_rows).cpu().numpy() == eb[0]).all()
+    assert (gv.cpu().numpy()[:len(ev)] == ev).all()
+    if leaf_null:
+        assert (pa_amd.read.unpack_bitmap(gf, len(ev)).cpu().numpy() == ef).all()
+    dec.close()
