@@ -72,6 +72,7 @@ struct sb_plan {
   uint8_t* d_region = nullptr;       // fixed width: the pages' HBM regions (PageDesc.reserved)
   uint32_t* d_spill = nullptr;       // [2] spilled-leaf job counts (by decode parity)
   uint32_t* d_sched = nullptr;       // [2] k_inflate's job claim counters (zero between launches)
+  uint8_t* d_ascii = nullptr;        // binary: per page, its values stream inflated all ASCII (k_inflate)
   sb::InflateJob* d_spill_jobs = nullptr;
   uint32_t n_spill = 0;              // pages with a spill area (bounds the spill launches)
   uint32_t n_big = 0;                // binary: big Extend pages (tables in d_region)
@@ -212,6 +213,7 @@ void sb_plan_destroy(sb_plan* p) {
   if (p->d_region) (void)hipFree(p->d_region);
   if (p->d_spill) (void)hipFree(p->d_spill);
   if (p->d_sched) (void)hipFree(p->d_sched);
+  if (p->d_ascii) (void)hipFree(p->d_ascii);
   if (p->d_spill_jobs) (void)hipFree(p->d_spill_jobs);
   if (p->d_bin) (void)hipFree(p->d_bin);
   if (p->d_lb) (void)hipFree(p->d_lb);
@@ -572,6 +574,13 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "plan alloc: scratch");
     }
+    // the pages whose values stream k_inflate expands are the same every
+    // decode; it rewrites their flags each time, the rest stay 0 (scanned)
+    if (p->n_bin_jobs && (hipMalloc(&p->d_ascii, n_pages) != hipSuccess ||
+                          hipMemsetAsync(p->d_ascii, 0, n_pages, ctx->stream) != hipSuccess)) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "plan alloc: ascii flags");
+    }
     // every page staged (no header-only or big pages): one fused pass sizes,
     // bases and decodes them (k_bin_fused)
     if (n_staged == n_pages && !p->n_big && !p->n_bin_jobs && !getenv("SB_NO_BIN_FUSED") &&
@@ -621,7 +630,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
                   p->bin_grid, p->d_region, nullptr, p->n_big};
   if (p->n_bin_jobs) {  // Basic LZ4 / Snappy pages: streams expanded first, one wave each
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2, p->n_bin_jobs, out->d_values, p->d_scratch,
-                        p->d_bin + np, p->d_status, (uint8_t*)out->d_offsets, p->d_sched};
+                        p->d_bin + np, p->d_status, (uint8_t*)out->d_offsets, p->d_sched, p->d_ascii};
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))
@@ -636,7 +645,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
     uint32_t* flags = (uint32_t*)(p->d_bin + 2 * np + 1);
     HIP_TRY(ctx, hipMemsetAsync(flags, 0, sizeof(uint32_t), ctx->stream));
     sb::Utf8Launch U{out->d_values, p->values_bytes, (const uint8_t*)out->d_offsets, p->n_rows, p->d_pages,
-                     (uint32_t)np, p->d_bin + np, p->d_status, flags};
+                     (uint32_t)np, p->d_bin + np, p->d_status, flags, p->d_lb ? nullptr : p->d_ascii};
     if (sb::launch_utf8_check(p->offset_width, U, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "utf8 check launch failed: %s", hipGetErrorString(hipGetLastError()));
   }

@@ -862,6 +862,9 @@ struct WaveOut {
   // binary/mod.rs:136-144) but kept in w0; far reads undo both.
   bool xf, skip0;
   uint32_t xadd, w0;
+  // RING: some flushed byte has its high bit set (wave-uniform; Utf8 values
+  // streams whose bytes are all ASCII skip the UTF-8 scan, k_utf8_pages)
+  bool hib = false;
 
   __device__ __forceinline__ uint32_t slot(uint32_t q) const { return RING ? (q & (kRing - 1)) : q; }
   __device__ __forceinline__ uint32_t far8(uint32_t q) const {  // stream byte q < far_limit(), from HBM
@@ -903,6 +906,7 @@ struct WaveOut {
     }
     if (len == kChunk) {
       const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(ring + slot(c0 + 16 * lane));
+      hib |= __ballot(((v.x | v.y | v.z | v.w) & 0x80808080u) != 0) != 0;
       const uintptr_t al = (uintptr_t)d;
       if ((al & 15) == 0) {
         ((u32x4*)d)[lane] = v;
@@ -915,7 +919,13 @@ struct WaveOut {
       }
       return;
     }
-    for (uint32_t j = lane; j < len; j += 64) d[j] = ring[slot(c0 + j)];
+    uint32_t hb = 0;
+    for (uint32_t j = lane; j < len; j += 64) {
+      const uint32_t b = ring[slot(c0 + j)];
+      hb |= b;
+      d[j] = (uint8_t)b;
+    }
+    hib |= __ballot((hb & 0x80u) != 0) != 0;
   }
   __device__ __forceinline__ void advance(uint32_t m) {
     op += m;
@@ -974,6 +984,7 @@ struct WaveOut {
         v.y = __builtin_amdgcn_alignbyte(w[h][2], w[h][1], sh);
         v.z = __builtin_amdgcn_alignbyte(w[h][3], w[h][2], sh);
         v.w = __builtin_amdgcn_alignbyte(w[h][4], w[h][3], sh);
+        hib |= __ballot(((v.x | v.y | v.z | v.w) & 0x80808080u) != 0) != 0;
         if (xf) {
           uint32_t* q = (uint32_t*)(d + x);
           if (!skip0 || pos + x) q[0] = v.x + xadd;
@@ -1230,10 +1241,6 @@ __device__ __forceinline__ uint32_t lds_chain(lds_u8* tab, uint32_t t1) {
 }
 
 constexpr uint32_t kIb = 1024, kIbHalf = kIb / 2, kLitFast = 64, kMatchFast = 32;
-#ifndef SB_HAZ_WORD
-#define SB_HAZ_WORD 16
-#endif
-constexpr uint32_t kHazWord = SB_HAZ_WORD;  // hazards copied word-wise in rounds: at most this long
 constexpr uint32_t kChainTabs = 6;  // T1..T32: batches of up to 64 sequences
 constexpr uint32_t kChainEnd = 0xFE, kChainStop = 0xFF;  // chain sentinels (see cand_steps)
 
@@ -1612,42 +1619,10 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     }
     INF_T(5);
     INF_N(11, __popcll(__ballot(hazard)));
-#ifndef SB_HAZ_SERIAL
-    // Hazards in rounds: the first pending hazard (destination D) is ready,
-    // and so is every pending word-copyable hazard whose source ends at or
-    // before D (every byte below D is final once the hazards before it are
-    // done; the round's destinations all lie at or past D, so its copies are
-    // independent).  A batch of Float64 pages holds ~8 hazards in ~3 rounds.
-    // Self-overlapping, long (> kHazWord) and far-sourced hazards go one at
-    // a time, in order, when they are the first pending.
-    const bool hword = hazard && s.ml <= kHazWord && s.off >= s.ml && src >= farlim;
-    const uint64_t wordm = __ballot(hword);
-    for (uint64_t hm = __ballot(hazard); hm;) {
-      const uint32_t l = (uint32_t)__builtin_ctzll(hm);
-      const uint32_t D = __builtin_amdgcn_readlane(dm, l);
-      if ((wordm >> l) & 1) {
-        const bool rd = ((hm >> lane) & 1) && hword && (src + s.ml <= D || lane == l);
-        constexpr uint32_t NW = kHazWord / 4 + 1;
-        const uint32_t sh = src & 3, a0 = src - sh, need = rd ? sh + s.ml : 0u;
-        uint32_t w[NW];
-#pragma unroll
-        for (uint32_t t = 0; t < NW; t++) {
-          w[t] = 0;
-          if (!__ballot(4 * t < need)) continue;
-          w[t] = r32[((a0 + 4 * t) & (kRing - 1)) >> 2];
-        }
-        if (rd) ring_put<NW>(o.ring, dm, s.ml, sh, w);
-        hm &= ~__ballot(rd);
-        continue;
-      }
-      hm &= hm - 1;
-      const uint32_t O = __builtin_amdgcn_readlane(s.off, l), M = __builtin_amdgcn_readlane(s.ml, l);
-#else
     for (uint64_t hm = __ballot(hazard); hm; hm &= hm - 1) {
       const uint32_t l = (uint32_t)__builtin_ctzll(hm);
       const uint32_t D = __builtin_amdgcn_readlane(dm, l), O = __builtin_amdgcn_readlane(s.off, l),
                      M = __builtin_amdgcn_readlane(s.ml, l);
-#endif
       if (M <= 64 && O >= M && D - O >= farlim) {  // no self-overlap, source in the ring: one byte a lane
         if (lane < M) o.ring[(D + lane) & (kRing - 1)] = o.ring[(D - O + lane) & (kRing - 1)];
         continue;
@@ -2563,6 +2538,7 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
     }
 #endif
     if (st && lane == 0) a.status[jb.page] = st;
+    if (kind == 2 && a.ascii && lane == 0) a.ascii[jb.page] = (st == ST_OK && !o.hib) ? 1 : 0;
   }
   if (a.sched && lane == 0 && atomicAdd(&a.sched[1], 1u) == gridDim.x * kInfWaves - 1) {
     a.sched[0] = 0;  // every wave has claimed its last job: reset for the next launch
@@ -3237,6 +3213,72 @@ __device__ bool bin_light_parse(const GlbSrc& s, uint32_t len, uint32_t n, int n
   return true;
 }
 
+// Bytes [x, x + 20) of a page from HBM by six aligned dword loads (clamped to
+// the dwords that hold page bytes), so a header costs one load round trip,
+// not one per byte.  Offsets k <= 16 of the window.
+struct HdrWin {
+  uint32_t w[6], sh;
+  __device__ __forceinline__ void load(const uint8_t* pg, uint32_t x, uint32_t len) {
+    const uintptr_t a = (uintptr_t)(pg + x), lastw = (uintptr_t)(pg + (len ? len - 1 : 0)) & ~(uintptr_t)3;
+    const uintptr_t a0 = a & ~(uintptr_t)3;
+    sh = (uint32_t)(a & 3);
+#pragma unroll
+    for (int k = 0; k < 6; k++) w[k] = *(gmem_u32*)min<uintptr_t>(a0 + 4 * k, lastw);
+  }
+  __device__ __forceinline__ uint32_t u32(uint32_t k) const {
+    const uint32_t b = sh + k, i = b >> 2;
+    return __builtin_amdgcn_alignbyte(w[i + 1], w[i], b & 3);
+  }
+  __device__ __forceinline__ uint32_t u8(uint32_t k) const { return u32(k) & 0xFFu; }
+};
+
+// bin_light_parse over HdrWin windows: the validity prefix, the offsets
+// stream header and the values stream header, three load round trips.
+template <int OW>
+__device__ bool bin_light_parse_hbm(const uint8_t* pg, uint32_t len, uint32_t n, int nullable, LightPage& lp) {
+  uint32_t p = 0;
+  lp.vbpos = 0;
+  if (n == 0) return false;
+  HdrWin h;
+  if (nullable) {  // light_validity
+    if (len < 4) return false;
+    h.load(pg, 0, len);
+    const uint32_t def_len = h.u32(0);
+    p = 4;
+    if (def_len == 0 || def_len > len - p) return false;
+    uint32_t q = p, hv = 0, sft = 0;
+    for (;;) {
+      if (q >= p + def_len || sft > 28) return false;
+      const uint32_t c = h.u8(q++);  // (q <= 8)
+      hv |= (c & 0x7Fu) << sft;
+      if (!(c & 0x80)) break;
+      sft += 7;
+    }
+    if (!(hv & 1)) return false;
+    if ((uint64_t)min(hv >> 1, p + def_len - q) * 8 < n) return false;
+    lp.vbpos = q;
+    p += def_len;
+  }
+  if (p + 9 > len) return false;
+  h.load(pg, p, len);
+  lp.codec = h.u8(0);
+  if (lp.codec > 3) return false;
+  const uint32_t cs = h.u32(1), body = p + 9;
+  if (cs > len - body) return false;
+  const uint32_t vh = body + cs;
+  if (vh + 9 > len) return false;
+  h.load(pg, vh, len);
+  lp.vcs = h.u32(1);
+  lp.S = h.u32(5);
+  lp.vb = vh + 9;
+  if (lp.vcs > len - lp.vb) return false;
+  lp.ob = body;
+  lp.ocs = cs;
+  if (lp.codec == 0 && (cs != (n + 1) * (uint32_t)OW || lp.vcs != lp.S)) return false;
+  if (lp.codec == 2 && (uint64_t)len + (uint64_t)(n + 1) * OW + lp.S + kZTablesMax + 1024 <= kDeferredLds) return false;
+  return true;
+}
+
 // Classifies every page (one thread each): header-only pages get their two
 // inflate jobs and size here; the rest are listed for k_bin_size.
 template <int OW>
@@ -3246,7 +3288,7 @@ __global__ __launch_bounds__(NT) void k_bin_light(BinArgs a) {
   for (uint32_t page = blockIdx.x * NT + threadIdx.x; page < np; page += gridDim.x * NT) {
     const PageDesc pd = a.pages[page];
     LightPage lp;
-    const bool lt = bin_light_parse<OW>(GlbSrc{a.chunk + pd.byte_off}, pd.byte_len, pd.num_values, a.nullable, lp);
+    const bool lt = bin_light_parse_hbm<OW>(a.chunk + pd.byte_off, pd.byte_len, pd.num_values, a.nullable, lp);
     // one atomic per wave and counter (12k contended atomics on one address cost ~100 us)
     const bool jobs = lt && lp.codec != 0;  // None pages: copied by k_bin_light_out
     const uint32_t slot = wave_slot(a.job_count, jobs, 2), li = wave_slot(&cnt[1], lt, 1),
@@ -3474,18 +3516,23 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
 }
 
 // Exclusive scan of the page sizes (one workgroup).
+// One workgroup: each thread sums a contiguous run of pages (its loads all
+// in flight at once), one block scan, then the run's bases.
 __global__ __launch_bounds__(NT) void k_bin_scan(BinArgs a) {
   __shared__ Shared sh;
-  uint64_t carry = 0;
-  for (uint32_t p0 = 0; p0 < a.n_pages; p0 += NT) {
-    const uint32_t p = p0 + threadIdx.x;
-    const uint64_t v = p < a.n_pages ? a.sizes[p] : 0;
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan<uint64_t>(v, sh, &tot);
-    if (p < a.n_pages) a.bases[p] = carry + ex;
-    carry += tot;
+  const uint32_t n = a.n_pages, c = (n + NT - 1) / NT;
+  const uint32_t b = min(n, threadIdx.x * c), e = min(n, b + c);
+  uint64_t sum = 0;
+#pragma unroll 8
+  for (uint32_t p = b; p < e; p++) sum += a.sizes[p];
+  uint64_t tot;
+  uint64_t ex = block_excl_scan<uint64_t>(sum, sh, &tot);
+#pragma unroll 8
+  for (uint32_t p = b; p < e; p++) {
+    a.bases[p] = ex;
+    ex += a.sizes[p];
   }
-  if (threadIdx.x == 0) *a.total = carry;
+  if (threadIdx.x == 0) *a.total = tot;
 }
 
 // Rows longer than this are copied by the whole wave (bin_emit_wave).
@@ -3918,10 +3965,11 @@ __device__ __forceinline__ uint32_t utf8_len(uint32_t b) {
   return b < 0x80u ? 1u : b < 0xC2u ? 0u : b < 0xE0u ? 2u : b < 0xF0u ? 3u : b < 0xF5u ? 4u : 0u;
 }
 
+// The 16 bytes of chunk c: a bad byte marks its page OutOfSpec; a non-ASCII
+// byte raises flags[0].
 template <bool ALIGNED>
-__global__ __launch_bounds__(NT) void k_utf8_bytes(Utf8Args a) {
-  const uint64_t chunks = (a.len + 15) / 16;
-  for (uint64_t c = blockIdx.x * (uint64_t)NT + threadIdx.x; c < chunks; c += (uint64_t)gridDim.x * NT) {
+__device__ __forceinline__ void utf8_chunk(const Utf8Args& a, uint64_t c) {
+  {
     const int64_t p0 = (int64_t)(c * 16);
     uint32_t w[6];  // bytes [p0 - 4, p0 + 20)
     if (ALIGNED && (uint64_t)p0 + 16 <= a.len) {
@@ -3932,10 +3980,8 @@ __global__ __launch_bounds__(NT) void k_utf8_bytes(Utf8Args a) {
       for (int k = 0; k < 4; k++) w[1 + k] = utf8_word<ALIGNED>(a.values, a.len, p0 + 4 * k);
     }
     const bool ascii = ((w[1] | w[2] | w[3] | w[4]) & 0x80808080u) == 0;
-    const uint64_t na = __ballot(!ascii);
-    if (na && __lane_id() == __ffsll((unsigned long long)na) - 1 && *(volatile uint32_t*)a.flags == 0)
-      atomicOr(a.flags, 1u);
-    if (ascii) continue;  // no trail byte here; a lead just before is checked by its own thread
+    if (!ascii && *(volatile uint32_t*)a.flags == 0) atomicOr(a.flags, 1u);
+    if (ascii) return;  // no trail byte here; a lead just before is checked by its own thread
     w[0] = utf8_word<ALIGNED>(a.values, a.len, p0 - 4);
     w[5] = utf8_word<ALIGNED>(a.values, a.len, p0 + 16);
     auto at = [&](int i) { return (w[(i + 4) >> 2] >> (8 * ((i + 4) & 3))) & 0xFFu; };  // i in [-4, 20)
@@ -3966,6 +4012,28 @@ __global__ __launch_bounds__(NT) void k_utf8_bytes(Utf8Args a) {
       const uint32_t pg = utf8_page(a.n_pages, (uint64_t)bad_pos, [&](uint32_t i) { return a.bases[i]; });
       atomicCAS(&a.status[pg], (uint32_t)ST_OK, (uint32_t)ST_OUT_OF_SPEC);  // (a page's earlier failure stands)
     }
+  }
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(NT) void k_utf8_bytes(Utf8Args a) {
+  const uint64_t chunks = (a.len + 15) / 16;
+  for (uint64_t c = blockIdx.x * (uint64_t)NT + threadIdx.x; c < chunks; c += (uint64_t)gridDim.x * NT)
+    utf8_chunk<ALIGNED>(a, c);
+}
+
+// The same check page by page, skipping the pages whose values k_inflate
+// found all ASCII (a.ascii[page]): their bytes are characters by
+// themselves, and a lead byte before such a page still checks its trail
+// bytes in it.  The chunks a page's values range touches (a chunk on a page
+// boundary is checked by both pages).
+template <bool ALIGNED>
+__global__ __launch_bounds__(NT) void k_utf8_pages(Utf8Args a) {
+  for (uint32_t pg = blockIdx.x; pg < a.n_pages; pg += gridDim.x) {
+    if (a.ascii[pg]) continue;
+    const uint64_t b = a.bases[pg], e = pg + 1 < a.n_pages ? a.bases[pg + 1] : a.len;
+    if (b >= e) continue;
+    for (uint64_t c = b / 16 + threadIdx.x; c < (e + 15) / 16; c += NT) utf8_chunk<ALIGNED>(a, c);
   }
 }
 
@@ -5207,7 +5275,11 @@ int launch_utf8_check(int offset_width, const Utf8Launch& a, void* stream) {
   if (a.n_rows == 0 || a.n_pages == 0) return 0;  // an empty array: nothing to check (try_check_utf8)
   hipStream_t st = (hipStream_t)stream;
   const uint64_t chunks = (a.len + 15) / 16;
-  if (chunks) {
+  if (chunks && a.ascii) {  // page by page, skipping the pages k_inflate saw all ASCII
+    const dim3 g(std::min<uint32_t>(a.n_pages, 65535u));
+    if ((uintptr_t)a.values % 16) hipLaunchKernelGGL(sbk::k_utf8_pages<false>, g, dim3(sbk::NT), 0, st, a);
+    else hipLaunchKernelGGL(sbk::k_utf8_pages<true>, g, dim3(sbk::NT), 0, st, a);
+  } else if (chunks) {
     const dim3 g((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + sbk::NT - 1) / sbk::NT, 8192)));
     if ((uintptr_t)a.values % 16) hipLaunchKernelGGL(sbk::k_utf8_bytes<false>, g, dim3(sbk::NT), 0, st, a);
     else hipLaunchKernelGGL(sbk::k_utf8_bytes<true>, g, dim3(sbk::NT), 0, st, a);

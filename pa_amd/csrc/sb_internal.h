@@ -100,6 +100,7 @@ struct InflateLaunch {
   uint32_t* status;
   uint8_t* offs;  // kDstBinOffs jobs: the column's 32-bit offsets (dword-aligned)
   uint32_t* sched;  // k_inflate's job claim counters [2], zero between launches (self-resetting), or nullptr
+  uint8_t* ascii;   // binary values jobs: per page, 1 = every byte written was ASCII (else 0), or nullptr
 };
 int launch_inflate(const InflateLaunch& a, void* stream);
 // Zstd jobs (codec 2) of the same list: one wave per frame, tables in LDS, output in HBM.
@@ -195,6 +196,7 @@ struct Utf8Launch {
   const uint64_t* bases;   // first values byte of each page
   uint32_t* status;
   uint32_t* flags;         // [0]: a non-ASCII byte was seen
+  const uint8_t* ascii;    // per page: values known all ASCII (skip), or nullptr = scan everything
 };
 int launch_utf8_check(int offset_width, const Utf8Launch& a, void* stream);
 
