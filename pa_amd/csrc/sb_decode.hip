@@ -1619,14 +1619,22 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     }
     INF_T(5);
     INF_N(11, __popcll(__ballot(hazard)));
+    // Hazards in sequence order.  The common kind (no self-overlap, source in
+    // the ring, <= 64 bytes) is one byte a lane; its ring positions and
+    // length are packed per lane beforehand, so each takes one v_readlane.
+    const bool hfast = hazard && s.ml <= 64 && s.off >= s.ml && src >= farlim;
+    const uint32_t hpack = ((src & (kRing - 1)) << 20) | ((dm & (kRing - 1)) << 8) | (hfast ? s.ml : 0u);
+    const uint64_t fastm = __ballot(hfast);
     for (uint64_t hm = __ballot(hazard); hm; hm &= hm - 1) {
       const uint32_t l = (uint32_t)__builtin_ctzll(hm);
-      const uint32_t D = __builtin_amdgcn_readlane(dm, l), O = __builtin_amdgcn_readlane(s.off, l),
-                     M = __builtin_amdgcn_readlane(s.ml, l);
-      if (M <= 64 && O >= M && D - O >= farlim) {  // no self-overlap, source in the ring: one byte a lane
-        if (lane < M) o.ring[(D + lane) & (kRing - 1)] = o.ring[(D - O + lane) & (kRing - 1)];
+      if ((fastm >> l) & 1) {
+        const uint32_t h = __builtin_amdgcn_readlane(hpack, l);
+        if (lane < (h & 0xFFu))
+          o.ring[((h >> 8) + lane) & (kRing - 1)] = o.ring[((h >> 20) + lane) & (kRing - 1)];
         continue;
       }
+      const uint32_t D = __builtin_amdgcn_readlane(dm, l), O = __builtin_amdgcn_readlane(s.off, l),
+                     M = __builtin_amdgcn_readlane(s.ml, l);
       for (uint32_t c = 0; c < M; c += 64) {
         if (lane < M - c) {
           const uint32_t x = D + c;

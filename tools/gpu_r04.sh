@@ -17,10 +17,10 @@ case $step in
       PA_AMD_LIB=$L timeout -k 10 200 python tools/c3bench.py ${2:-100000000} 2>&1 | grep -v amdgpu.ids || exit 1
     done ;;
   prof)  # prof <tag> <python args...>: rocprofv3 kernel trace + stats of a python command, per-kernel summary
-    tag=$1; shift
+    tag=$1; script=$2; shift 2
     R=$GRAFT_REPO_ROOT
     cd /tmp && export TMPDIR=/tmp
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${tag}_kt -o k -- python3 "$@" > $R/gpurun_out/${tag}_kt.log 2>&1 || { echo "prof failed"; tail -5 $R/gpurun_out/${tag}_kt.log; exit 1; }
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${tag}_kt -o k -- python3 $R/$script "$@" > $R/gpurun_out/${tag}_kt.log 2>&1 || { echo "prof failed"; tail -5 $R/gpurun_out/${tag}_kt.log; exit 1; }
     cd $R && python3 tools/prof_summary.py trace gpurun_out/${tag}_kt/k_kernel_trace.csv 1 gpurun_out/${tag}_kernels.json | head -60 ;;
   phases)
     PA_AMD_LIB=pa_amd/variants/libsb_phases.so timeout -k 10 200 python tools/infphases.py ${1:-10000000} 2>&1 | grep -v amdgpu.ids ;;
