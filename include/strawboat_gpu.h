@@ -346,6 +346,11 @@ uint64_t sb_page_seed(uint64_t seed, uint64_t page);
  * Return the compressed size. */
 uint64_t sb_lz4_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst);
 uint64_t sb_snappy_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst);
+/* The device encoder's Zstd frame writer (pa_amd/csrc/sb_zstdc.h) on the host:
+ * an RFC 8878 frame of n bytes that libzstd decodes to src (the reference's
+ * libzstd level-3 bytes are not reproduced; decode equivalence is the bar).
+ * dst holds n + n/2048 + 3*(n/131072) + 512 bytes.  Returns the frame size. */
+uint64_t sb_zstd_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst);
 /* encode_chunk on the device (HIP, gfx950), byte-identical to
  * sb_encode_column with the same options: the adaptive cascade
  * (compress_integer / compress_double / compress_boolean with the seeded

@@ -27,7 +27,7 @@ EXPORTED = [
     "sb_decompress_values", "sb_read_meta", "sb_encode_page", "sb_encode_column", "sb_page_seed",
     "sb_write_footer", "sb_free", "sb_encode_binary_column", "sb_plan_values_bytes", "sb_decode_binary_planned",
     "sb_encode_list_column", "sb_plan_list_column", "sb_plan_num_leaves", "sb_decode_list_planned",
-    "sb_encode_device_bound", "sb_encode_column_device", "sb_lz4_compress_host", "sb_snappy_compress_host",
+    "sb_encode_device_bound", "sb_encode_column_device", "sb_lz4_compress_host", "sb_snappy_compress_host", "sb_zstd_compress_host",
     "sb_encode_binary_device_bound", "sb_encode_binary_column_device", "sb_plan_nested_column",
     "sb_plan_nested_count", "sb_decode_nested_planned", "sb_parse_schema", "sb_file_open", "sb_file_close",
     "sb_file_last_error", "sb_file_num_columns", "sb_file_column", "sb_file_schema", "sb_file_upload",

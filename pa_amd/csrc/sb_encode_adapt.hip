@@ -23,8 +23,9 @@
 //     delta_bp.rs:37-67; BitPacker4x words computed per lane word), Patas
 //     (double/patas.rs:37-105; the back reference found by a 127-row window
 //     search), and the Basic codecs None / LZ4 (sb_lz4c.h, one wave) /
-//     Snappy (one lane;
-//     Zstd level 3 is not restated: NotYetImplemented).
+//     Snappy (one lane) / Zstd (sb_zstdc.h: frames transcoded from the LZ4
+//     parse; libzstd level 3's bytes are not reproduced, any Zstd decoder
+//     returns the page's bytes).
 // Pages are written into per-page slots of a batch, then compacted.
 // Integer work; bound by the per-page hash/scan work, not by MFMA.
 #include <hip/hip_runtime.h>
@@ -36,6 +37,7 @@
 #include "../../include/strawboat_gpu.h"
 #include "sb_internal.h"
 #include "sb_lz4c.h"
+#include "sb_zstdc.h"
 
 namespace sba {
 
@@ -44,7 +46,6 @@ namespace sba {
 #endif
 constexpr int NT = SB_ENC_NT, NW = NT / 64;
 constexpr uint32_t kMaxRows = 16384;      // pages whose statistics' tables fit the LDS work area
-constexpr uint32_t kMaxNarrowRows = 65535;  // table words with 16-bit rows; larger pages use 64-bit words
 constexpr uint32_t SC = 10, SS = 64, kSample = SC * SS;
 // A big Boolean page's HBM work area: the RLE run starts (or the Snappy
 // table), then the page's bits one byte a row, then its rebuilt bitmap.
@@ -742,7 +743,7 @@ __device__ int choose(Ctx& c, Sh& sh, const Av& a, uint32_t fm) {
   return result;
 }
 
-// Basic codecs: the raw bytes of the values, None / LZ4 / Snappy
+// Basic codecs: the raw bytes of the values, None / LZ4 / Snappy / Zstd
 __device__ uint32_t basic_body(Ctx& c, Sh& sh, int codec, const uint8_t* src, uint32_t len, uint32_t pos) {
   const uint32_t tid = threadIdx.x;
   if (codec == C_NONE) {
@@ -775,9 +776,35 @@ __device__ uint32_t basic_body(Ctx& c, Sh& sh, int codec, const uint8_t* src, ui
     __syncthreads();
     return r;
   }
-  if (tid == 0) set_err(sh, E_NYI);  // Zstd: libzstd level 3 is not restated on the device
+  // Zstd (sb_zstdc.h): wave 0 parses each 128 KiB chunk with the LZ4
+  // compressor into the slot past the frame's bound, lane 0 transcodes the
+  // parse into the chunk's blocks (sequence records in the LZ4 tables' LDS)
+  const uint32_t cl0 = min(len, sbz::kZChunk);
+  const uint64_t zb = sbz::zstd_bound(len);
+  if (!room(c, sh, (uint64_t)pos + zb + sbc::lz4_bound(cl0) + 16)) return 0;
+  if (tid < 64) {
+    uint8_t* frame = c.out + pos;
+    uint8_t* tmp = frame + zb;
+    uint32_t op = 0;
+    if (len == 0 && tid == 0) op = sbz::zstd_empty(frame);
+    if (len && tid == 0) op = sbz::zstd_frame_header(frame, len);
+    for (uint32_t off = 0; off < len; off += sbz::kZChunk) {
+      const uint32_t cl = min(len - off, sbz::kZChunk);
+      for (uint32_t i = tid; i < 4096; i += 64) ((uint32_t*)c.lz4)[i] = 0;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's table stores land before its loads
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t r = sbc::lz4_compress_wave(src + off, cl, tmp, (sbc::lz4_lds8*)c.lz4);
+      __threadfence();  // the parse's stores, visible to lane 0
+      if (tid == 0) op += sbz::zstd_transcode(tmp, r, src + off, cl, frame + op, (uint64_t*)c.lz4, off + cl == len);
+      __threadfence();
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (tid == 0) sh.redu[0] = op;
+  }
   __syncthreads();
-  return 0;
+  const uint32_t r = sh.redu[0];
+  __syncthreads();
+  return r;
 }
 
 __device__ __forceinline__ void write_hdr(Ctx& c, uint32_t pos, int codec, uint32_t csize, uint32_t usize) {
@@ -1681,7 +1708,9 @@ namespace sb {
 
 static uint64_t stream_bound(uint64_t n, uint64_t w, int depth) {
   // worst case of one headered stream of n values of w bytes (cascade depth left)
-  const uint64_t leaf = 9 + std::max({n * (4 + w), n * w + n * w / 255 + 32, (n / 128) * 513, w + n * (2 + w)});
+  // (Zstd: the frame's bound + the LZ4 parse of one chunk behind it)
+  const uint64_t zstd = sbz::zstd_bound(n * w) + sbc::lz4_bound((uint32_t)std::min<uint64_t>(n * w, sbz::kZChunk)) + 16;
+  const uint64_t leaf = 9 + std::max({n * (4 + w), n * w + n * w / 255 + 32, (n / 128) * 513, w + n * (2 + w), zstd});
   if (depth == 0) return leaf;
   const uint64_t dict = 9 + stream_bound(n, 4, depth - 1) + 4 + n * w;
   const uint64_t freq = 9 + w + 4 + 16 + 8 * ((n + 65535) / 65536) + std::max<uint64_t>(2 * n, 8192) +
@@ -1699,7 +1728,9 @@ uint64_t adaptive_slot_bytes(uint64_t P, uint32_t w, int nullable) {
 // statistics needs only its codec's (more workgroups per CU for LZ4 pages)
 uint32_t adaptive_work_bytes(uint64_t P, const sba::Opts& o) {
   if (!sba::needs_stats(o, o.forbidden))
-    return o.dflt == sba::C_SNAPPY ? sbc::kSnappyTableBytes : o.dflt == sba::C_LZ4 ? sbc::kLz4WaveLds : 8192;
+    return o.dflt == sba::C_SNAPPY                          ? sbc::kSnappyTableBytes
+           : (o.dflt == sba::C_LZ4 || o.dflt == sba::C_ZSTD) ? sbc::kLz4WaveLds
+                                                             : 8192;
   uint64_t s = 64;
   while (s < 2 * P) s <<= 1;
   return (uint32_t)std::max<uint64_t>({4 * s, sbc::kSnappyTableBytes, 8192});
@@ -1749,7 +1780,7 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
   }
   const bool is_bool = phys == SB_T_BOOLEAN;
   // Pages over kMaxRows rows keep their work area in HBM (any size; over
-  // kMaxNarrowRows with 64-bit table words and several roaring containers);
+  // 65535 rows with 64-bit table words and several roaring containers);
   // Boolean pages stage their bits in LDS up to kMaxRows, in HBM past it
   const bool stats = sba::needs_stats(o, o.forbidden);
   const bool big = P > sba::kMaxRows;

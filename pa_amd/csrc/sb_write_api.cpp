@@ -11,6 +11,7 @@
 #include "../../include/strawboat_gpu.h"
 #include "sb_encode.h"
 #include "sb_lz4c.h"
+#include "sb_zstdc.h"
 
 using sb::enc::Opts;
 
@@ -47,6 +48,22 @@ uint64_t sb_lz4_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst) {
 uint64_t sb_snappy_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst) {
   std::vector<uint8_t> table(sbc::kSnappyTableBytes);
   return sbc::snappy_compress(src, (uint32_t)n, dst, table.data());
+}
+
+// The device encoder's Zstd frame writer (sb_zstdc.h): LZ4 parse per 128 KiB
+// chunk, transcoded into Predefined_Mode sequence blocks.
+uint64_t sb_zstd_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst) {
+  if (!n) return sbz::zstd_empty(dst);
+  std::vector<uint8_t> table(sbc::kLz4TableBytes), lz(sbc::lz4_bound(sbz::kZChunk));
+  std::vector<uint64_t> recs(sbz::kZSeqPerBlock);
+  uint64_t op = sbz::zstd_frame_header(dst, (uint32_t)n);
+  for (uint64_t off = 0; off < n; off += sbz::kZChunk) {
+    const uint32_t cl = (uint32_t)std::min<uint64_t>(sbz::kZChunk, n - off);
+    std::fill(table.begin(), table.end(), 0);
+    const uint32_t ll = sbc::lz4_compress(src + off, cl, lz.data(), table.data());
+    op += sbz::zstd_transcode(lz.data(), ll, src + off, cl, dst + op, recs.data(), off + cl == n);
+  }
+  return op;
 }
 
 sb_status sb_encode_page(int32_t phys, const void* h_values, const uint8_t* h_validity, uint64_t n, int32_t nullable,

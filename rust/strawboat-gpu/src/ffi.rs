@@ -118,6 +118,7 @@ extern "C" {
     pub fn sb_page_seed(seed: u64, page: u64) -> u64;
     pub fn sb_lz4_compress_host(src: *const u8, n: u64, dst: *mut u8) -> u64;
     pub fn sb_snappy_compress_host(src: *const u8, n: u64, dst: *mut u8) -> u64;
+    pub fn sb_zstd_compress_host(src: *const u8, n: u64, dst: *mut u8) -> u64;
     pub fn sb_decompress_values(ctx: *mut sb_ctx, physical_type: i32, d_stream: *const u8, stream_len: u64,
                                 length: u64, d_out: *mut c_void) -> i32;
     pub fn sb_decode_page_validity(ctx: *mut sb_ctx, d_page: *const u8, page_len: u64, length: u64,

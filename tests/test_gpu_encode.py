@@ -158,17 +158,99 @@ def test_big_binary_freq_roaring_tmp(ctx, P):
     assert dev.cpu().numpy().tobytes() == host
 
 
-def test_unsupported_options_are_nyi(ctx):
-    """Zstd as the default codec (libzstd's compressor is not restated on the
-    device) reports NotYetImplemented."""
+ZSTD_OPTS = {
+    "basic": dict(default_compression=2),
+    "adaptive": dict(default_compression=2, default_compress_ratio=1.2),
+    "dict": dict(default_compression=2, default_compress_ratio=2.0, forced_codec=11),
+    "freq": dict(default_compression=2, default_compress_ratio=2.0, forced_codec=13),
+}
+
+
+def page_codecs(chunk, metas, nullable):
+    """the codec byte of every page (after its validity prefix)"""
+    out, pos = [], 0
+    for m in metas:
+        q = pos + (4 + int.from_bytes(chunk[pos:pos + 4], "little") if nullable else 0)
+        out.append(chunk[q])
+        pos += m.length
+    return out
+
+
+@pytest.mark.parametrize("P", [8192, 70_000, None])
+@pytest.mark.parametrize("kind", ["f64", "int32_runs", "int64_freq", "int8"])
+@pytest.mark.parametrize("opt", list(ZSTD_OPTS))
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+def test_device_zstd_pages(ctx, P, kind, opt, nullable):
+    """Zstd as the default codec (CommonCompression::compress, basic.rs:122-135):
+    the device writes Zstd frames transcoded from its LZ4 parse (sb_zstdc.h),
+    not libzstd level 3's bytes -- the pages carry the host writer's codec
+    choices and row counts, and decode (oracle through libzstd, and the GPU
+    reader) to the input values."""
     import pa_amd
 
-    tv = torch.arange(70000, dtype=torch.int32, device="cuda")
-    for opts in (pa_amd.WriteOptions(default_compression=2), pa_amd.WriteOptions(default_compression=2,
-                                                                                  default_compress_ratio=1.2)):
-        with pytest.raises(pa_amd.StrawboatError) as e:
-            pa_amd.encode_column_device(tv, None, False, opts, ctx=ctx)
-        assert e.value.status == 2
+    rng = np.random.default_rng(abs(hash((P, kind, opt))) % 2**32)
+    n = 150_001
+    if kind == "f64":
+        v = np.round(rng.standard_normal(n) * 1e3, 1)
+    elif kind == "int32_runs":
+        v = np.repeat(rng.integers(0, 1 << 30, n // 40 + 1), 40)[:n].astype(np.int32)
+    elif kind == "int64_freq":
+        v = np.where(rng.random(n) < 0.93, 1 << 40, rng.integers(0, 1 << 50, n)).astype(np.int64)
+    else:
+        v = rng.integers(-100, 100, n).astype(np.int8)
+    valid = rng.random(n) > 0.1
+    opts = pa_amd.WriteOptions(max_page_size=P, **ZSTD_OPTS[opt])
+    host, hm = pa_amd.encode_column(v, valid, nullable, opts)
+    dev, dm = pa_amd.encode_column_device(torch.from_numpy(v.copy()).cuda(), torch.from_numpy(valid).cuda(), nullable,
+                                          opts, ctx=ctx)
+    got = dev.cpu().numpy().tobytes()
+    assert [m.num_values for m in dm] == [m.num_values for m in hm]
+    assert sum(m.length for m in dm) == len(got)
+    assert page_codecs(got, dm, nullable) == page_codecs(host, hm, nullable)
+    metas = [(m.length, m.num_values) for m in dm]
+    ov, ovalid = O.read_column(got, metas, v.dtype, nullable)
+    keep = valid if nullable else np.ones(n, bool)
+    assert ov[keep].tobytes() == v[keep].tobytes()
+    if nullable:
+        assert (ovalid == valid).all()
+    dec = pa_amd.ColumnDecoder(dev, dm, v.dtype, nullable, ctx=ctx)
+    gv, _ = dec.decode()
+    assert gv.cpu().numpy().view(v.dtype)[:n][keep].tobytes() == v[keep].tobytes()
+
+
+@pytest.mark.parametrize("nullable", [False, True], ids=["req", "null"])
+def test_device_zstd_bool_and_utf8(ctx, nullable):
+    """Zstd Boolean pages (the bitmap bytes) and Utf8 pages (offsets and
+    values streams) from the device decode to the input."""
+    import pa_amd
+
+    rng = np.random.default_rng(21)
+    n = 100_003
+    valid = rng.random(n) > 0.1
+    keep = valid if nullable else np.ones(n, bool)
+    for P in (4096, 30_000):
+        opts = pa_amd.WriteOptions(max_page_size=P, default_compression=2)
+        b = np.repeat(rng.random(n // 5 + 1) > 0.5, 5)[:n]
+        dev, dm = pa_amd.encode_column_device(torch.from_numpy(b.copy()).cuda(), torch.from_numpy(valid).cuda(),
+                                              nullable, opts, ctx=ctx)
+        got = dev.cpu().numpy().tobytes()
+        ov, _ = O.read_bool_column(got, [(m.length, m.num_values) for m in dm], nullable)
+        assert (ov[keep] == b[keep]).all()
+        strs = [b"common" if r < 0.5 else str(x).encode() for r, x in zip(rng.random(n), rng.integers(0, 10**6, n))]
+        vals, offs = pa_amd.binary.strings_to_arrow(strs)
+        for o in (opts, pa_amd.WriteOptions(max_page_size=P, default_compression=2, default_compress_ratio=1.5)):
+            dev, dm = pa_amd.encode_binary_column_device(torch.from_numpy(np.frombuffer(vals, np.uint8).copy()).cuda(),
+                                                         torch.from_numpy(offs).cuda(), torch.from_numpy(valid).cuda(),
+                                                         nullable, o, pa_amd.UTF8, ctx=ctx)
+            got = dev.cpu().numpy().tobytes()
+            goffs, gvals, gvalid = O.read_binary_column(got, [(m.length, m.num_values) for m in dm], nullable)
+            for i in np.flatnonzero(keep)[::97]:
+                assert gvals[goffs[i]:goffs[i + 1]] == strs[i]
+            d = pa_amd.BinaryColumnDecoder(dev, dm, pa_amd.UTF8, nullable, ctx=ctx)
+            to, tv, _ = d.decode()
+            to, tv = to.cpu().numpy(), tv.cpu().numpy().tobytes()
+            for i in np.flatnonzero(keep)[::97]:
+                assert tv[to[i]:to[i + 1]] == strs[i]
 
 
 @pytest.mark.parametrize("P", [20000, 65535, 65537, 300_000])
