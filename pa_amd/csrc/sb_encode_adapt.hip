@@ -743,7 +743,36 @@ __device__ int choose(Ctx& c, Sh& sh, const Av& a, uint32_t fm) {
   return result;
 }
 
+// A Zstd frame of src[0, len) at `frame`, one wave: each 128 KiB chunk is
+// parsed by the wave LZ4 compressor into `tmp` (the slot past the frame's
+// bound), then lane 0 transcodes the parse into the chunk's blocks (sequence
+// records in the LZ4 tables' LDS).  Only the ZS kernels hold it: with it
+// (inlined, or out of line) the encode kernels grew from 152 to 184-248
+// VGPRs (one or two waves a SIMD instead of three).  Returns the frame size.
+__device__ __forceinline__ uint32_t zstd_frame_wave(const uint8_t* src, uint32_t len, uint8_t* frame, uint8_t* tmp,
+                                                 sbc::lz4_lds8* tab) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t op = 0;
+  if (len == 0 && lane == 0) op = sbz::zstd_empty(frame);
+  if (len && lane == 0) op = sbz::zstd_frame_header(frame, len);
+  for (uint32_t off = 0; off < len; off += sbz::kZChunk) {
+    const uint32_t cl = min(len - off, sbz::kZChunk);
+    for (uint32_t i = lane; i < 4096; i += 64) ((uint32_t*)tab)[i] = 0;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's table stores land before its loads
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t r = sbc::lz4_compress_wave(src + off, cl, tmp, tab);
+    __threadfence();  // the parse's stores, visible to lane 0
+    if (lane == 0) op += sbz::zstd_transcode(tmp, r, src + off, cl, frame + op, (uint64_t*)tab, off + cl == len);
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+  }
+  return op;
+}
+
 // Basic codecs: the raw bytes of the values, None / LZ4 / Snappy / Zstd
+// ZS: the kernel instantiation for a Zstd default codec (only those carry the
+// frame writer: the others keep their register budget).
+template <bool ZS>
 __device__ uint32_t basic_body(Ctx& c, Sh& sh, int codec, const uint8_t* src, uint32_t len, uint32_t pos) {
   const uint32_t tid = threadIdx.x;
   if (codec == C_NONE) {
@@ -776,35 +805,24 @@ __device__ uint32_t basic_body(Ctx& c, Sh& sh, int codec, const uint8_t* src, ui
     __syncthreads();
     return r;
   }
-  // Zstd (sb_zstdc.h): wave 0 parses each 128 KiB chunk with the LZ4
-  // compressor into the slot past the frame's bound, lane 0 transcodes the
-  // parse into the chunk's blocks (sequence records in the LZ4 tables' LDS)
-  const uint32_t cl0 = min(len, sbz::kZChunk);
-  const uint64_t zb = sbz::zstd_bound(len);
-  if (!room(c, sh, (uint64_t)pos + zb + sbc::lz4_bound(cl0) + 16)) return 0;
-  if (tid < 64) {
-    uint8_t* frame = c.out + pos;
-    uint8_t* tmp = frame + zb;
-    uint32_t op = 0;
-    if (len == 0 && tid == 0) op = sbz::zstd_empty(frame);
-    if (len && tid == 0) op = sbz::zstd_frame_header(frame, len);
-    for (uint32_t off = 0; off < len; off += sbz::kZChunk) {
-      const uint32_t cl = min(len - off, sbz::kZChunk);
-      for (uint32_t i = tid; i < 4096; i += 64) ((uint32_t*)c.lz4)[i] = 0;
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's table stores land before its loads
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t r = sbc::lz4_compress_wave(src + off, cl, tmp, (sbc::lz4_lds8*)c.lz4);
-      __threadfence();  // the parse's stores, visible to lane 0
-      if (tid == 0) op += sbz::zstd_transcode(tmp, r, src + off, cl, frame + op, (uint64_t*)c.lz4, off + cl == len);
-      __threadfence();
-      __builtin_amdgcn_wave_barrier();
+  if constexpr (!ZS) {
+    if (tid == 0) set_err(sh, E_NYI);  // (never: Zstd pages run the ZS instantiation)
+    __syncthreads();
+    return 0;
+  } else {
+    // Zstd (sb_zstdc.h): wave 0 writes the frame (zstd_frame_wave)
+    const uint32_t cl0 = min(len, sbz::kZChunk);
+    const uint64_t zb = sbz::zstd_bound(len);
+    if (!room(c, sh, (uint64_t)pos + zb + sbc::lz4_bound(cl0) + 16)) return 0;
+    if (tid < 64) {
+      const uint32_t r = zstd_frame_wave(src, len, c.out + pos, c.out + pos + zb, (sbc::lz4_lds8*)c.lz4);
+      if (tid == 0) sh.redu[0] = r;
     }
-    if (tid == 0) sh.redu[0] = op;
+    __syncthreads();
+    const uint32_t r = sh.redu[0];
+    __syncthreads();
+    return r;
   }
-  __syncthreads();
-  const uint32_t r = sh.redu[0];
-  __syncthreads();
-  return r;
 }
 
 __device__ __forceinline__ void write_hdr(Ctx& c, uint32_t pos, int codec, uint32_t csize, uint32_t usize) {
@@ -819,13 +837,13 @@ __device__ __forceinline__ void write_hdr(Ctx& c, uint32_t pos, int codec, uint3
 // compress_integer / compress_double: [codec u8][csize u32][usize u32][body]
 // at c.out + pos; returns the position after it.  D = cascade depth.
 // ---------------------------------------------------------------------------
-template <int W, bool FLT, bool SGN, int D>
+template <int W, bool FLT, bool SGN, int D, bool ZS>
 __device__ uint32_t enc_stream(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos);
 
 // Dict (dict.rs:34-73): ids by first occurrence over valid rows (a null row
 // repeats the previous row's id; a null row 0 is T::default()), the u32
 // index stream cascades with Dict forbidden, then u32 k + k raw values.
-template <int W, bool FLT, bool SGN, int D>
+template <int W, bool FLT, bool SGN, int D, bool ZS>
 __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos) {
   const uint32_t tid = threadIdx.x, n = a.n;
   uint32_t* idx = (uint32_t*)(c.scratch + (uint64_t)D * c.nmax * 8);
@@ -880,7 +898,7 @@ __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
   }
   __syncthreads();
   const Av ia{(const uint8_t*)idx, nullptr, 0, n};
-  const uint32_t p2 = enc_stream<4, false, false, D + 1>(c, sh, ia, fm | (1u << C_DICT), pos);
+  const uint32_t p2 = enc_stream<4, false, false, D + 1, ZS>(c, sh, ia, fm | (1u << C_DICT), pos);
   if (sh.err) return pos;
   if (!room(c, sh, (uint64_t)p2 + 4 + (uint64_t)k * W)) return pos;
   if (tid == 0) put8(c.out + p2, k, 4);
@@ -961,7 +979,7 @@ __device__ uint32_t roaring_multi(Ctx& c, Sh& sh, const uint32_t* bm, const uint
 // Freq (freq.rs:34-86): top value (the most frequent, first occurrence on
 // ties; T::default() when >= 90 % nulls), roaring bitmap of the valid rows
 // that differ from it, their values as a cascaded stream (Freq forbidden).
-template <int W, bool FLT, bool SGN, int D>
+template <int W, bool FLT, bool SGN, int D, bool ZS>
 __device__ uint32_t freq_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos) {
   const uint32_t tid = threadIdx.x, n = a.n;
   const bool top_null = (double)sh.nulls / (double)n >= 0.9;
@@ -1011,7 +1029,7 @@ __device__ uint32_t freq_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
     }
     __syncthreads();
     const Av ea{exc, nullptr, 0, e};
-    return enc_stream<W, FLT, SGN, D + 1>(c, sh, ea, fm | (1u << C_FREQ), rpos + bytes);
+    return enc_stream<W, FLT, SGN, D + 1, ZS>(c, sh, ea, fm | (1u << C_FREQ), rpos + bytes);
   }
   const uint32_t bytes = e == 0 ? 8u : (e <= 4096 ? 16 + 2 * e : 16 + 8192u);
   if (!room(c, sh, (uint64_t)rpos + bytes)) return pos;
@@ -1030,7 +1048,7 @@ __device__ uint32_t freq_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
     for (uint32_t i = tid; i < 2048; i += NT) put8(c.out + data + 4 * i, bm[i], 4);
   __syncthreads();
   const Av ea{exc, nullptr, 0, e};
-  return enc_stream<W, FLT, SGN, D + 1>(c, sh, ea, fm | (1u << C_FREQ), rpos + bytes);
+  return enc_stream<W, FLT, SGN, D + 1, ZS>(c, sh, ea, fm | (1u << C_FREQ), rpos + bytes);
 }
 
 #ifdef SB_ENC_PHASES  // A/B instrumentation: per workgroup, s_memrealtime at each phase of the top two streams
@@ -1040,7 +1058,7 @@ __device__ uint64_t sb_enc_phase[4096 * 12];
 #define SB_EPHASE(k, v) do { } while (0)
 #endif
 
-template <int W, bool FLT, bool SGN, int D>
+template <int W, bool FLT, bool SGN, int D, bool ZS>
 __device__ uint32_t enc_stream(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t pos) {
   const uint32_t tid = threadIdx.x, n = a.n;
   SB_EPHASE(0, wall_clock64());
@@ -1058,7 +1076,7 @@ __device__ uint32_t enc_stream(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_
     case C_NONE:
     case C_LZ4:
     case C_ZSTD:
-    case C_SNAPPY: end = body + basic_body(c, sh, codec, a.p, n * W, body); break;
+    case C_SNAPPY: end = body + basic_body<ZS>(c, sh, codec, a.p, n * W, body); break;
     case C_RLE: end = body + rle_body<W, FLT, SGN, true>(c, sh, a, body); break;
     case C_ONE: {  // one_value.rs:63-75: the first valid value, else default
       if (!room(c, sh, (uint64_t)body + W)) break;
@@ -1076,18 +1094,18 @@ __device__ uint32_t enc_stream(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_
       const uint32_t r = patas_body<W, true>(c, sh, a, body);
       if (r == ~0u) {  // f32 desync guard (sb_encode.cpp compress_stream): Basic instead
         codec = c.o.dflt;
-        end = body + basic_body(c, sh, codec, a.p, n * W, body);
+        end = body + basic_body<ZS>(c, sh, codec, a.p, n * W, body);
       } else {
         end = body + r;
       }
       break;
     }
     case C_DICT:
-      if constexpr (D < 2) end = dict_body<W, FLT, SGN, D>(c, sh, a, fm, body);
+      if constexpr (D < 2) end = dict_body<W, FLT, SGN, D, ZS>(c, sh, a, fm, body);
       else set_err(sh, E_SPEC);
       break;
     case C_FREQ:
-      if constexpr (D < 2) end = freq_body<W, FLT, SGN, D>(c, sh, a, fm, body);
+      if constexpr (D < 2) end = freq_body<W, FLT, SGN, D, ZS>(c, sh, a, fm, body);
       else set_err(sh, E_SPEC);
       break;
     default: set_err(sh, E_SPEC);
@@ -1216,6 +1234,7 @@ __device__ void ctx_init(Ctx& c, Sh& sh, const AdArgs& A, uint32_t p) {
 // over the page's bitmap bytes (the parent's bytes when the page starts on a
 // byte, a rebuilt zero-padded bitmap otherwise).  The page's bits are staged
 // one byte per row so the integer RLE and sampler serve unchanged.
+template <bool ZS>
 __global__ __launch_bounds__(NT) void k_enc_bool(AdArgs A) {
   extern __shared__ uint32_t lds[];
   __shared__ Sh sh;
@@ -1295,7 +1314,7 @@ __global__ __launch_bounds__(NT) void k_enc_bool(AdArgs A) {
     }
   } else if (codec <= C_SNAPPY) {
     const uint8_t* src = (r0 & 7) ? rebuilt : A.values + r0 / 8;
-    end = body + basic_body(c, sh, codec, src, nb, body);
+    end = body + basic_body<ZS>(c, sh, codec, src, nb, body);
   } else {
     set_err(sh, E_SPEC);
   }
@@ -1308,7 +1327,7 @@ __global__ __launch_bounds__(NT) void k_enc_bool(AdArgs A) {
   }
 }
 
-template <int W, bool FLT, bool SGN>
+template <int W, bool FLT, bool SGN, bool ZS>
 __global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
   extern __shared__ uint32_t lds[];
   __shared__ Sh sh;
@@ -1323,7 +1342,7 @@ __global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
   uint32_t pos = write_prefix(c, A, r0, n);
   const Av a{A.values + r0 * W, has_vb ? A.validity : nullptr, r0, n};
   __syncthreads();
-  pos = enc_stream<W, FLT, SGN, 0>(c, sh, a, A.o.forbidden, pos);
+  pos = enc_stream<W, FLT, SGN, 0, ZS>(c, sh, a, A.o.forbidden, pos);
   __syncthreads();
   if (tid == 0) {
     A.sizes[p] = sh.err ? 0 : pos;
@@ -1399,7 +1418,7 @@ __device__ uint32_t put_records(Ctx& c, Sh& sh, const Strs& S, uint32_t cnt, Row
   return carry;
 }
 
-template <int OW>
+template <int OW, bool ZS>
 __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
   extern __shared__ uint32_t lds[];
   __shared__ Sh sh;
@@ -1510,14 +1529,14 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
     } else {
       for (uint32_t i = tid; i <= n; i += NT) put8(obuf + i * OW, (uint64_t)(A.offsets[r0 + i] - base), OW);
       __syncthreads();
-      cs = basic_body(c, sh, codec, obuf, ob, body);
+      cs = basic_body<ZS>(c, sh, codec, obuf, ob, body);
     }
     __syncthreads();
     write_hdr(c, pos, codec, cs, ob);
     const uint32_t h2 = body + cs;
     const uint32_t vl = (uint32_t)(A.offsets[r0 + n] - base);
     if (room(c, sh, (uint64_t)h2 + 9)) {
-      const uint32_t cs2 = basic_body(c, sh, codec, A.values + base, vl, h2 + 9);
+      const uint32_t cs2 = basic_body<ZS>(c, sh, codec, A.values + base, vl, h2 + 9);
       __syncthreads();
       write_hdr(c, h2, codec, cs2, vl);
       end = h2 + 9 + cs2;
@@ -1572,7 +1591,7 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
     }
     // the index stream cascades (Dict forbidden) at depth 1 (its scratch: region 1)
     const Av ia{(const uint8_t*)idx, nullptr, 0, n};
-    const uint32_t p2 = enc_stream<4, false, false, 1>(c, sh, ia, fm | (1u << C_DICT), body);
+    const uint32_t p2 = enc_stream<4, false, false, 1, ZS>(c, sh, ia, fm | (1u << C_DICT), body);
     if (!sh.err && room(c, sh, (uint64_t)p2 + 4)) {
       if (tid == 0) put8(c.out + p2, k, 4);
       const Strs SS2{A.values, A.offsets + r0, hsh};
@@ -1753,8 +1772,23 @@ static uint32_t batch_pages(uint64_t np, uint64_t per_page) {
 
 template <int W, bool FLT, bool SGN>
 static void launch_t(const sba::AdArgs& a, uint32_t lds, hipStream_t st) {
-  ensure_lds_attr(sba::k_enc_adaptive<W, FLT, SGN>, (int)lds);
-  hipLaunchKernelGGL((sba::k_enc_adaptive<W, FLT, SGN>), dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+  if (a.o.dflt == sba::C_ZSTD) {
+    ensure_lds_attr(sba::k_enc_adaptive<W, FLT, SGN, true>, (int)lds);
+    hipLaunchKernelGGL((sba::k_enc_adaptive<W, FLT, SGN, true>), dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+  } else {
+    ensure_lds_attr(sba::k_enc_adaptive<W, FLT, SGN, false>, (int)lds);
+    hipLaunchKernelGGL((sba::k_enc_adaptive<W, FLT, SGN, false>), dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+  }
+}
+template <int OW>
+static void launch_bin(const sba::AdArgs& a, uint32_t lds, hipStream_t st) {
+  if (a.o.dflt == sba::C_ZSTD) {
+    ensure_lds_attr(sba::k_enc_binary<OW, true>, (int)lds);
+    hipLaunchKernelGGL((sba::k_enc_binary<OW, true>), dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+  } else {
+    ensure_lds_attr(sba::k_enc_binary<OW, false>, (int)lds);
+    hipLaunchKernelGGL((sba::k_enc_binary<OW, false>), dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+  }
 }
 
 // Encodes every page of a fixed-width column; returns SB status.
@@ -1809,8 +1843,13 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
                   nullable, o, opts->seed, slots, slot, scratch, scr, work, gwork, gwb, sizes, status, offs, d_out, out_cap,
                   (uint32_t)np, nullptr, 0, 0, nullptr};
     if (is_bool) {
-      ensure_lds_attr(sba::k_enc_bool, (int)lds);
-      hipLaunchKernelGGL(sba::k_enc_bool, dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+      if (o.dflt == sba::C_ZSTD) {
+        ensure_lds_attr(sba::k_enc_bool<true>, (int)lds);
+        hipLaunchKernelGGL(sba::k_enc_bool<true>, dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+      } else {
+        ensure_lds_attr(sba::k_enc_bool<false>, (int)lds);
+        hipLaunchKernelGGL(sba::k_enc_bool<false>, dim3(a.n_batch), dim3(sba::NT), lds, st, a);
+      }
     } else if (flt) {
       if (w == 4) launch_t<4, true, false>(a, lds, st);
       else launch_t<8, true, false>(a, lds, st);
@@ -1930,13 +1969,8 @@ int encode_binary_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, uint6
     sba::AdArgs a{d_values, d_validity, n_rows, (uint32_t)P, (uint32_t)b0, (uint32_t)(b1 - b0), nullable, o,
                   opts->seed, slots, 0, scratch, scr, work, gwork, gwb, sizes, status, offs, d_out, out_cap, (uint32_t)np,
                   d_offsets, values_len, ow, d_soff + batches[b].second};
-    if (ow == 4) {
-      ensure_lds_attr(sba::k_enc_binary<4>, (int)lds);
-      hipLaunchKernelGGL(sba::k_enc_binary<4>, dim3(a.n_batch), dim3(sba::NT), lds, st, a);
-    } else {
-      ensure_lds_attr(sba::k_enc_binary<8>, (int)lds);
-      hipLaunchKernelGGL(sba::k_enc_binary<8>, dim3(a.n_batch), dim3(sba::NT), lds, st, a);
-    }
+    if (ow == 4) launch_bin<4>(a, lds, st);
+    else launch_bin<8>(a, lds, st);
     hipLaunchKernelGGL(sba::k_enc_offsets, dim3(1), dim3(sba::NT), 0, st, a);
     hipLaunchKernelGGL(sba::k_enc_compact, dim3(a.n_batch), dim3(sba::NT), 0, st, a);
     if (const hipError_t e = hipGetLastError(); e != hipSuccess)

@@ -73,3 +73,25 @@ def oracle_decode_column(chunk: bytes, metas, dtype, nullable: bool):
     values = np.concatenate(vals) if vals else np.zeros(0, dtype)
     validity = np.concatenate(valid) if nullable and valid else (np.zeros(0, bool) if nullable else None)
     return values, validity
+
+
+def page_codecs(chunk: bytes, metas, nullable: bool) -> list:
+    """The codec byte of every page of a chunk ([(length, num_values)])."""
+    out, pos = [], 0
+    for length, _ in metas:
+        out.append(O.page_codec(chunk[pos:pos + length], nullable))
+        pos += length
+    return out
+
+
+def same_pages_but_zstd(dev: bytes, dev_metas, host: bytes, host_metas, nullable: bool) -> list:
+    """A Zstd-default chunk from the device encoder against the host writer's:
+    the device's frames come from sb_zstdc.h, not libzstd level 3, so the bar
+    is decode equivalence -- the same pages (row counts) with the same codec
+    choices.  Returns the device's (length, num_values) metas."""
+    dm = [(m.length, m.num_values) for m in dev_metas]
+    hm = [(m.length, m.num_values) for m in host_metas]
+    assert [nv for _, nv in dm] == [nv for _, nv in hm]
+    assert sum(length for length, _ in dm) == len(dev)
+    assert page_codecs(dev, dm, nullable) == page_codecs(host, hm, nullable)
+    return dm
