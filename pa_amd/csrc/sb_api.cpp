@@ -98,6 +98,7 @@ struct sb_plan {
   uint64_t* d_lb = nullptr;   // binary, every page staged: the fused pass's look-back states + counter
   uint32_t bin_grid = 0;      // staged-pass workgroups: the plan pass's staged page count
   uint32_t bin_lds = 0;       // dynamic LDS of the binary kernels (the largest page need, from the plan pass)
+  uint32_t zstd = 1;          // some page has a Zstd stream (0: the decode kernels without the Zstd decoder)
   uint64_t values_bytes = 0;
   uint32_t n_staged = 0, n_global = 0;
   bool staged_identity = false;  // every page staged: no index list
@@ -352,9 +353,9 @@ static hipError_t plan_regions(sb_ctx* ctx, sb_plan* p, std::vector<sb::PageDesc
 
 // LDS a staged Boolean page takes in k_bool_decode: the page, its expanded
 // bitmap and the Zstd decoder's tables.
-static uint64_t bool_lds_need(uint64_t len, uint64_t n) {
+static uint64_t bool_lds_need(uint64_t len, uint64_t n, bool zstd = true) {
   return ((len + 15 + sb::kStagePad + 15) & ~15ull) + (((n + 7) / 8 + 15) & ~15ull) + sb::kStagePad +
-         sb::kZTablesBytes;
+         (zstd ? sb::kZTablesBytes : 0);
 }
 
 // Boolean pages too large for that (max_page_size = None: one page per
@@ -391,7 +392,7 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
 
   std::vector<uint32_t> staged, global;
   uint64_t rows = 0;
-  uint32_t max_stage = 0, max_bool = 0;
+  uint32_t max_stage = 0, max_bool = 0, max_bool_noz = 0;
   bool needs_zero = false;
   for (uint64_t i = 0; i < n_pages; i++) {
     const sb::PageDesc& pd = pages[i];
@@ -403,6 +404,9 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
     if (is_bool)  // page + its expanded bitmap, as k_bool_decode lays them out in LDS (big pages: all of it)
       max_bool = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(max_bool, bool_lds_need(m.length, m.num_values)),
                                               sb::kDeferredLds);
+    if (is_bool)
+      max_bool_noz = (uint32_t)std::min<uint64_t>(
+          std::max<uint64_t>(max_bool_noz, bool_lds_need(m.length, m.num_values, false)), sb::kDeferredLds);
     if (m.length + 16 <= sb::kStageMaxBytes) {
       staged.push_back((uint32_t)i);
       max_stage = std::max<uint32_t>(max_stage, (uint32_t)m.length);
@@ -453,6 +457,24 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
   if (e != hipSuccess) {
     sb_plan_destroy(p);
     return fail(ctx, SB_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
+  }
+  if (!owidth && n_pages) {  // any Zstd stream?  (binary plans learn it from their probe below)
+    uint32_t* d_flag = nullptr;
+    uint32_t flag = 1;
+    e = hipMalloc(&d_flag, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, sizeof(uint32_t), ctx->stream);
+    if (e == hipSuccess && sb::launch_zstd_scan(d_chunk, p->d_pages, (uint32_t)n_pages, is_bool ? 1 : width,
+                                                desc->nullable, d_flag, ctx->stream))
+      e = hipErrorLaunchFailure;
+    if (e == hipSuccess) e = hipMemcpyAsync(&flag, d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (d_flag) (void)hipFree(d_flag);
+    if (e != hipSuccess) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "plan zstd scan: %s", hipGetErrorString(e));
+    }
+    p->zstd = flag ? 1 : 0;
+    if (is_bool && !p->zstd) p->stage_bytes = std::max<uint32_t>(max_bool_noz, 64);
   }
   if (is_bool && n_pages) {
     e = plan_bool_regions(ctx, p, pages);
@@ -512,17 +534,21 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
       uint64_t* d_rneed = nullptr;
       std::vector<uint32_t> need(n_pages);
       std::vector<uint64_t> rneed(n_pages);
+      uint64_t zflag = 1;  // the probe ORs bit 0 for a page with a Zstd stream (into the total's slot)
       e = hipMalloc(&d_need, np * sizeof(uint32_t));
       if (e == hipSuccess) e = hipMalloc(&d_rneed, np * sizeof(uint64_t));
+      if (e == hipSuccess) e = hipMemsetAsync(p->d_bin + 2 * np, 0, sizeof(uint64_t), ctx->stream);
       if (e == hipSuccess) {
-        sb::BinLaunch P{d_chunk, p->d_pages, (uint32_t)n_pages, desc->nullable, nullptr, nullptr, nullptr, nullptr,
-                        nullptr, 0, nullptr, p->d_status, nullptr, nullptr, nullptr, 0, d_need, cls, 1, nullptr,
-                        d_rneed, 0};
+        sb::BinLaunch P{d_chunk, p->d_pages, (uint32_t)n_pages, desc->nullable, nullptr, nullptr, p->d_bin + 2 * np,
+                        nullptr, nullptr, 0, nullptr, p->d_status, nullptr, nullptr, nullptr, 0, d_need, cls, 1,
+                        nullptr, d_rneed, 0};
         if (sb::launch_binary(2, owidth, P, ctx->stream)) e = hipErrorLaunchFailure;
       }
       if (e == hipSuccess) e = hipMemcpyAsync(need.data(), d_need, n_pages * 4, hipMemcpyDeviceToHost, ctx->stream);
       if (e == hipSuccess) e = hipMemcpyAsync(rneed.data(), d_rneed, n_pages * 8, hipMemcpyDeviceToHost, ctx->stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(&zflag, p->d_bin + 2 * np, 8, hipMemcpyDeviceToHost, ctx->stream);
       if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+      p->zstd = (zflag & 1) ? 1 : 0;
       if (d_need) (void)hipFree(d_need);
       if (d_rneed) (void)hipFree(d_rneed);
       uint64_t off = 0;
@@ -548,6 +574,7 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
     sb::BinLaunch L{d_chunk, p->d_pages, (uint32_t)n_pages, desc->nullable, p->d_bin, p->d_bin + np,
                     p->d_bin + 2 * np, nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr,
                     p->bin_lds, nullptr, cls, (uint32_t)std::min<size_t>(np, 65535), p->d_region, nullptr, p->n_big};
+    L.zstd = p->zstd;
     if (sb::launch_binary(0, owidth, L, ctx->stream) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "binary sizing failed: %s", hipGetErrorString(hipGetLastError()));
@@ -613,6 +640,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
                     p->d_bin + 2 * np, (uint8_t*)out->d_offsets, out->d_values, out->values_capacity,
                     (uint32_t*)out->d_validity, p->d_status, p->d_jobs, nullptr, p->d_scratch, p->bin_lds, nullptr,
                     (uint32_t*)(p->d_bin + 2 * np + 2), p->bin_grid, p->d_region, nullptr, p->n_big, p->d_lb};
+    F.zstd = p->zstd;
     if (sb::launch_binary(3, p->offset_width, F, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else {
@@ -622,6 +650,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   sb::BinLaunch S{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
                   nullptr, nullptr, 0, nullptr, p->d_status, p->d_jobs, p->d_defer + 2, nullptr, p->bin_lds, nullptr,
                   (uint32_t*)(p->d_bin + 2 * np + 2), p->bin_grid, p->d_region, nullptr, p->n_big};
+  S.zstd = p->zstd;
   if (sb::launch_binary(0, p->offset_width, S, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "binary sizing launch failed: %s", hipGetErrorString(hipGetLastError()));
   sb::BinLaunch L{p->d_chunk, p->d_pages, (uint32_t)np, p->desc.nullable, p->d_bin, p->d_bin + np, p->d_bin + 2 * np,
@@ -636,6 +665,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
     if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "zstd inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
+  L.zstd = p->zstd;
   if (sb::launch_binary(1, p->offset_width, L, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
@@ -668,6 +698,7 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
     HIP_TRY(ctx, hipMemsetAsync(out->d_values, 0, (p->n_rows + 31) / 32 * 4, ctx->stream));
   if (p->timing) HIP_TRY(ctx, hipEventRecord(p->ev0, ctx->stream));
   sb::LaunchArgs a{};
+  a.zstd = p->zstd;
   a.chunk = p->d_chunk;
   a.pages = p->d_pages;
   a.out_values = (uint8_t*)out->d_values;
@@ -809,6 +840,9 @@ sb_status sb_plan_list_column(sb_ctx* ctx, const sb_list_desc* d, const uint8_t*
   sb_plan* inner = nullptr;
   sb_status st = plan_column(ctx, &cd, d_chunk, chunk_len, h_metas, n_pages, &inner, kRegionsBySize);
   if (st) return st;
+  // the inner plan's pages become the values streams only at decode time (its
+  // plan-time Zstd scan read the list pages): keep the Zstd kernels
+  inner->zstd = 1;
   sb_plan* p = new sb_plan();
   p->desc = cd;
   p->list = true;

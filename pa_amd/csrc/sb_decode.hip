@@ -2058,7 +2058,10 @@ __device__ __forceinline__ bool general_codec(uint32_t c) { return c == 1 || c =
 // fit -- or any leaf of a page too large to stage (xcap 0) -- is queued for
 // k_inflate / k_zinflate to expand into the page's HBM region, sh.defer = 3);
 // MODE 2: spilled pass (that expanded leaf, read from `lsrc` as a None stream).
-template <int W, bool FLT, int MODE, class Src>
+// Z: the instantiation carries the Zstd decoder (sb_zstd.h).  Its out-of-line
+// calls make a kernel take the decoder's registers (245 VGPRs, one wave a
+// SIMD), so plans without Zstd streams launch Z = false kernels.
+template <int W, bool FLT, int MODE, bool Z, class Src>
 __device__ __forceinline__ void decode_page(const Src& s, Shared& sh, const PageDesc& pd, const LaunchArgs& a, uint32_t page,
                             uint8_t* xbuf = nullptr, uint32_t xpos = 0, uint32_t xcap = 0,
                             const GlbSrc* lsrc = nullptr) {
@@ -2172,10 +2175,11 @@ __device__ __forceinline__ void decode_page(const Src& s, Shared& sh, const Page
           uint32_t st = ST_OK;
           if (lf.codec == 1 || lf.codec == 3)
             st = expand_to_lds(lf.codec, a.chunk + pd.byte_off + lf.body, lf.csize, xo, (uint32_t)bytes);
-          else {
+          else if constexpr (Z)
             st = zs::zstd_to_lds(LdsSrc{s.w, s.base + lf.body}, lf.csize, xo, (uint32_t)bytes, xo + zt,
                                  (uint32_t)(xcap - zt));
-          }
+          else
+            st = ST_NYI;  // (a plan with Zstd streams launches the Z kernels)
           if (st) set_err(sh, st);
         }
         __syncthreads();
@@ -2315,7 +2319,7 @@ __global__ __launch_bounds__(NT) void k_decode_staged(LaunchArgs a) {
   if (light_page(a, pd, page)) return;
   const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
   LdsSrc s{(const uint32_t*)stage, base};
-  decode_page<W, FLT, 0>(s, sh, pd, a, page);
+  decode_page<W, FLT, 0, false>(s, sh, pd, a, page);
   __syncthreads();
   if (threadIdx.x == 0 && sh.defer != 1) a.status[page] = sh.err;
 }
@@ -2334,14 +2338,14 @@ __global__ __launch_bounds__(NT) void k_decode_global(LaunchArgs a) {
   }
   if (light_page(a, pd, page)) return;
   GlbSrc s{a.chunk + pd.byte_off};
-  decode_page<W, FLT, 0>(s, sh, pd, a, page);
+  decode_page<W, FLT, 0, false>(s, sh, pd, a, page);
   __syncthreads();
   if (threadIdx.x == 0 && sh.defer != 1) a.status[page] = sh.err;
 }
 
 // Deferred pages (general codecs, Patas): one workgroup per listed page, the
 // page and its expanded leaf stream both in LDS (a.stage_bytes in total).
-template <int W, bool FLT>
+template <int W, bool FLT, bool Z>
 __global__ __launch_bounds__(NT) void k_decode_deferred(LaunchArgs a) {
   extern __shared__ u32x4 stage[];
   __shared__ Shared sh;
@@ -2354,7 +2358,7 @@ __global__ __launch_bounds__(NT) void k_decode_deferred(LaunchArgs a) {
     if (need + 64 > a.stage_bytes) {
       // page too large to stage: parsed from HBM, its leaf spills into the
       // page's region (NYI when the plan reserved none)
-      decode_page<W, FLT, 1>(GlbSrc{a.chunk + pd.byte_off}, sh, pd, a, page);
+      decode_page<W, FLT, 1, Z>(GlbSrc{a.chunk + pd.byte_off}, sh, pd, a, page);
       __syncthreads();
       if (threadIdx.x == 0) a.status[page] = sh.err;
       __syncthreads();
@@ -2363,7 +2367,7 @@ __global__ __launch_bounds__(NT) void k_decode_deferred(LaunchArgs a) {
     const uint32_t base = stage_page(stage, a.chunk + pd.byte_off, pd.byte_len);
     LdsSrc s{(const uint32_t*)stage, base};
     uint8_t* xbuf = (uint8_t*)stage + need;
-    decode_page<W, FLT, 1>(s, sh, pd, a, page, xbuf, (uint32_t)need, a.stage_bytes - (uint32_t)need - kStagePad);
+    decode_page<W, FLT, 1, Z>(s, sh, pd, a, page, xbuf, (uint32_t)need, a.stage_bytes - (uint32_t)need - kStagePad);
     __syncthreads();
     if (threadIdx.x == 0) a.status[page] = sh.err;
     __syncthreads();
@@ -2384,29 +2388,25 @@ __global__ __launch_bounds__(NT) void k_decode_spilled(LaunchArgs a) {
     const PageDesc pd = a.pages[page];
     if (threadIdx.x == 0) sh.err = 0;
     const GlbSrc ls{a.region + (jb.dst & kDstMask)};
-    decode_page<W, FLT, 2>(GlbSrc{a.chunk + pd.byte_off}, sh, pd, a, page, nullptr, 0, 0, &ls);
+    decode_page<W, FLT, 2, false>(GlbSrc{a.chunk + pd.byte_off}, sh, pd, a, page, nullptr, 0, 0, &ls);
     __syncthreads();
     if (threadIdx.x == 0) a.status[page] = sh.err;
     __syncthreads();
   }
 }
 
-// Plan-time cascade probe of a fixed-width page, one thread per page from
-// HBM (the header walk of decode_page without the tables): bit 0 a Freq in
-// the cascade, bit 1 a general-codec / Patas leaf, bit 2 under a Dict / Freq.
-__global__ __launch_bounds__(NT) void k_fix_probe(const uint8_t* chunk, const PageDesc* pages, const uint32_t* list,
-                                                  uint32_t n_list, uint32_t W, int nullable, uint32_t* probe) {
-  const uint32_t i = blockIdx.x * NT + threadIdx.x;
-  if (i >= n_list) return;
-  const PageDesc pd = pages[list[i]];
-  const GlbSrc s{chunk + pd.byte_off};
-  const uint32_t len = pd.byte_len;
+// Plan-time cascade walk of a fixed-width (or Boolean: W 1, one stream) page
+// from HBM, the header walk of decode_page without the tables: bit 0 a Freq
+// in the cascade, bit 1 a general-codec / Patas leaf, bit 2 under a Dict /
+// Freq, bit 3 some stream of the cascade is Zstd.
+__device__ uint32_t fix_cascade(const GlbSrc& s, uint32_t len, uint32_t W, int nullable) {
   uint32_t p = 0, bits = 0;
   auto hdr = [&](uint32_t q, uint32_t* codec, uint32_t* body, uint32_t* cs) {
     if (q + 9 > len) return false;
     *codec = s.u8(q);
     *cs = s.u32(q + 1);
     *body = q + 9;
+    if (*codec == 2) bits |= 8;
     return *cs <= len - *body;
   };
   do {
@@ -2446,7 +2446,29 @@ __global__ __launch_bounds__(NT) void k_fix_probe(const uint8_t* chunk, const Pa
     }
     if (general_codec(leaf)) bits |= 2;
   } while (0);
-  probe[i] = bits;
+  return bits;
+}
+
+// The cascade bits of each listed page (fix_cascade), one thread per page.
+__global__ __launch_bounds__(NT) void k_fix_probe(const uint8_t* chunk, const PageDesc* pages, const uint32_t* list,
+                                                  uint32_t n_list, uint32_t W, int nullable, uint32_t* probe) {
+  const uint32_t i = blockIdx.x * NT + threadIdx.x;
+  if (i >= n_list) return;
+  const PageDesc pd = pages[list[i]];
+  probe[i] = fix_cascade(GlbSrc{chunk + pd.byte_off}, pd.byte_len, W, nullable);
+}
+
+// Plan time: *flag = 1 when some page has a Zstd stream (the plan then
+// launches the kernels that carry the Zstd decoder).
+__global__ __launch_bounds__(NT) void k_zstd_scan(const uint8_t* chunk, const PageDesc* pages, uint32_t n, uint32_t W,
+                                                  int nullable, uint32_t* flag) {
+  const uint32_t i = blockIdx.x * NT + threadIdx.x;
+  bool z = false;
+  if (i < n) {
+    const PageDesc pd = pages[i];
+    z = (fix_cascade(GlbSrc{chunk + pd.byte_off}, pd.byte_len, W, nullable) & 8) != 0;
+  }
+  if (__ballot(z) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 
 template <int W, bool FLT>
@@ -2458,8 +2480,13 @@ static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   if (kind == 2) {
-    ensure_lds_attr(k_decode_deferred<W, FLT>, (int)kDeferredLds);
-    hipLaunchKernelGGL((k_decode_deferred<W, FLT>), dim3(a.n_list), block, a.stage_bytes, stream, a);
+    if (a.zstd) {
+      ensure_lds_attr(k_decode_deferred<W, FLT, true>, (int)kDeferredLds);
+      hipLaunchKernelGGL((k_decode_deferred<W, FLT, true>), dim3(a.n_list), block, a.stage_bytes, stream, a);
+    } else {
+      ensure_lds_attr(k_decode_deferred<W, FLT, false>, (int)kDeferredLds);
+      hipLaunchKernelGGL((k_decode_deferred<W, FLT, false>), dim3(a.n_list), block, a.stage_bytes, stream, a);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   if (a.n_list == 0) return 0;
@@ -2486,18 +2513,29 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = a.count ? *a.count : a.n_jobs;
-  // Jobs are claimed from a counter (a.sched[0]) as waves free up, so the
-  // last wave slots do not idle behind a fixed job-to-wave assignment; the
-  // last wave out (a.sched[1] counts them) zeroes both words for the next
-  // launch on the stream.  Without a.sched: grid-strided.
+  // Wave g takes job g first, with no atomic; later jobs are claimed from a
+  // counter (a.sched[0] + waves) as waves free up, so the last wave slots do
+  // not idle behind a fixed job-to-wave assignment.  Only the min(waves, n)
+  // waves that got a first job take part in the counter's reset (the last of
+  // them out, counted in a.sched[1], zeroes both words for the next launch on
+  // the stream), so a launch with few or no jobs costs no same-address
+  // atomics per idle wave (they serialize in L2: ~11 ns each, 70 us for the
+  // 6144 waves of a full grid).  Without a.sched: grid-strided.
+  const uint32_t waves = gridDim.x * kInfWaves;
   uint32_t j = blockIdx.x * kInfWaves + wv;
+  if (j >= n) return;
   for (bool first = true;; first = false) {
-    if (a.sched) {
-      uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(&a.sched[0], 1u);
-      j = __builtin_amdgcn_readfirstlane(c);  // (every lane is active here: lane 0's claim, in an SGPR)
-    } else if (!first) {
-      j += gridDim.x * kInfWaves;
+    if (!first) {
+      if (a.sched) {
+        uint32_t c = 0;
+        if (lane == 0)
+          c = __hip_atomic_load(&a.sched[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + waves >= n
+                  ? n - waves  // (every job is taken: no claim)
+                  : atomicAdd(&a.sched[0], 1u);
+        j = __builtin_amdgcn_readfirstlane(c) + waves;  // (every lane is active here: lane 0's claim, in an SGPR)
+      } else {
+        j += waves;
+      }
     }
     if (j >= n) break;
     const InflateJob jb = a.jobs[j];
@@ -2548,8 +2586,8 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
     if (st && lane == 0) a.status[jb.page] = st;
     if (kind == 2 && a.ascii && lane == 0) a.ascii[jb.page] = (st == ST_OK && !o.hib) ? 1 : 0;
   }
-  if (a.sched && lane == 0 && atomicAdd(&a.sched[1], 1u) == gridDim.x * kInfWaves - 1) {
-    a.sched[0] = 0;  // every wave has claimed its last job: reset for the next launch
+  if (a.sched && lane == 0 && atomicAdd(&a.sched[1], 1u) == min(waves, n) - 1) {
+    a.sched[0] = 0;  // every taking part wave has claimed its last job: reset for the next launch
     a.sched[1] = 0;
   }
 }
@@ -2900,9 +2938,13 @@ __device__ uint32_t walk_records(const Src& s, uint32_t q, uint32_t end, uint32_
 // One wave expands a general-codec stream (LZ4 / Snappy / Zstd) from HBM
 // into HBM, with k_inflate's per-wave LDS (output ring, input ring, chain
 // tables) or the Zstd decoder's tables.
+template <bool Z>
 __device__ uint32_t expand_to_hbm(uint32_t codec, const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t usize,
                                   uint8_t* lds) {
-  if (codec == 2) return zs::zstd_decode(GlbSrc{src}, csize, dst, usize, (lds_u8*)(lds + kBigZt), kZTablesMax);
+  if (codec == 2) {
+    if constexpr (Z) return zs::zstd_decode(GlbSrc{src}, csize, dst, usize, (lds_u8*)(lds + kBigZt), kZTablesMax);
+    return ST_NYI;
+  }
   WaveOut<true> o;
   o.xf = false;
   o.xadd = 0;
@@ -2939,7 +2981,7 @@ __device__ uint32_t expand_to_hbm(uint32_t codec, const uint8_t* src, uint32_t c
 // filled, then the exceptions (a leaf stream, or a general-codec stream
 // expanded into the xex table first) scattered at their roaring rows.  All
 // NT threads.
-template <class Src>
+template <bool Z, class Src>
 __device__ void materialize_idx(const Src& s, Shared& sh, const BinInfo& bi, TabBase<kLdsSrc<Src>> tb, const Stream ix,
                                 const uint8_t* gpage, uint8_t* lds, uint32_t lds_bytes, uint8_t* biglds,
                                 uint8_t* region) {
@@ -2950,12 +2992,15 @@ __device__ void materialize_idx(const Src& s, Shared& sh, const BinInfo& bi, Tab
   auto expand = [&](uint32_t codec, uint32_t body, uint32_t csize, uint64_t off, uint32_t bytes) -> uint32_t {
     if constexpr (L) {
       lds_u8* dst = (lds_u8*)(lds + bi.tb + off);
-      if (codec == 2)
-        return zs::zstd_to_lds(LdsSrc{s.w, s.base + body}, csize, dst, bytes, (lds_u8*)(lds + bi.ztab),
-                               lds_bytes - bi.ztab - kStagePad);
+      if (codec == 2) {
+        if constexpr (!Z) return ST_NYI;
+        else
+          return zs::zstd_to_lds(LdsSrc{s.w, s.base + body}, csize, dst, bytes, (lds_u8*)(lds + bi.ztab),
+                                 lds_bytes - bi.ztab - kStagePad);
+      }
       return expand_to_lds(codec, gpage + body, csize, dst, bytes);
     } else {
-      return expand_to_hbm(codec, gpage + body, csize, region + off, bytes, biglds);
+      return expand_to_hbm<Z>(codec, gpage + body, csize, region + off, bytes, biglds);
     }
   };
   if (ix.codec == 1 || ix.codec == 2 || ix.codec == 3) {
@@ -3043,7 +3088,7 @@ __device__ void freq_tables(const Src& s, Shared& sh, BinInfo& bi, TabBase<kLdsS
 // walks the k entry records, then the index stream is materialized; S = the
 // page's values bytes, sum of its rows' entry lengths (an index >= k is
 // out of range, dict.rs:131-139 panics).
-template <class Src>
+template <bool Z, class Src>
 __device__ void dict_tables(const Src& s, Shared& sh, BinInfo& bi, TabBase<kLdsSrc<Src>> tb, const Stream& ix,
                             const PageDesc& pd, const uint8_t* gpage, uint8_t* lds, uint32_t lds_bytes, uint8_t* biglds,
                             uint8_t* region, bool sized) {
@@ -3055,7 +3100,7 @@ __device__ void dict_tables(const Src& s, Shared& sh, BinInfo& bi, TabBase<kLdsS
   }
   __syncthreads();
   if (sh.err) return;
-  materialize_idx(s, sh, bi, tb, ix, gpage, lds, lds_bytes, biglds, region);
+  materialize_idx<Z>(s, sh, bi, tb, ix, gpage, lds, lds_bytes, biglds, region);
   if (sh.err || !sized) return;
   const uint32_t k = bi.k;
   mptr<L, uint32_t> xi = tb.template at<uint32_t>(0);
@@ -3415,6 +3460,7 @@ __global__ __launch_bounds__(NT) void k_bin_probe(BinArgs a) {
     const uint32_t len = pd.byte_len, n = pd.num_values;
     uint32_t need = 0;
     uint64_t rneed = 0;
+    bool zpage = false;
     LightPage lp;
     if (!bin_light_parse<OW>(s, len, n, a.nullable, lp)) {
       const uint64_t stage_end = align16((uint64_t)len + 15 + kStagePad);
@@ -3431,6 +3477,7 @@ __global__ __launch_bounds__(NT) void k_bin_probe(BinArgs a) {
       const uint32_t end = body + cs;
       if (ok && codec == 2) {
         nd = kDeferredLds;
+        zpage = true;
       } else if (ok && (codec == BIN_ONE || codec == BIN_DICT || codec == BIN_FREQ)) {
         uint32_t k = 0, tot = 0, xcodec = 0;
         bool zstd = false, xex = false, roar = false;
@@ -3459,6 +3506,7 @@ __global__ __launch_bounds__(NT) void k_bin_probe(BinArgs a) {
             }
           }
         }
+        zpage = zstd;
         const BinLayout L = bin_layout(codec, n, k, tot, xex, false);
         nd = align16(stage_end + L.end) + (zstd ? kZTablesBytes : 0) + kEmitBytes + kStagePad;
         rneed = max<uint64_t>(bin_layout(codec, n, k, tot, xex, roar).end, 16);
@@ -3467,10 +3515,11 @@ __global__ __launch_bounds__(NT) void k_bin_probe(BinArgs a) {
     }
     a.lds_need[page] = need;
     a.rneed[page] = rneed;
+    if (zpage && a.total) atomicOr((unsigned long long*)a.total, 1ull);  // (stage 2: the plan's Zstd flag)
   }
 }
 
-template <int OW>
+template <int OW, bool Z>
 __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
   extern __shared__ u32x4 stage[];
   __shared__ Shared sh;
@@ -3509,7 +3558,7 @@ __global__ __launch_bounds__(NT) void k_bin_size(BinArgs a) {
           a.jobs[slot + 1] = InflateJob{pd.byte_off + bi.vb, kDstBinBase | page, bi.vcs, (uint32_t)bi.S, bi.codec, page};
         }
       } else if (bi.codec == BIN_DICT) {
-        dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, true);
+        dict_tables<Z>(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, true);
       } else if (bi.codec == BIN_FREQ) {
         freq_tables(s, sh, bi, tb, pd, nullptr);
       }
@@ -3654,33 +3703,58 @@ __device__ __forceinline__ void bin_emit_extend(Shared& sh, const Src& s, const 
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 1ull << 63, kLbVal = kLbAgg - 1;
 
 // The values base of `page` from its predecessors' look-back states, wave 0
-// (the single-pass chained scan with a wave-wide look-back: 64 predecessor
-// states per probe; the nearest INCL ends the walk, AGGs before it add up; a
-// page waits only for lower pages, which resident workgroups claimed before
-// it, so every wait ends).  Returns the base in every lane.
+// (the single-pass chained scan with a wave-wide look-back: 4 x 64
+// predecessor states per probe, their loads issued together; the nearest
+// INCL ends the walk, AGGs before it add up; a page waits only for lower
+// pages, which resident workgroups claimed before it, so every wait ends).
+// When every page is resident at once (C5's 1024-page columns) their tables
+// finish together and INCL spreads from page 0 one probe at a time, so a
+// probe covers 256 pages.  The states are the only data exchanged: relaxed
+// agent-scope loads and stores (coherent in L2, no L1 invalidate or L2
+// writeback per probe).  Returns the base in every lane.
 __device__ uint64_t lookback(uint64_t* lb, uint32_t page, uint64_t S) {
+  constexpr uint32_t kProbe = 4;  // windows of 64 states per probe
   const uint32_t lane = threadIdx.x & 63;
   if (page == 0) {
-    if (lane == 0) __hip_atomic_store(&lb[0], kLbIncl | S, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(&lb[0], kLbIncl | S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
-  if (lane == 0) __hip_atomic_store(&lb[page], kLbAgg | S, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_store(&lb[page], kLbAgg | S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint64_t acc = 0;
   for (int64_t top = (int64_t)page - 1;;) {
-    const int64_t j = top - (int64_t)lane;  // lane 0: the nearest predecessor
-    const uint64_t v = j >= 0 ? __hip_atomic_load(&lb[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
-    const uint64_t incl = __ballot((v & kLbIncl) != 0);
-    const uint32_t k = incl ? (uint32_t)__builtin_ctzll(incl) : 63u;  // lanes 0..k decide this probe
-    const uint64_t upto = k == 63 ? ~0ull : ((2ull << k) - 1);
-    if (__ballot(!(v & (kLbAgg | kLbIncl))) & upto) {  // some needed state not published yet
+    uint64_t v[kProbe];
+#pragma unroll
+    for (uint32_t k = 0; k < kProbe; k++) {
+      const int64_t j = top - (int64_t)(64 * k + lane);  // window 0 lane 0: the nearest predecessor
+      v[k] = j >= 0 ? __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+    }
+    // the first INCL in walk order (window k, lane l) ends the walk; every state up to it must be published
+    uint32_t kk = kProbe, kl = 63;
+    bool waiting = false;
+#pragma unroll
+    for (uint32_t k = 0; k < kProbe; k++) {
+      if (kk < kProbe) break;
+      const uint64_t incl = __ballot((v[k] & kLbIncl) != 0);
+      const uint64_t upto = incl ? ((2ull << __builtin_ctzll(incl)) - 1) : ~0ull;
+      if (__ballot(!(v[k] & (kLbAgg | kLbIncl))) & upto) waiting = true;
+      if (incl) {
+        kk = k;
+        kl = (uint32_t)__builtin_ctzll(incl);
+      }
+    }
+    if (waiting) {  // some needed state not published yet
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    acc += wave_sum64(lane <= k ? (v & kLbVal) : 0ull);
-    if (incl) break;
-    top -= 64;
+    uint64_t part = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kProbe; k++)
+      if (k < kk || (k == kk && lane <= kl)) part += v[k] & kLbVal;
+    acc += wave_sum64(part);
+    if (kk < kProbe) break;
+    top -= 64 * kProbe;
   }
-  if (lane == 0) __hip_atomic_store(&lb[page], kLbIncl | (acc + S), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_store(&lb[page], kLbIncl | (acc + S), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return acc;
 }
 
@@ -3696,7 +3770,7 @@ __device__ uint64_t sb_dbg_phase[4096 * 6];
 #define SB_PHASE(k) do { } while (0)
 #endif
 
-template <int OW, bool FUSED>
+template <int OW, bool FUSED, bool Z>
 __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
   extern __shared__ u32x4 stage[];
   __shared__ Shared sh;
@@ -3745,7 +3819,7 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
     if (FUSED) {  // tables (and so the size), then the base
       if (!sh.err) {
         if (bi.codec == BIN_DICT) {
-          dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, true);
+          dict_tables<Z>(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, true);
         } else if (bi.codec == BIN_FREQ) {
           freq_tables(s, sh, bi, tb, pd, nullptr);
           if (!sh.err) freq_rows(s, sh, bi, tb, n);
@@ -3773,7 +3847,9 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
       if (sh.has_valid) write_validity(s, sh.vb_pos, n, R, a.out_validity);
       if (page == 0 && tid == 0) bin_put_off(a.out_offsets, 0, 0, OW);  // Extend codecs push 0 first
       if (bi.codec == 2) {  // Zstd: wave 0 decodes both streams into LDS; they then read as a None page
-        if (tid < 64) {
+        if constexpr (!Z) {
+          if (tid == 0) set_err(sh, ST_NYI);  // (a plan with Zstd streams launches the Z kernels)
+        } else if (tid < 64) {
           const uint32_t tcap = a.lds_bytes - bi.ztab - kStagePad;
           uint32_t r = zs::zstd_to_lds(LdsSrc{s.w, s.base + bi.ob}, bi.ocs, (lds_u8*)(lds + bi.xoff), (n + 1) * OW,
                                        (lds_u8*)(lds + bi.ztab), tcap);
@@ -3826,7 +3902,7 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
       } else {
         if (!FUSED) {
           if (bi.codec == BIN_DICT) {
-            dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, false);
+            dict_tables<Z>(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, lds, a.lds_bytes, nullptr, nullptr, false);
           } else if (bi.codec == BIN_FREQ) {
             freq_tables(s, sh, bi, tb, pd, nullptr);
             if (!sh.err) freq_rows(s, sh, bi, tb, n);
@@ -3842,13 +3918,13 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
   }
 }
 
-template <int OW>
+template <int OW, bool Z>
 __global__ __launch_bounds__(NT) void k_bin_decode(BinArgs a) {
-  bin_decode_pages<OW, false>(a);
+  bin_decode_pages<OW, false, Z>(a);
 }
-template <int OW>
+template <int OW, bool Z>
 __global__ __launch_bounds__(NT) void k_bin_fused(BinArgs a) {
-  bin_decode_pages<OW, true>(a);
+  bin_decode_pages<OW, true, Z>(a);
 }
 
 // Big Extend pages (OneValue / Dict / Freq pages whose tables do not fit one
@@ -3890,7 +3966,7 @@ __global__ __launch_bounds__(NT) void k_bin_big(BinArgs a) {
     if (!sh.err) {
       if (STAGE == 0) {
         if (bi.codec == BIN_DICT) {
-          dict_tables(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, nullptr, 0, lds, rgn, true);
+          dict_tables<true>(s, sh, bi, tb, idx, pd, a.chunk + pd.byte_off, nullptr, 0, lds, rgn, true);
         } else if (bi.codec == BIN_FREQ) {
           freq_tables(s, sh, bi, tb, pd, rgn);
           if (!sh.err) freq_rows(s, sh, bi, tb, n);
@@ -4108,6 +4184,7 @@ __device__ __forceinline__ void set_bit_range(uint32_t* bm, uint64_t b, uint64_t
 // (wave 0, expand_to_hbm) expand into the page's HBM region, which is then
 // funnel-shifted to the page's first row.  `lds` = the dynamic LDS
 // (expand_to_hbm's kBig* layout).
+template <bool Z>
 __device__ void bool_big_page(const LaunchArgs& a, uint32_t page, const PageDesc& pd, Shared& sh, Stream& bs,
                               uint8_t* lds) {
   const uint32_t tid = threadIdx.x, n = pd.num_values, len = pd.byte_len, nb = (n + 7) / 8;
@@ -4156,7 +4233,7 @@ __device__ void bool_big_page(const LaunchArgs& a, uint32_t page, const PageDesc
     case 2:
     case 3:  // LZ4 / Zstd / Snappy over the bitmap bytes
       if (tid < 64) {
-        const uint32_t r = expand_to_hbm(st.codec, a.chunk + pd.byte_off + st.body, st.csize, rg, nb, lds);
+        const uint32_t r = expand_to_hbm<Z>(st.codec, a.chunk + pd.byte_off + st.body, st.csize, rg, nb, lds);
         if (r && tid == 0) set_err(sh, r);
       }
       break;
@@ -4170,6 +4247,7 @@ __device__ void bool_big_page(const LaunchArgs& a, uint32_t page, const PageDesc
   if (!sh.err) write_validity(GlbSrc{rg}, 0, n, pd.row_off, (uint32_t*)a.out_values);
 }
 
+template <bool Z>
 __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
   extern __shared__ u32x4 stage[];
   __shared__ Shared sh;
@@ -4184,7 +4262,7 @@ __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
     if (tid == 0) sh.err = 0;
     if (a.region && pd.reserved) {  // planned as a big page (sb_api plan_bool_regions)
       __syncthreads();
-      bool_big_page(a, page, pd, sh, bs, (uint8_t*)stage);
+      bool_big_page<Z>(a, page, pd, sh, bs, (uint8_t*)stage);
       __syncthreads();
       if (tid == 0) a.status[page] = sh.err;
       __syncthreads();
@@ -4245,11 +4323,11 @@ __global__ __launch_bounds__(NT) void k_bool_decode(LaunchArgs a) {
           break;
         }
         case 2:  // Zstd over the bitmap bytes: wave 0 decodes into LDS, its tables after the bitmap
-          if (need + xb + kZTablesBytes + kStagePad > a.stage_bytes) {
-            if (tid == 0) set_err(sh, ST_NYI);
+          if (!Z || need + xb + kZTablesBytes + kStagePad > a.stage_bytes) {
+            if (tid == 0) set_err(sh, ST_NYI);  // (Z false: a plan with Zstd pages launches the Z kernel)
             break;
           }
-          if (tid < 64) {
+          if constexpr (Z) if (tid < 64) {
             const uint32_t r = zs::zstd_to_lds(LdsSrc{s.w, s.base + st.body}, st.csize, (lds_u8*)xbits, (n + 7) / 8,
                                                (lds_u8*)xbits + xb, a.stage_bytes - need - xb - kStagePad);
             if (r) set_err(sh, r);
@@ -5208,6 +5286,14 @@ int launch_fix_probe(const uint8_t* chunk, const PageDesc* pages, const uint32_t
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int launch_zstd_scan(const uint8_t* chunk, const PageDesc* pages, uint32_t n, int width, int nullable, uint32_t* flag,
+                     void* stream) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(sbk::k_zstd_scan, dim3((n + sbk::NT - 1) / sbk::NT), dim3(sbk::NT), 0, (hipStream_t)stream, chunk,
+                     pages, n, (uint32_t)width, nullable, flag);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_decode_fixed(int width, bool is_float, int kind, const LaunchArgs& a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (is_float) {
@@ -5241,12 +5327,19 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
   const dim3 cgrid((L.n_pages + sbk::NT - 1) / sbk::NT);
   const dim3 lgrid(std::min<uint32_t>(L.n_pages, 65535u));
   const dim3 bgrid(std::max<uint32_t>(1, std::min<uint32_t>(L.n_big, 1024u)));
-  ensure_lds_attr(sbk::k_bin_size<4>, (int)kDeferredLds);
-  ensure_lds_attr(sbk::k_bin_size<8>, (int)kDeferredLds);
-  ensure_lds_attr(sbk::k_bin_decode<4>, (int)kDeferredLds);
-  ensure_lds_attr(sbk::k_bin_decode<8>, (int)kDeferredLds);
-  ensure_lds_attr(sbk::k_bin_fused<4>, (int)kDeferredLds);
-  ensure_lds_attr(sbk::k_bin_fused<8>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_size<4, true>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_size<8, true>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_decode<4, true>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_decode<8, true>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_fused<4, true>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_fused<8, true>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_size<4, false>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_size<8, false>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_decode<4, false>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_decode<8, false>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_fused<4, false>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bin_fused<8, false>, (int)kDeferredLds);
+  const bool z = L.zstd != 0;
   if (stage == 2) {  // plan time: per-page LDS / region needs
     if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_probe<8>, cgrid, block, 0, st, a);
     else hipLaunchKernelGGL(sbk::k_bin_probe<4>, cgrid, block, 0, st, a);
@@ -5254,25 +5347,34 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
     if (hipMemsetAsync(L.cls + 4 * (size_t)L.n_pages, 0, 3 * sizeof(uint32_t), st) != hipSuccess) return -1;
     if (offset_width == 8) {
       hipLaunchKernelGGL(sbk::k_bin_light<8>, cgrid, block, 0, st, a);
-      hipLaunchKernelGGL(sbk::k_bin_size<8>, grid, block, lds, st, a);
+      if (z) hipLaunchKernelGGL((sbk::k_bin_size<8, true>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((sbk::k_bin_size<8, false>), grid, block, lds, st, a);
       if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<8, 0>), bgrid, block, sbk::kBigLds, st, a);
     } else {
       hipLaunchKernelGGL(sbk::k_bin_light<4>, cgrid, block, 0, st, a);
-      hipLaunchKernelGGL(sbk::k_bin_size<4>, grid, block, lds, st, a);
+      if (z) hipLaunchKernelGGL((sbk::k_bin_size<4, true>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((sbk::k_bin_size<4, false>), grid, block, lds, st, a);
       if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<4, 0>), bgrid, block, sbk::kBigLds, st, a);
     }
     hipLaunchKernelGGL(sbk::k_bin_scan, dim3(1), block, 0, st, a);
   } else if (stage == 3) {  // every page staged: size, base and decode in one pass
     if (hipMemsetAsync(L.lb, 0, (L.n_pages + 1) * sizeof(uint64_t), st) != hipSuccess) return -1;
-    if (offset_width == 8) hipLaunchKernelGGL(sbk::k_bin_fused<8>, grid, block, lds, st, a);
-    else hipLaunchKernelGGL(sbk::k_bin_fused<4>, grid, block, lds, st, a);
+    if (offset_width == 8) {
+      if (z) hipLaunchKernelGGL((sbk::k_bin_fused<8, true>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((sbk::k_bin_fused<8, false>), grid, block, lds, st, a);
+    } else {
+      if (z) hipLaunchKernelGGL((sbk::k_bin_fused<4, true>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((sbk::k_bin_fused<4, false>), grid, block, lds, st, a);
+    }
   } else {
     if (offset_width == 8) {
-      hipLaunchKernelGGL(sbk::k_bin_decode<8>, grid, block, lds, st, a);
+      if (z) hipLaunchKernelGGL((sbk::k_bin_decode<8, true>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((sbk::k_bin_decode<8, false>), grid, block, lds, st, a);
       if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<8, 1>), bgrid, block, sbk::kBigLds, st, a);
       hipLaunchKernelGGL(sbk::k_bin_light_out<8>, lgrid, block, 0, st, a);
     } else {
-      hipLaunchKernelGGL(sbk::k_bin_decode<4>, grid, block, lds, st, a);
+      if (z) hipLaunchKernelGGL((sbk::k_bin_decode<4, true>), grid, block, lds, st, a);
+      else hipLaunchKernelGGL((sbk::k_bin_decode<4, false>), grid, block, lds, st, a);
       if (L.n_big) hipLaunchKernelGGL((sbk::k_bin_big<4, 1>), bgrid, block, sbk::kBigLds, st, a);
       hipLaunchKernelGGL(sbk::k_bin_light_out<4>, lgrid, block, 0, st, a);
     }
@@ -5360,9 +5462,11 @@ int launch_zinflate(const InflateLaunch& a, void* stream) {
 namespace sb {
 int launch_bool(const LaunchArgs& a, void* stream) {
   if (a.n_list == 0) return 0;
-  ensure_lds_attr(sbk::k_bool_decode, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bool_decode<true>, (int)kDeferredLds);
+  ensure_lds_attr(sbk::k_bool_decode<false>, (int)kDeferredLds);
   const uint32_t grid = std::min<uint32_t>(a.n_list, 65535u);
-  hipLaunchKernelGGL(sbk::k_bool_decode, dim3(grid), dim3(sbk::NT), a.stage_bytes, (hipStream_t)stream, a);
+  if (a.zstd) hipLaunchKernelGGL(sbk::k_bool_decode<true>, dim3(grid), dim3(sbk::NT), a.stage_bytes, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(sbk::k_bool_decode<false>, dim3(grid), dim3(sbk::NT), a.stage_bytes, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace sb

@@ -127,6 +127,8 @@ struct LaunchArgs {
   uint8_t* region;        // the plan's HBM regions (PageDesc.reserved), or nullptr
   uint32_t* spill_count;  // [2]: spilled leaf jobs, double-buffered like defer_count
   InflateJob* spill_jobs; // leaves expanded into regions by k_inflate / k_zinflate, then k_decode_spilled
+  uint32_t zstd = 1;      // 0: no page of the plan has a Zstd stream (kernels without the decoder, whose
+                          // out-of-line calls would take 245 VGPRs: one wave a SIMD)
 };
 
 // kind: 0 = LDS-staged pages, 1 = pages read from HBM, 2 = deferred work list,
@@ -140,6 +142,10 @@ int launch_fix_probe(const uint8_t* chunk, const PageDesc* pages, const uint32_t
 // Header-only fixed-width pages (LZ4 / Snappy leaf, Float Patas leaf): their
 // inflate jobs and light[] tags, one thread per page, before the staged pass.
 int launch_fix_light(const LaunchArgs& a, uint32_t n_pages, int width, bool is_float, uint32_t* light, void* stream);
+// Plan time: *flag |= 1 when a fixed-width or Boolean page (width 1, one
+// stream) has a Zstd stream anywhere in its cascade.
+int launch_zstd_scan(const uint8_t* chunk, const PageDesc* pages, uint32_t n, int width, int nullable, uint32_t* flag,
+                     void* stream);
 
 // Boolean pages: one workgroup per page (grid-strided), page + expanded
 // bitmap in a.stage_bytes of dynamic LDS.
@@ -178,6 +184,8 @@ struct BinLaunch {
   uint64_t* rneed;        // stage 2 (plan time) out: region bytes per page; lds_need: LDS bytes per page
   uint32_t n_big;         // big pages of the plan (0: their kernels are not launched)
   uint64_t* lb;           // stage 3: look-back states (n_pages) + page counter
+  uint32_t zstd = 1;      // 0: no page has a Zstd stream (the kernels without the decoder, LaunchArgs::zstd);
+                          // stage 2 reports it through `total` (bit 0 set by a page with a Zstd stream)
 };
 // stage 2: plan-time probe (lds_need / rneed per page); stage 3: the fused
 // single pass when every page is staged (sizes, bases, offsets, values).

@@ -37,6 +37,17 @@ def main():
         print(f"{kind}: pages {len(metas)} span {span:.1f} us; per page median us: stage+parse {np.median(dt[:, 0]):.1f} "
               f"tables {np.median(dt[:, 1]):.1f} lookback {np.median(dt[:, 2]):.1f} emit {np.median(dt[:, 3]):.1f}; "
               f"p90 lookback {np.percentile(dt[:, 2], 90):.1f}", flush=True)
+        t0 = a[:, 0].min()
+        st, en = (a[:, 0] - t0) / 100.0, (a[:, 4] - t0) / 100.0
+        ev = sorted([(x, 1) for x in st] + [(x, -1) for x in en])
+        cur = peak = 0
+        for _, d_ in ev:
+            cur += d_
+            peak = max(peak, cur)
+        tot = en - st
+        print(f"    peak pages in flight {peak}; page total us mean {tot.mean():.1f} p10 {np.percentile(tot, 10):.1f} "
+              f"p90 {np.percentile(tot, 90):.1f} max {tot.max():.1f}; starts at us: p50 {np.percentile(st, 50):.1f} "
+              f"p90 {np.percentile(st, 90):.1f} last {st.max():.1f}; ends p50 {np.percentile(en, 50):.1f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -1,6 +1,8 @@
 """Config-5 decode units timed alone (median of 5 solo decodes, host clock
 around decode + device synchronize), then the 4-stream step:
-python tools/c5units.py [rows]"""
+python tools/c5units.py [rows].  Each unit's solo decodes are separated by
+10 ms of idle device, so a kernel trace of this run splits into units by its
+gaps (tools/unit_kernels.py); the encode comes first."""
 import os
 import sys
 import time
@@ -26,6 +28,7 @@ def main():
         ts = []
         for _ in range(5):
             torch.cuda.synchronize()
+            time.sleep(0.01)
             t0 = time.perf_counter()
             dec.decode_async(*outs)
             torch.cuda.synchronize()
