@@ -398,12 +398,11 @@ class StreamSet:
 
     def __init__(self, torch, pa, device, n):
         self.torch = torch
-        self.streams = [torch.cuda.Stream(device=device) for _ in range(n)]
-        self.ctxs = []
-        for st in self.streams:
-            c = pa.Context(device)
-            c.use_stream(st)
-            self.ctxs.append(c)
+        # each context on its own HIP stream: contexts made one after another
+        # get distinct hardware queues (pa.Context.use_own_stream); torch's
+        # pooled side streams were seen sharing two queues among four
+        self.ctxs = [pa.Context(device) for _ in range(n)]
+        self.streams = [c.use_own_stream() for c in self.ctxs]
         torch.cuda.synchronize()
 
     def fork(self):

@@ -1352,6 +1352,105 @@ __global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
 
 
 // ---------------------------------------------------------------------------
+// Basic pages of a default LZ4 / Zstd codec that need no statistics (ratio
+// None, no forced codec: choose_compressor returns the default codec,
+// integer/mod.rs:267-307, binary/mod.rs:302-348): the page is the validity
+// prefix and one headered stream of the raw values (BIN: two -- the offsets
+// rebased to the page's first value, then the values), and the whole work is
+// the one-wave LZ4 parse.  One 64-lane workgroup a page with only the LZ4
+// tables in LDS: six pages a CU, where a 256-thread page workgroup of the
+// general kernels holds three idle waves (and the register file for them) --
+// C5's four LZ4 columns then overlap the rest of the table.  Bytes identical
+// to k_enc_adaptive / k_enc_binary (write_prefix, enc_stream, basic_body).
+// W: the value width (fixed-width pages) or the offset width (BIN).
+template <int W, bool BIN, bool ZS>
+__global__ __launch_bounds__(64) void k_enc_basic_wave(AdArgs A) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t p = A.page0 + blockIdx.x;
+  const uint64_t r0 = (uint64_t)p * A.P;
+  const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
+  uint8_t* out = slot_of(A, blockIdx.x);
+  const uint64_t cap = slot_cap(A, blockIdx.x);
+  const int codec = A.o.dflt;
+  sbc::lz4_lds8* tab = (sbc::lz4_lds8*)lds;
+  uint32_t err = E_OK;
+  uint32_t pos = 0;
+  if (A.nullable) {  // write_prefix (serialize.rs:200-215), one wave
+    const uint32_t nb = (n + 7) / 8;
+    uint64_t h = ((uint64_t)nb << 1) | 1;
+    const uint32_t hl = uleb_len(h);
+    if (4 + hl + nb > cap) {
+      err = E_CAP;
+    } else {
+      if (lane == 0) {
+        put8(out, hl + nb, 4);
+        for (uint32_t j = 0; j < hl; j++, h >>= 7) out[4 + j] = (uint8_t)((h & 0x7F) | (j + 1 < hl ? 0x80 : 0));
+      }
+      for (uint32_t j = lane; j < nb; j += 64) {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 8; b++) {
+          const uint32_t i = 8 * j + b;
+          const bool ok = i < n && (!A.validity || ((A.validity[(r0 + i) >> 3] >> ((r0 + i) & 7)) & 1));
+          v |= (ok ? 1u : 0u) << b;
+        }
+        out[4 + hl + j] = (uint8_t)v;
+      }
+      pos = 4 + hl + nb;
+    }
+  }
+  // one headered stream of src[0, len) at `at` ([codec][csize][usize][body]); returns its end
+  auto stream = [&](const uint8_t* src, uint32_t len, uint32_t at) -> uint32_t {
+    const uint32_t body = at + 9;
+    uint32_t cs = 0;
+    if (codec == C_LZ4) {
+      if ((uint64_t)body + sbc::lz4_bound(len) > cap) {
+        err = E_CAP;
+        return at;
+      }
+      for (uint32_t i = lane; i < 4096; i += 64) ((__attribute__((address_space(3))) uint32_t*)tab)[i] = 0;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the table's zeroes land before its reads
+      __builtin_amdgcn_wave_barrier();
+      cs = sbc::lz4_compress_wave(src, len, out + body, tab);
+    } else if constexpr (ZS) {
+      const uint64_t zb = sbz::zstd_bound(len);
+      if ((uint64_t)body + zb + sbc::lz4_bound(min(len, sbz::kZChunk)) + 16 > cap) {
+        err = E_CAP;
+        return at;
+      }
+      cs = __builtin_amdgcn_readfirstlane(zstd_frame_wave(src, len, out + body, out + body + zb, tab));  // (lane 0's)
+    } else {
+      err = E_NYI;  // (the host launches the ZS instantiation for a Zstd default codec)
+      return at;
+    }
+    if (lane == 0) {
+      out[at] = (uint8_t)codec;
+      put8(out + at + 1, cs, 4);
+      put8(out + at + 5, len, 4);
+    }
+    return body + cs;
+  };
+  if (!err) {
+    if constexpr (!BIN) {
+      pos = stream(A.values + r0 * W, n * W, pos);
+    } else {
+      // offsets rebased to the page's first value (the page's scratch), then the values
+      const int64_t base = A.offsets[r0];
+      uint8_t* obuf = A.scratch + (uint64_t)blockIdx.x * A.scratch_bytes;
+      for (uint32_t i = lane; i <= n; i += 64) put8(obuf + i * W, (uint64_t)(A.offsets[r0 + i] - base), W);
+      __threadfence_block();  // (the wave's stores before its loads of them)
+      __builtin_amdgcn_wave_barrier();
+      pos = stream(obuf, (n + 1) * W, pos);
+      if (!err) pos = stream(A.values + base, (uint32_t)(A.offsets[r0 + n] - base), pos);
+    }
+  }
+  if (lane == 0) {
+    A.sizes[p] = err ? 0 : pos;
+    A.status[p] = err;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Binary / Utf8 pages: compress_binary (compression/binary/mod.rs:26-93) --
 // gen_stats (:265-300: distinct strings over every slot, nulls, the bytes of
 // the distinct strings + 8 each, the most frequent string), choose_compressor
@@ -1770,8 +1869,29 @@ static uint32_t batch_pages(uint64_t np, uint64_t per_page) {
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({np, 2048, (2ull << 30) / std::max<uint64_t>(per_page, 1)}));
 }
 
+// A Basic page of a default LZ4 / Zstd codec without statistics: the
+// one-wave page kernel (k_enc_basic_wave), LDS = the LZ4 tables.
+static bool wave_basic(const sba::Opts& o) {
+  return !sba::needs_stats(o, o.forbidden) && (o.dflt == sba::C_LZ4 || o.dflt == sba::C_ZSTD);
+}
+template <int W, bool BIN>
+static void launch_wave_basic(const sba::AdArgs& a, hipStream_t st) {
+  constexpr uint32_t lds = sbc::kLz4WaveLds;
+  if (a.o.dflt == sba::C_ZSTD) {
+    ensure_lds_attr(sba::k_enc_basic_wave<W, BIN, true>, (int)lds);
+    hipLaunchKernelGGL((sba::k_enc_basic_wave<W, BIN, true>), dim3(a.n_batch), dim3(64), lds, st, a);
+  } else {
+    ensure_lds_attr(sba::k_enc_basic_wave<W, BIN, false>, (int)lds);
+    hipLaunchKernelGGL((sba::k_enc_basic_wave<W, BIN, false>), dim3(a.n_batch), dim3(64), lds, st, a);
+  }
+}
+
 template <int W, bool FLT, bool SGN>
 static void launch_t(const sba::AdArgs& a, uint32_t lds, hipStream_t st) {
+  if (wave_basic(a.o)) {
+    launch_wave_basic<W, false>(a, st);
+    return;
+  }
   if (a.o.dflt == sba::C_ZSTD) {
     ensure_lds_attr(sba::k_enc_adaptive<W, FLT, SGN, true>, (int)lds);
     hipLaunchKernelGGL((sba::k_enc_adaptive<W, FLT, SGN, true>), dim3(a.n_batch), dim3(sba::NT), lds, st, a);
@@ -1782,6 +1902,10 @@ static void launch_t(const sba::AdArgs& a, uint32_t lds, hipStream_t st) {
 }
 template <int OW>
 static void launch_bin(const sba::AdArgs& a, uint32_t lds, hipStream_t st) {
+  if (wave_basic(a.o)) {
+    launch_wave_basic<OW, true>(a, st);
+    return;
+  }
   if (a.o.dflt == sba::C_ZSTD) {
     ensure_lds_attr(sba::k_enc_binary<OW, true>, (int)lds);
     hipLaunchKernelGGL((sba::k_enc_binary<OW, true>), dim3(a.n_batch), dim3(sba::NT), lds, st, a);

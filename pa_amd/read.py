@@ -128,11 +128,23 @@ class Context:
         if st:
             raise N.StrawboatError(st, f"sb_ctx_create(device={device}) failed: no usable GPU")
         self._h = h
+        self._own = N.lib().sb_ctx_stream(h)  # the context's own HIP stream (non-blocking)
         with torch.cuda.device(device):
             self.use_stream(torch.cuda.current_stream(device))
 
     def use_stream(self, stream):
         N.lib().sb_ctx_set_stream(self._h, ctypes.c_void_p(stream.cuda_stream))
+
+    def use_own_stream(self):
+        """Launch on the context's own HIP stream; returns it as a torch
+        ExternalStream (for wait_stream / stream contexts).  Contexts created
+        one after another get their own streams on distinct hardware queues
+        (the runtime spreads new streams over its queues), where torch's
+        pooled side streams may share one -- independent columns then
+        really run side by side."""
+        st = self._torch.cuda.ExternalStream(self._own, device=self.device)
+        self.use_stream(st)
+        return st
 
     def error(self) -> str:
         return N.lib().sb_last_error(self._h).decode()

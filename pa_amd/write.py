@@ -167,11 +167,9 @@ def _table_contexts(device: int, n: int):
     key = (device, n)
     if key not in _table_ctx:
         ctxs = []
-        for _ in range(n):
-            st = torch.cuda.Stream(device=device)
+        for _ in range(n):  # (own streams: on distinct hardware queues, Context.use_own_stream)
             c = Context(device)
-            c.use_stream(st)
-            ctxs.append((c, st))
+            ctxs.append((c, c.use_own_stream()))
         _table_ctx[key] = ctxs
     return _table_ctx[key]
 

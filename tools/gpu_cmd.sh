@@ -1,3 +1,4 @@
-bash tools/gpu_tests.sh z2 -m gpu tests/test_gpu_binary.py tests/test_gpu_binary_errors.py tests/test_gpu_configs.py tests/test_gpu_table.py tests/test_gpu_utf8.py tests/test_gpu_shard.py > /dev/null; rc=$?; tail -3 gpurun_out/z2.log; [ $rc = 0 ] || exit $rc
-PA_AMD_LIB=pa_amd/variants/libsb_phases.so timeout -k 10 200 python tools/binphases.py 2>&1 | grep -v amdgpu.ids
-timeout -k 10 200 python tools/c5units.py > gpurun_out/z2_c5units.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/z2_c5units.log; exit $rc
+bash tools/gpu_tests.sh w1 -m gpu tests/test_gpu_encode.py tests/test_gpu_encode_adaptive.py tests/test_gpu_encode_binary_bool.py tests/test_lz4c.py > /dev/null; rc=$?; tail -2 gpurun_out/w1.log; [ $rc = 0 ] || exit $rc
+bash tools/gpu_r04.sh prof c5e3 tools/c5enc.py > /dev/null; grep "c5 encode" gpurun_out/c5e3_kt.log
+timeout -k 10 300 python bench.py --no-cpu --no-b12 --no-hard --no-c3 --no-c4 --no-file --no-c5 --steps 5 > gpurun_out/w1_bench.json 2>&1; python -c "
+import json; d=json.loads(open('gpurun_out/w1_bench.json').read().strip().splitlines()[-1]); print(json.dumps(d.get('encode_gpu')))"
