@@ -398,11 +398,17 @@ class StreamSet:
 
     def __init__(self, torch, pa, device, n):
         self.torch = torch
-        # each context on its own HIP stream: contexts made one after another
-        # get distinct hardware queues (pa.Context.use_own_stream); torch's
-        # pooled side streams were seen sharing two queues among four
         self.ctxs = [pa.Context(device) for _ in range(n)]
-        self.streams = [c.use_own_stream() for c in self.ctxs]
+        if os.environ.get("SB_BENCH_STREAMS", "torch") == "own":
+            # each context on its own HIP stream (pa.Context.use_own_stream):
+            # measured slower for C5 (3.39 vs 2.74 ms/step) -- the four
+            # streams then run on four hardware queues at once and the LZ4 /
+            # Patas units contend with the rest
+            self.streams = [c.use_own_stream() for c in self.ctxs]
+        else:  # torch's pooled side streams
+            self.streams = [torch.cuda.Stream(device=device) for _ in range(n)]
+            for c, st in zip(self.ctxs, self.streams):
+                c.use_stream(st)
         torch.cuda.synchronize()
 
     def fork(self):

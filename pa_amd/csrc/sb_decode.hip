@@ -2513,29 +2513,28 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = a.count ? *a.count : a.n_jobs;
-  // Wave g takes job g first, with no atomic; later jobs are claimed from a
-  // counter (a.sched[0] + waves) as waves free up, so the last wave slots do
-  // not idle behind a fixed job-to-wave assignment.  Only the min(waves, n)
-  // waves that got a first job take part in the counter's reset (the last of
-  // them out, counted in a.sched[1], zeroes both words for the next launch on
-  // the stream), so a launch with few or no jobs costs no same-address
-  // atomics per idle wave (they serialize in L2: ~11 ns each, 70 us for the
-  // 6144 waves of a full grid).  Without a.sched: grid-strided.
-  const uint32_t waves = gridDim.x * kInfWaves;
+  // Jobs are claimed from a counter (a.sched[0]) as waves free up, so the
+  // last wave slots do not idle behind a fixed job-to-wave assignment (a
+  // static first job per wave measured 2.14 -> 2.55 ms on C3's Utf8 column).
+  // Only the first min(waves, n) waves take part; the others leave at once,
+  // so a launch with few or no jobs costs no same-address atomics per idle
+  // wave (they serialize in L2, ~11 ns each: a full grid of 6144 waves spent
+  // 70-140 us on a launch with no jobs).  The last taking-part wave out
+  // (a.sched[1] counts them) zeroes both words for the next launch on the
+  // stream.  (Reading the counter before each claim, to skip claims once
+  // every job is taken, measured 2.14 -> 2.7 ms on that column: the loads
+  // queue behind the claims on the one L2 line.)  Without a.sched:
+  // grid-strided.
+  const uint32_t waves = gridDim.x * kInfWaves, part = min(waves, n);
   uint32_t j = blockIdx.x * kInfWaves + wv;
-  if (j >= n) return;
+  if (j >= part) return;
   for (bool first = true;; first = false) {
-    if (!first) {
-      if (a.sched) {
-        uint32_t c = 0;
-        if (lane == 0)
-          c = __hip_atomic_load(&a.sched[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + waves >= n
-                  ? n - waves  // (every job is taken: no claim)
-                  : atomicAdd(&a.sched[0], 1u);
-        j = __builtin_amdgcn_readfirstlane(c) + waves;  // (every lane is active here: lane 0's claim, in an SGPR)
-      } else {
-        j += waves;
-      }
+    if (a.sched) {
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(&a.sched[0], 1u);
+      j = __builtin_amdgcn_readfirstlane(c);  // (every lane is active here: lane 0's claim, in an SGPR)
+    } else if (!first) {
+      j += waves;
     }
     if (j >= n) break;
     const InflateJob jb = a.jobs[j];
@@ -2586,7 +2585,7 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
     if (st && lane == 0) a.status[jb.page] = st;
     if (kind == 2 && a.ascii && lane == 0) a.ascii[jb.page] = (st == ST_OK && !o.hib) ? 1 : 0;
   }
-  if (a.sched && lane == 0 && atomicAdd(&a.sched[1], 1u) == min(waves, n) - 1) {
+  if (a.sched && lane == 0 && atomicAdd(&a.sched[1], 1u) == part - 1) {
     a.sched[0] = 0;  // every taking part wave has claimed its last job: reset for the next launch
     a.sched[1] = 0;
   }
