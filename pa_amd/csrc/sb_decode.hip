@@ -1669,8 +1669,14 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
 //     by pointer jumping across lanes (6 rounds of ds_bpermute);
 //  3. the block's values go to the ring and, coalesced, to HBM.
 // The first bad record decides the status, as in the reference's loop.
+// The stream is read through k_inflate's 1 KiB LDS input ring (InRing: the
+// next 512 bytes loaded ahead in registers), slid to each window's start:
+// a block's headers and records lie within ~650 bytes of it, so they are LDS
+// reads; the rare byte past the staged KiB is read from HBM (the same
+// clamped dwords).  (Read from HBM directly, a 64-row block cost three
+// dependent HBM round trips: 0.37 ms for a C5 Float64 Patas column.)
 template <int W>
-__device__ uint32_t patas_wave(const uint8_t* src, uint32_t ilen, uint8_t* dst, uint32_t n, lds_u8* ring) {
+__device__ uint32_t patas_wave(const uint8_t* src, uint32_t ilen, uint8_t* dst, uint32_t n, lds_u8* ring, lds_u8* ibuf) {
   using T = typename VT<W>::T;
   const uint32_t lane = threadIdx.x & 63;
   if (n == 0) return ST_OUT_OF_SPEC;  // `length - 1` underflows (patas.rs:117)
@@ -1678,12 +1684,21 @@ __device__ uint32_t patas_wave(const uint8_t* src, uint32_t ilen, uint8_t* dst, 
   gmem_u32* g = (gmem_u32*)((uintptr_t)src & ~(uintptr_t)3);
   const uint32_t sb0 = (uint32_t)((uintptr_t)src & 3);
   const uint32_t nd = (sb0 + ilen + 3) >> 2;
+  InRing in;
+  in.g = g;
+  in.nd = nd;
+  in.ib = ibuf;
+  in.ct = nullptr;
+  in.seek(sb0);
+  typedef __attribute__((address_space(3))) uint32_t l32;
+  const l32* ib32 = (const l32*)ibuf;
   auto dw = [&](uint32_t i) -> uint32_t { return g[min(i, nd - 1)]; };
   auto bytes4 = [&](uint32_t pos) -> uint32_t {  // the 4 stream bytes at pos (clamped at the end)
     const uint32_t a = sb0 + pos, i = a >> 2;
+    if (((i + 1) << 2) - in.base < kIb && (i << 2) >= in.base)
+      return __builtin_amdgcn_alignbyte(ib32[(i + 1) & (kIb / 4 - 1)], ib32[i & (kIb / 4 - 1)], a & 3);
     return __builtin_amdgcn_alignbyte(dw(i + 1), dw(i), a & 3);
   };
-  typedef __attribute__((address_space(3))) uint32_t l32;
   l32* rlo = (l32*)ring;
   l32* rhi = rlo + 256;
   const uint32_t f_lo = bytes4(0), f_hi = W == 8 ? bytes4(4) : 0u;
@@ -1692,6 +1707,7 @@ __device__ uint32_t patas_wave(const uint8_t* src, uint32_t ilen, uint8_t* dst, 
     const uint32_t r_end = min(b0 + 64, n);
     uint32_t i = b0 ? b0 : 1, start = 0, cerr = 0;
     while (i < r_end && !cerr) {  // record starts of rows [i, r_end), a window at a time
+      in.slide(sb0 + q);
       uint32_t t1 = 0, dr = 0, ec = 0;
       {
         const uint32_t w4 = bytes4(q + 4 * lane), w5 = bytes4(q + 4 * lane + 4);
@@ -2578,8 +2594,8 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
       st = snappy_wave<true>(w, p0, p0 + jb.csize, o);
     } else if ((jb.codec & 0xFF) == 16) {  // Patas leaf: codec 16 | width << 8
       const uint32_t W = jb.codec >> 8;
-      st = W == 8 ? patas_wave<8>(src, jb.csize, dst, jb.usize / 8, o.ring)
-                  : patas_wave<4>(src, jb.csize, dst, jb.usize / 4, o.ring);
+      st = W == 8 ? patas_wave<8>(src, jb.csize, dst, jb.usize / 8, o.ring, (lds_u8*)&ibufs[wv][0])
+                  : patas_wave<4>(src, jb.csize, dst, jb.usize / 4, o.ring, (lds_u8*)&ibufs[wv][0]);
     }
 #endif
     if (st && lane == 0) a.status[jb.page] = st;
