@@ -3523,7 +3523,13 @@ __global__ __launch_bounds__(NT) void k_bin_probe(BinArgs a) {
         }
         zpage = zstd;
         const BinLayout L = bin_layout(codec, n, k, tot, xex, false);
+#ifdef SB_BIN_EMIT_BLOCK
         nd = align16(stage_end + L.end) + (zstd ? kZTablesBytes : 0) + kEmitBytes + kStagePad;
+#else
+        // (as bin_parse: staged pages emit through bin_emit_wave, no LDS window --
+        // the 8 KiB window held C5's Dict pages at two workgroups a CU)
+        nd = align16(stage_end + L.end) + (zstd ? kZTablesBytes : 0) + kStagePad;
+#endif
         rneed = max<uint64_t>(bin_layout(codec, n, k, tot, xex, roar).end, 16);
       }
       need = (uint32_t)min<uint64_t>(nd, 0xFFFFFFFFull);
