@@ -1,6 +1,8 @@
 // sb_zstd.h -- one-wave Zstd frame decoder (RFC 8878) into LDS: the Zstd leg
-// of CommonCompression (compression/basic.rs:93-97, one frame whose
-// decompressed size is the page header's usize).  The reference calls
+// of CommonCompression (compression/basic.rs:93-97: the frames whose
+// decompressed sizes add up to the page header's usize -- the writer emits
+// one; ZSTD_decompress also takes several, skippable frames between them and
+// content checksums, verified here with XXH64).  The reference calls
 // libzstd 1.4.8 (zstd 0.11 crate); the checks below follow that library's
 // acceptance rules so a page the reference rejects is rejected here.
 //
@@ -11,7 +13,7 @@
 //   * the (up to 4) Huffman literal streams are decoded by lanes 0..3, the
 //     literals landing at the TAIL of the output window (olen - litSize):
 //     every sequence writes below the literals it has not read yet, since the
-//     frame's output is exactly olen bytes (op + ml <= lp is checked anyway);
+//     frames' output is exactly olen bytes (op + ml <= lp is checked anyway);
 //   * sequences are decoded by lane 0 in batches of 64 and executed by the
 //     whole wave: literal copies and matches sourced before the batch in
 //     parallel (one sequence per lane), the rest in order, 64 bytes a step.
@@ -454,7 +456,63 @@ __device__ void exec_batch(O out, const Tabs& t, uint32_t cnt, uint32_t op0, uin
   }
 }
 
-// Decode one Zstd frame of csize bytes (in[0, csize)) into out[0, olen).
+// XXH64 (seed 0) of out[s, s + len), low 32 bits: the frame content
+// checksum (RFC 8878 3.1.1).  Lanes 0-3 run the four stripe accumulators,
+// every lane the (uniform) merge and tail.
+constexpr uint64_t kX1 = 11400714785074694791ull, kX2 = 14029467366897019727ull, kX3 = 1609587929392839161ull,
+                   kX4 = 9650029242287828579ull, kX5 = 2870177450012600261ull;
+__device__ __forceinline__ uint64_t xrotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t in) { return xrotl(acc + in * kX2, 31) * kX1; }
+template <class O>
+__device__ uint32_t xxh64_low32(O out, uint32_t s, uint32_t len) {
+  const uint32_t lane = threadIdx.x & 63;
+  auto rd = [&](uint32_t i, uint32_t nb) {
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < nb; k++) v |= (uint64_t)(uint8_t)out[s + i + k] << (8 * k);
+    return v;
+  };
+  uint64_t h;
+  uint32_t i = 0;
+  if (len >= 32) {
+    uint64_t v = lane == 0 ? kX1 + kX2 : lane == 1 ? kX2 : lane == 2 ? 0ull : 0ull - kX1;
+    const uint32_t stripes = len / 32;
+    if (lane < 4)
+      for (uint32_t k = 0; k < stripes; k++) v = xround(v, rd(32 * k + 8 * lane, 8));
+    __builtin_amdgcn_wave_barrier();
+    uint64_t a[4];
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, 64);
+      a[l] = ((uint64_t)hi << 32) | lo;
+    }
+    h = xrotl(a[0], 1) + xrotl(a[1], 7) + xrotl(a[2], 12) + xrotl(a[3], 18);
+#pragma unroll
+    for (int l = 0; l < 4; l++) h = (h ^ xround(0, a[l])) * kX1 + kX4;
+    i = stripes * 32;
+  } else {
+    h = kX5;
+  }
+  h += len;
+  for (; i + 8 <= len; i += 8) h = xrotl(h ^ xround(0, rd(i, 8)), 27) * kX1 + kX4;
+  if (i + 4 <= len) {
+    h = xrotl(h ^ (rd(i, 4) * kX1), 23) * kX2 + kX3;
+    i += 4;
+  }
+  for (; i < len; i++) h = xrotl(h ^ (rd(i, 1) * kX5), 11) * kX1;
+  h ^= h >> 33;
+  h *= kX2;
+  h ^= h >> 29;
+  h *= kX3;
+  h ^= h >> 32;
+  return (uint32_t)h;
+}
+
+// Decode the Zstd frames of in[0, csize) into out[0, olen): frames one
+// after another (ZSTD_decompress's loop), skippable frames skipped, each
+// frame's content size checked against its output, a content checksum
+// (XXH64) verified.  Each frame's literals decode into the tail of the
+// whole output, which no frame before the last writes.
 // All 64 lanes of the wave call it; `tb` is a 16-aligned LDS area of tcap >=
 // kZTablesBytes bytes.  Returns a wave-uniform status.
 template <class Src, class O>
@@ -462,12 +520,25 @@ __device__ __attribute__((noinline)) uint32_t zstd_decode(const Src& in, uint32_
                                 uint32_t tcap) {
   const uint32_t lane = threadIdx.x & 63;
   const Tabs t(tb);
+  uint32_t p = 0, op = 0;
+  bool first = true;
+  while (first || p < csize) {
+  // skippable frames (RFC 8878 3.1.2): magic 0x184D2A5?, u32 size, payload
+  if (csize - p >= 8 && (in.u32(p) & 0xFFFFFFF0u) == 0x184D2A50u) {
+    const uint32_t sz = in.u32(p + 4);
+    if (sz > csize - p - 8) return ST_CODEC;
+    p += 8 + sz;
+    first = false;
+    continue;
+  }
+  first = false;
+  const uint32_t op0 = op;
   // ---- frame header (RFC 8878 3.1.1.1)
-  if (csize < 8 || in.u32(0) != 0xFD2FB528u) return ST_CODEC;
-  const uint32_t fhd = in.u8(4);
+  if (csize - p < 8 || in.u32(p) != 0xFD2FB528u) return ST_CODEC;
+  const uint32_t fhd = in.u8(p + 4);
   if (fhd & 8) return ST_CODEC;  // reserved bit
   const uint32_t single = (fhd >> 5) & 1, fcs_flag = fhd >> 6, did_flag = fhd & 3;
-  uint32_t p = 5;
+  p += 5;
   if (!single) {
     const uint32_t wd = in.u8(p++);
     const uint32_t wlog = 10 + (wd >> 3);
@@ -482,11 +553,12 @@ __device__ __attribute__((noinline)) uint32_t zstd_decode(const Src& in, uint32_
   for (uint32_t k = 0; k < did_len; k++) did |= in.u8(p + k) << (8 * k);
   p += did_len;
   if (did) return ST_CODEC;  // a dictionary the caller does not have
+  uint64_t fcs = ~0ull;
   if (fcs_len) {
-    uint64_t fcs = 0;
+    fcs = 0;
     for (uint32_t k = 0; k < fcs_len; k++) fcs |= (uint64_t)in.u8(p + k) << (8 * k);
     if (fcs_len == 2) fcs += 256;
-    if (fcs != olen) return ST_CODEC;
+    if (fcs > olen - op0) return ST_CODEC;
     p += fcs_len;
   }
   // ---- blocks
@@ -494,7 +566,6 @@ __device__ __attribute__((noinline)) uint32_t zstd_decode(const Src& in, uint32_
   uint32_t al_ll = 0, al_ml = 0, al_of = 0;
   bool h_ll = false, h_ml = false, h_of = false, p_ll = false, p_ml = false, p_of = false;
   uint32_t htl = 0;  // Huffman table log, 0 = none yet
-  uint32_t op = 0;
   for (;;) {
     if (p + 3 > csize) return ST_CODEC;
     const uint32_t bh = in.u8(p) | (in.u8(p + 1) << 8) | (in.u8(p + 2) << 16);
@@ -716,8 +787,14 @@ __device__ __attribute__((noinline)) uint32_t zstd_decode(const Src& in, uint32_
     }
     if (last) break;
   }
-  if (fhd & 4) return ST_NYI;     // content checksum (XXH64): the writer never sets it
-  if (p != csize) return ST_NYI;  // further frames / trailing bytes
+  if (fcs != ~0ull && op - op0 != fcs) return ST_CODEC;  // the frame's content size
+  if (fhd & 4) {  // content checksum: XXH64 of the frame's output, low 32 bits
+    if (csize - p < 4) return ST_CODEC;
+    zsync();
+    if (xxh64_low32(out, op0, op - op0) != in.u32(p)) return ST_CODEC;
+    p += 4;
+  }
+  }  // frames
   if (op != olen) return ST_CODEC;
   zsync();
   return ST_OK;

@@ -176,18 +176,50 @@ def test_small_and_odd_sizes(ctx):
             check_page(ctx, v, zstd_page(v, stream_frame(v.tobytes(), min(pieces, n), 3, pledged=True)))
 
 
-def test_checksum_frames_report_nyi(ctx):
-    """Content checksums (XXH64) are not verified on the device: such pages
-    report NotYetImplemented (libzstd verifies and decodes them)."""
+def test_checksum_frames(ctx):
+    """Frames with a content checksum (XXH64, low 32 bits) decode; a wrong
+    checksum is rejected by both libzstd (the oracle) and the device."""
     import pa_amd
 
-    v = np.arange(4096, dtype=np.int64) % 97
-    page = zstd_page(v, stream_frame(v.tobytes(), 1, 3, checksum=True, pledged=True))
-    ov, _ = O.read_page(page, len(v), np.int64, False)
-    assert ov.tobytes() == v.tobytes()
-    with pytest.raises(pa_amd.StrawboatError) as e:
-        gpu_decode(ctx, page, [(len(page), len(v))], np.int64)
-    assert e.value.status == 2
+    rng = np.random.default_rng(8)
+    for n in (3, 4, 5, 100, 4096, 20000):
+        v = gen_values("index", n, np.int64, rng, uniq=97)
+        for pieces in (1, 3):
+            frame = stream_frame(v.tobytes(), min(pieces, n), 3, checksum=True, pledged=bool(pieces == 1))
+            check_page(ctx, v, zstd_page(v, frame))
+            bad = bytearray(frame)
+            bad[-1 - int(rng.integers(0, 4))] ^= 1 << int(rng.integers(0, 8))  # inside the 4 checksum bytes
+            page = zstd_page(v, bytes(bad))
+            with pytest.raises(O.OracleError):
+                O.read_page(page, n, np.int64, False)
+            with pytest.raises(pa_amd.StrawboatError):
+                gpu_decode(ctx, page, [(len(page), n)], np.int64)
+
+
+def skippable(payload: bytes, k: int = 0) -> bytes:
+    """A skippable frame (RFC 8878 3.1.2): magic 0x184D2A50 + k, size, payload."""
+    return (0x184D2A50 + k).to_bytes(4, "little") + len(payload).to_bytes(4, "little") + payload
+
+
+def test_multiple_and_skippable_frames(ctx):
+    """Several frames back to back, with skippable frames between them (as
+    ZSTD_decompress, compression/basic.rs:93-97, accepts): the output is the
+    frames' contents in order."""
+    rng = np.random.default_rng(9)
+    for n in (7, 1000, 9000):
+        v = gen_values("runs", n, np.int64, rng)
+        raw = v.tobytes()
+        cuts = sorted({0, len(raw), *(int(x) for x in rng.integers(0, len(raw), 2))})
+        parts = [raw[a:b] for a, b in zip(cuts, cuts[1:]) if b > a]
+        for variant in range(4):
+            frame = b""
+            for k, part in enumerate(parts):
+                if variant & 1:
+                    frame += skippable(bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8)), k)
+                frame += stream_frame(part, 1 + (k % 2), 3, checksum=bool(variant & 2), pledged=bool(k % 2 == 0))
+            if variant == 3:
+                frame += skippable(b"tail", 15)
+            check_page(ctx, v, zstd_page(v, frame))
 
 
 def test_corrupt_frames_match_libzstd(ctx):
