@@ -1110,9 +1110,14 @@ static double sample_ratio(int codec, const arr_t* a, const stats_t* full, orc_r
       size_t range_end = (k == SC - 1 ? sep + rem : sep) - SS;
       size_t begin = k * sep + (size_t)(rng_next(rng) % range_end);
       memcpy(vals + k * SS * a->width, a->values + begin * a->width, SS * (size_t)a->width);
+      /* the sample is rebuilt by MutablePrimitiveArray::extend_trusted_len
+       * (integer/mod.rs:334-336, double/mod.rs:334-336): arrow2 writes
+       * T::default() under each None, so null slots read 0 from here on */
       if (bits)
-        for (size_t j = 0; j < SS; j++)
+        for (size_t j = 0; j < SS; j++) {
           if (get_bit(a->validity, begin + j)) bits[(k * SS + j) >> 3] |= (uint8_t)(1u << ((k * SS + j) & 7));
+          else memset(vals + (k * SS + j) * a->width, 0, (size_t)a->width);
+        }
     }
     sa.values = vals;
     sa.validity = bits;

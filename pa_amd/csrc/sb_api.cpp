@@ -71,7 +71,8 @@ struct sb_plan {
   uint8_t* d_scratch = nullptr;      // binary: expanded offsets streams
   uint8_t* d_region = nullptr;       // fixed width: the pages' HBM regions (PageDesc.reserved)
   uint32_t* d_spill = nullptr;       // [2] spilled-leaf job counts (by decode parity)
-  uint32_t* d_sched = nullptr;       // [2] k_inflate's job claim counters (zero between launches)
+  uint32_t* d_sched = nullptr;       // [2][2] k_inflate's job claim counters (zero between launches), two pairs
+  uint32_t sched_flip = 0;           // the pair the next inflate launch claims from
   uint8_t* d_ascii = nullptr;        // binary: per page, its values stream inflated all ASCII (k_inflate)
   sb::InflateJob* d_spill_jobs = nullptr;
   uint32_t n_spill = 0;              // pages with a spill area (bounds the spill launches)
@@ -108,6 +109,16 @@ struct sb_plan {
   bool timing = false;  // record HIP events around each decode (sb_plan_enable_timing)
   bool timed = false;
 };
+
+// k_inflate claims from one of the plan's two counter pairs and zeroes the
+// other at entry; the pairs alternate per launch (see InflateLaunch::sched_spare)
+static void sched_pair(sb_plan* p, sb::InflateLaunch& I) {
+  if (!p->d_sched || I.n_jobs == 0) return;
+  const uint32_t f = p->sched_flip;
+  p->sched_flip ^= 1u;
+  I.sched = p->d_sched + 2 * f;
+  I.sched_spare = p->d_sched + 2 * (f ^ 1u);
+}
 
 static sb_status fail(sb_ctx* ctx, sb_status st, const char* fmt, ...) {
   if (ctx) {
@@ -441,8 +452,8 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
   if (e == hipSuccess) e = hipMalloc(&p->d_defer, (np + 4) * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemsetAsync(p->d_defer, 0, 4 * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipMalloc(&p->d_jobs, (owidth ? 2 : 1) * np * sizeof(sb::InflateJob));
-  if (e == hipSuccess) e = hipMalloc(&p->d_sched, 2 * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemsetAsync(p->d_sched, 0, 2 * sizeof(uint32_t), ctx->stream);
+  if (e == hipSuccess) e = hipMalloc(&p->d_sched, 4 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(p->d_sched, 0, 4 * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipEventCreate(&p->ev0);
   if (e == hipSuccess) e = hipEventCreate(&p->ev1);
   if (e == hipSuccess && n_pages) {
@@ -660,6 +671,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
   if (p->n_bin_jobs) {  // Basic LZ4 / Snappy pages: streams expanded first, one wave each
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2, p->n_bin_jobs, out->d_values, p->d_scratch,
                         p->d_bin + np, p->d_status, (uint8_t*)out->d_offsets, p->d_sched, p->d_ascii};
+    sched_pair(p, I);
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))
@@ -743,6 +755,7 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
     // CH_LEAF LZ4 / Snappy pages listed by the pass above: values straight into the column
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2 + a.parity, (uint32_t)p->n_pages,
                         (uint8_t*)out->d_values, nullptr, nullptr, p->d_status, nullptr, p->d_sched};
+    sched_pair(p, I);
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))
@@ -760,6 +773,7 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
       // pages' regions (one wave per stream), then the pages decoded from there
       sb::InflateLaunch I{p->d_chunk, p->d_spill_jobs, p->d_spill + a.parity, p->n_spill, nullptr, p->d_region,
                           nullptr, p->d_status, nullptr, p->d_sched};
+      sched_pair(p, I);
       if (sb::launch_inflate(I, ctx->stream) || sb::launch_zinflate(I, ctx->stream))
         return fail(ctx, SB_E_DEVICE, "spill inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
       a.n_list = p->n_spill;

@@ -2543,6 +2543,7 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
   // grid-strided.
   const uint32_t waves = gridDim.x * kInfWaves, part = min(waves, n);
   uint32_t j = blockIdx.x * kInfWaves + wv;
+  if (a.sched_spare && j == 0 && lane < 2) a.sched_spare[lane] = 0;
   if (j >= part) return;
   for (bool first = true;; first = false) {
     if (a.sched) {

@@ -474,9 +474,13 @@ static double sample_ratio(int codec, const Arr<T>& a, const Stats<T>& full, Rng
     const size_t range_end = (k == SC - 1 ? sep + rem : sep) - SS;
     const size_t begin = k * sep + (size_t)(rng.next() % range_end);
     std::memcpy(vals.data() + k * SS, a.v + begin, SS * sizeof(T));
+    // extend_trusted_len (integer/mod.rs:334-336) writes T::default() under
+    // each null slot of the rebuilt sample
     if (a.valid)
-      for (size_t j = 0; j < SS; j++)
+      for (size_t j = 0; j < SS; j++) {
         if (bit(a.valid, begin + j)) bm[(k * SS + j) >> 3] |= (uint8_t)(1u << ((k * SS + j) & 7));
+        else vals[k * SS + j] = T{};
+      }
   }
   Arr<T> sa{vals.data(), a.valid ? bm.data() : nullptr, SC * SS, a.is_signed};
   Stats<T> st(sa.n);

@@ -649,19 +649,19 @@ __device__ Av take_sample(Ctx& c, Sh& sh, const Av& a) {
   uint8_t* vb = c.samp + kSample * 8;
   for (uint32_t i = tid; i < kSample / 8; i += NT) vb[i] = 0;
   __syncthreads();
+  // The reference rebuilds the sample through MutablePrimitiveArray::
+  // extend_trusted_len (integer/mod.rs:334-336, double/mod.rs:334-336),
+  // which writes T::default() under every null slot: the trial encoders then
+  // see zeros there, not the slot's original bits.
   for (uint32_t q = tid; q < kSample; q += NT) {
     const uint32_t src = sh.win[q / SS] + q % SS;
-    const uint64_t v = ld<W>(a.p, src);
+    const bool ok = !a.vb || valid_at(a, src);
+    const uint64_t v = ok ? ld<W>(a.p, src) : 0;
     if constexpr (W == 8) ((uint64_t*)c.samp)[q] = v;
     else if constexpr (W == 4) ((uint32_t*)c.samp)[q] = (uint32_t)v;
     else if constexpr (W == 2) ((uint16_t*)c.samp)[q] = (uint16_t)v;
     else c.samp[q] = (uint8_t)v;
-  }
-  if (a.vb) {
-    for (uint32_t q = tid; q < kSample; q += NT) {
-      const uint32_t src = sh.win[q / SS] + q % SS;
-      if (valid_at(a, src)) atomicOr((uint32_t*)vb + (q >> 5), 1u << (q & 31));
-    }
+    if (a.vb && ok) atomicOr((uint32_t*)vb + (q >> 5), 1u << (q & 31));
   }
   __syncthreads();
   return Av{c.samp, a.vb ? vb : nullptr, 0, kSample};

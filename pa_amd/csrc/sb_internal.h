@@ -101,6 +101,10 @@ struct InflateLaunch {
   uint8_t* offs;  // kDstBinOffs jobs: the column's 32-bit offsets (dword-aligned)
   uint32_t* sched;  // k_inflate's job claim counters [2], zero between launches (self-resetting), or nullptr
   uint8_t* ascii;   // binary values jobs: per page, 1 = every byte written was ASCII (else 0), or nullptr
+  // the other counter pair of the plan (the next launch's): zeroed at entry,
+  // so a launch that never reached its own reset cannot leave the plan's
+  // next launch a stale count (the plan alternates the pairs), or nullptr
+  uint32_t* sched_spare = nullptr;
 };
 int launch_inflate(const InflateLaunch& a, void* stream);
 // Zstd jobs (codec 2) of the same list: one wave per frame, tables in LDS, output in HBM.

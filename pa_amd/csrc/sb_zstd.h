@@ -753,7 +753,10 @@ __device__ __attribute__((noinline)) uint32_t zstd_decode(const Src& in, uint32_
               sLL = (uint32_t)(cl & 0xFFFF) + br.read((uint32_t)(cl >> 16) & 0xFF);
               sML = (uint32_t)(cm & 0xFFFF) + br.read((uint32_t)(cm >> 16) & 0xFF);
               sOF = (uint32_t)(co & 0xFFFF) + br.read((uint32_t)(co >> 16) & 0xFF);
-              if (ll > olen - l || off > o + ll || o + ml > l) {
+              // a frame's history starts at its own first byte: libzstd 1.4.8
+              // resets the prefix per frame (ZSTD_checkContinuity), so an
+              // offset reaching into an earlier frame's output is corrupt
+              if (ll > olen - l || off > o + ll - op0 || o + ml > l) {
                 st = ST_CODEC;
                 break;
               }

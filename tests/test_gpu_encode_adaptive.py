@@ -190,3 +190,18 @@ def test_bitmap_roaring_and_dict_freq_cascade(ctx):
     w = np.where(rng.random(n) < 0.95, 7, rng.integers(1000, 1010, n)).astype(np.int32)
     check(ctx, w, None, False, 8192, dict(ratio=1.0, forced=O.DICT))
     check(ctx, w, rng.random(n) > 0.1, True, 8192, dict(ratio=1.0, forced=O.FREQ))
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.uint32, np.int64, np.int16, np.float64], ids=lambda d: np.dtype(d).name)
+def test_sample_ratio_null_slots_read_default(ctx, dtype):
+    """Null slots read T::default() in the rebuilt trial sample
+    (integer/mod.rs:334-336, double/mod.rs:334-336): the device writer's
+    choices follow the zeros, byte-identical to oracle and host writer."""
+    from tests.test_roundtrip_cpu import _null_slot_column
+
+    rng = np.random.default_rng(78)
+    v, valid = _null_slot_column(20000, dtype, rng)
+    for o in (dict(ratio=1.2), dict(ratio=1.0), dict(ratio=2.0, default_codec=O.LZ4)):
+        codecs = check(ctx, v, valid, True, 8192, o, forbidden=())
+        if dtype == np.int32 and o["ratio"] == 1.2:
+            assert O.BITPACKING in codecs

@@ -254,3 +254,51 @@ def test_corrupt_frames_match_libzstd(ctx):
             assert gv.tobytes() == ov.tobytes(), f"case {t}: bytes differ"
             seen["ok"] += 1
     assert seen["ok"] and seen["err"]
+
+
+def prefix_frame(data: bytes, prefix: bytes, level: int = 3) -> bytes:
+    """A frame compressed against a referenced prefix (ZSTD_CCtx_refPrefix +
+    ZSTD_compress2): its sequences reach back into the prefix, i.e. before
+    the frame's own first output byte; no dictionary id is recorded."""
+    z = _zlib()
+    z.ZSTD_CCtx_refPrefix.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    z.ZSTD_CCtx_refPrefix.restype = ctypes.c_size_t
+    z.ZSTD_compress2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    z.ZSTD_compress2.restype = ctypes.c_size_t
+    cc = z.ZSTD_createCCtx()
+    try:
+        assert not z.ZSTD_isError(z.ZSTD_CCtx_setParameter(cc, 100, level))
+        pre = ctypes.create_string_buffer(prefix, max(len(prefix), 1))
+        assert not z.ZSTD_isError(z.ZSTD_CCtx_refPrefix(cc, pre, len(prefix)))
+        out = ctypes.create_string_buffer(2 * len(data) + 4096)
+        r = z.ZSTD_compress2(cc, out, len(out), data, len(data))
+        assert not z.ZSTD_isError(r)
+        return out.raw[:r]
+    finally:
+        z.ZSTD_freeCCtx(cc)
+
+
+@pytest.mark.parametrize("n", [1000, 4096, 20000], ids=lambda n: f"rows{n}")
+def test_match_into_previous_frame_is_rejected(ctx, n):
+    """libzstd starts each frame's history at the frame's first output byte
+    (ZSTD_checkContinuity per frame), so a second frame whose match reaches
+    into the first frame's output is corrupt for ZSTD_decompress
+    (compression/basic.rs:93-97) even though the bytes it would copy are
+    right there: the device must reject it too.  20000 rows of Int64 is a
+    page past the LDS stage (k_zinflate, HBM to HBM)."""
+    import pa_amd
+
+    rng = np.random.default_rng(n)
+    a = gen_values("index", n // 2, np.int64, rng, uniq=1 << 20)
+    raw = a.tobytes()
+    second = prefix_frame(raw, raw)
+    assert len(second) < len(raw) // 4, "the frame should be matches into the prefix"
+    v = np.concatenate([a, a])
+    page = zstd_page(v, stream_frame(raw, 1, 3, pledged=True) + second)
+    with pytest.raises(O.OracleError):
+        O.read_page(page, len(v), np.int64, False)
+    with pytest.raises(pa_amd.StrawboatError):
+        gpu_decode(ctx, page, [(len(page), len(v))], np.int64)
+    # two self-contained frames of the same bytes decode
+    ok = zstd_page(v, stream_frame(raw, 1, 3, pledged=True) + stream_frame(raw, 1, 3, pledged=True))
+    check_page(ctx, v, ok)

@@ -175,3 +175,55 @@ def test_binary_encoder_matches_oracle_encoder_big_pages():
                                      parent_values_len=len(vals))
             assert chunk[pos:pos + m.length] == ob, (ratio, forced, i)
             pos += m.length
+
+
+def _null_slot_column(n, dt, rng):
+    """Valid rows small (< 2^8, or a slowly varying double), null slots
+    holding 2^30-scale garbage: the sampled ratio of compress_sample_ratio
+    must see T::default() there (integer/mod.rs:334-336 rebuilds the sample
+    through MutablePrimitiveArray::extend_trusted_len, which writes zeros
+    under None), not the slot's bits."""
+    valid = rng.random(n) > 0.3
+    if np.dtype(dt).kind == "f":
+        v = np.round(np.cumsum(rng.integers(-1, 2, n)) * 0.25 + 100.0, 2).astype(dt)
+        garbage = rng.standard_normal(n).astype(dt) * dt(1e300 if dt == np.float64 else 1e30)
+    else:
+        v = rng.integers(0, 256, n).astype(dt)
+        garbage = rng.integers(2**30, 2**31, n).astype(dt)
+    v = np.where(valid, v, garbage)
+    return v, valid
+
+
+def test_sample_ratio_null_slots_read_default():
+    """The rule pinned: a nullable Int32 page whose null slots hold 2^30-scale
+    values and whose valid rows are < 2^8 chooses Bitpacking (the sample's
+    bit width comes from the zeros: b = 8, ratio ~3.97), not Dict (1.79, what
+    a sample keeping the slots' bits, b = 31, ratio 1.03, leaves as the best).
+    Oracle, host writer and the reference rule agree byte for byte."""
+    rng = np.random.default_rng(77)
+    n = 8192
+    v, valid = _null_slot_column(n, np.int32, rng)
+    page = O.write_page(v, valid, True, O.WriteOptions.make(ratio=1.2, seed=3))
+    assert O.page_codec(page, True) == O.BITPACKING
+    wo = pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=n, seed=3)
+    chunk, metas = pa_amd.encode_column(v, valid, True, wo)
+    ob = O.write_page(v, valid, True, O.WriteOptions.make(ratio=1.2, seed=pa_amd.page_seed(3, 0)))
+    assert chunk == ob
+    out, vv = O.read_column(chunk, [(m.length, m.num_values) for m in metas], np.int32, True)
+    assert out.tobytes() == v.tobytes() and (vv == valid).all()
+    # every sampled candidate, for each type the writers sample: host == oracle
+    for dt in (np.int32, np.uint32, np.int64, np.int16, np.float64, np.float32):
+        v, valid = _null_slot_column(20000, dt, rng)
+        for ratio, forbidden in ((1.2, ()), (1.0, (O.DICT, O.FREQ)), (2.0, (O.DICT,))):
+            if dt == np.float32:
+                forbidden = forbidden + (O.PATAS,)
+            wo = pa_amd.WriteOptions(default_compress_ratio=ratio, max_page_size=4096, seed=9,
+                                     forbidden_compressions=forbidden)
+            chunk, metas = pa_amd.encode_column(v, valid, True, wo)
+            pos = 0
+            for i, m in enumerate(metas):
+                sl = slice(i * 4096, i * 4096 + m.num_values)
+                ob = O.write_page(v[sl], valid[sl], True, O.WriteOptions.make(
+                    ratio=ratio, forbidden=forbidden, seed=pa_amd.page_seed(9, i)))
+                assert chunk[pos:pos + m.length] == ob, (np.dtype(dt).name, ratio, i)
+                pos += m.length
