@@ -461,19 +461,24 @@ def read_list_column(chunk, metas, dtype, list_nullable, item_nullable):
             np.concatenate(leafv_all) if item_nullable else None)
 
 
-def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable, leaf="fixed", offset_width=4):
-    """batch read of a leaf under len(list_nullable) list levels (outermost
-    first): per page orc_read_nested_page, then the pages concatenated with
-    each level's offsets moved onto its child's running length ->
-    ([offsets per level], [validity per level | None], values, leaf validity | None).
+def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable, leaf="fixed", offset_width=4,
+                       struct_mask=0, with_counts=False):
+    """batch read of a leaf under len(list_nullable) nests (outermost first;
+    bit d of struct_mask: nest d is a Struct, else a List / Map): per page
+    orc_read_nest_page, then the pages concatenated with each list level's
+    offsets moved onto its child's running length ->
+    ([offsets per nest | None for structs], [validity per nest | None],
+     values, leaf validity | None), and with_counts: a fifth item, the
+    entries of every nest and the leaf slots.
     leaf="binary": values = (offsets int64, bytes) of the concatenated per-page
     Utf8 arrays (each page's values[p0:pn], arrow concatenate);
     leaf="bool": values = a bool array."""
     L = _bin_lib()
     if not getattr(L, "_nested_ready", False):
         P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
-        L.orc_read_nested_page.argtypes = [P, S, S, I, P, I, I, I, P, P, P, P, P, ctypes.POINTER(S)]
+        L.orc_read_nest_page.argtypes = [P, S, S, I, P, ctypes.c_uint32, I, I, I, P, P, P, P, P, ctypes.POINTER(S)]
         L._nested_ready = True
+    struct_mask = int(struct_mask or 0)
     dtype = np.dtype(dtype)
     D = len(list_nullable)
     src = np.frombuffer(chunk, np.uint8)
@@ -492,15 +497,15 @@ def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable, leaf="
         b = [np.zeros(nlev // 8 + 2, np.uint8) for _ in range(D)]
         v = np.zeros(nlev + 1, dtype) if kind < 2 else np.zeros(nlev // 8 + 2, np.uint8)
         fb = np.zeros(nlev // 8 + 2, np.uint8)
-        op = (ctypes.c_void_p * D)(*[x.ctypes.data for x in o])
+        op = (ctypes.c_void_p * D)(*[None if (struct_mask >> d) & 1 else x.ctypes.data for d, x in enumerate(o)])
         bp = (ctypes.c_void_p * D)(*[x.ctypes.data for x in b])
         cnt = (ctypes.c_size_t * (D + 1))()
         rows = ctypes.c_size_t()
         bv = _BinVec()
         vptr = ctypes.addressof(bv) if kind == 2 else _ptr(v)
         try:
-            rc = L.orc_read_nested_page(_ptr(page), length, nlev, D, ln, int(item_nullable), kind, width, op, bp,
-                                        vptr, _ptr(fb), cnt, ctypes.byref(rows))
+            rc = L.orc_read_nest_page(_ptr(page), length, nlev, D, ln, struct_mask, int(item_nullable), kind, width,
+                                      op, bp, vptr, _ptr(fb), cnt, ctypes.byref(rows))
             _check(rc, "read_nested_page")
             if kind == 2:
                 po = np.ctypeslib.as_array(bv.offsets, shape=(bv.n_off,)).copy() if bv.n_off else np.zeros(1, np.int64)
@@ -523,9 +528,12 @@ def read_nested_column(chunk, metas, dtype, list_nullable, item_nullable, leaf="
         for d in range(D + 1):
             base[d] += cnt[d]
         pos += length
-    out_offs = [np.concatenate(offs[d] + [np.array([base[d + 1]], np.int64)]) for d in range(D)]
+    out_offs = [None if (struct_mask >> d) & 1 else np.concatenate(offs[d] + [np.array([base[d + 1]], np.int64)])
+                for d in range(D)]
     out_bits = [np.concatenate(bits[d]) if list_nullable[d] else None for d in range(D)]
     values = (np.concatenate(bin_offs), b"".join(bin_vals)) if kind == 2 else np.concatenate(vals)
+    if with_counts:
+        return out_offs, out_bits, values, (np.concatenate(leafv) if item_nullable else None), list(base)
     return out_offs, out_bits, values, (np.concatenate(leafv) if item_nullable else None)
 
 

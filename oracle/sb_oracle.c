@@ -670,6 +670,13 @@ static int uleb(const uint8_t* b, size_t n, size_t* p, uint64_t* v) {
 int orc_hybrid_decode(const uint8_t* buf, size_t len, uint32_t bw, size_t n, uint32_t* out) {
   size_t p = 0, got = 0;
   if (bw > 32) return ORC_E_ARG;
+  /* parquet2 0.17 HybridRleDecoder with num_bits 0 (max level 0: a required
+   * nest chain writes no stream, arrow2 write_rep_levels / write_def_levels
+   * return early) yields 0 for every level without reading the bytes */
+  if (bw == 0) {
+    for (size_t i = 0; i < n; i++) out[i] = 0;
+    return ORC_OK;
+  }
   while (got < n) {
     uint64_t h;
     if (uleb(buf, len, &p, &h)) return ORC_E_OUT_OF_SPEC;
@@ -1839,25 +1846,32 @@ int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int l
   return rc;
 }
 
-/* Nested page with `depth` list levels over a primitive leaf (List<List<T>>
- * ...): read_validity_nested (read/read_basic.rs:65-173) in its general form --
- * nests[0..depth) are lists (NestedOptional / NestedValid: repeated, nullable
- * per level), nests[depth] the primitive (NestedPrimitive); cum_sum /
- * cum_rep over (nullable + repeated) / repeated; a nest is pushed when
- * `rep <= cum_rep[d] && def >= cum_sum[d]` or the level above was a required
- * nest that was not valid (is_required: false for lists and primitives, the
- * arrow2 0.17 nested_utils rule, not vendored -- parity unpinned for struct
- * nests, which are not supported here).  A list push appends the child's
- * current length as its offset and `nullable && def > cum_sum[d]` as its
- * validity; the primitive push counts a leaf slot, valid when
- * `def != cum_sum[depth]` (:138-146).  Decoding stops after the level whose
- * successor would start row `additional + 1` (:150-162).  Outputs are
- * page-local: out_offsets[d] holds counts[d] entries (create_list appends the
- * child's length, counts[d + 1], read/array/list.rs:48), out_bits[d] the
- * list validity when list_nullable[d]; counts[depth] = leaf slots. */
-int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int depth, const int* list_nullable,
-                         int item_nullable, int kind, int width, int64_t** out_offsets, uint8_t** out_bits,
-                         uint8_t* out_values, uint8_t* out_leaf_bits, size_t* counts, size_t* out_rows) {
+/* Nested page with `depth` nests over a leaf: read_validity_nested
+ * (read/read_basic.rs:65-173) in its general form.  nests[0..depth) come
+ * from the field's InitNested chain (read/deserialize.rs:140-233): a List /
+ * LargeList / Map pushes InitNested::List (arrow2 NestedOptional /
+ * NestedValid: repeated, never "required"), a Struct InitNested::Struct
+ * (NestedStruct / NestedStructValid: not repeated, is_required() true);
+ * bit d of struct_mask marks the struct nests.  nests[depth] is the leaf
+ * (NestedPrimitive: not repeated, not required).  cum_sum / cum_rep run over
+ * (nullable + repeated) / repeated (:95-105); a nest is pushed when
+ * `rep <= cum_rep[d] && def >= cum_sum[d]` or the nest above was pushed as a
+ * required nest that was not valid (:118-137 -- so every child of a null
+ * struct gets a slot).  A list push appends the child's current length as
+ * its offset, every nullable push its validity `def > cum_sum[d]`; the leaf
+ * push counts a leaf slot, valid when right && `def != cum_sum[depth]`
+ * (:138-149).  Decoding stops after the level whose successor would start
+ * row `additional + 1` (:154-163).  Outputs are page-local: out_offsets[d]
+ * (list nests only; NULL for structs) holds counts[d] entries (create_list
+ * / create_map append the child's length, counts[d + 1]), out_bits[d] the
+ * nest validity when nest_nullable[d]; counts[depth] = leaf slots.
+ * (arrow2 0.17 nested_utils, not vendored: the is_required rule is restated
+ * from its published source, and pinned against pyarrow's levels for
+ * struct and map columns, tests/test_pyarrow_nested.py.) */
+int orc_read_nest_page(const uint8_t* page, size_t len, size_t num_levels, int depth, const int* nest_nullable,
+                       uint32_t struct_mask, int item_nullable, int kind, int width, int64_t** out_offsets,
+                       uint8_t** out_bits, uint8_t* out_values, uint8_t* out_leaf_bits, size_t* counts,
+                       size_t* out_rows) {
   if (depth < 1 || depth > 4) return ORC_E_NYI;
   if (len < 12) return ORC_E_IO;
   uint32_t additional = rd_u32(page), rep_len = rd_u32(page + 4), def_len = rd_u32(page + 8);
@@ -1865,7 +1879,12 @@ int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int
   if (pos + rep_len > len || pos + rep_len + def_len > len) return ORC_E_IO;
   const int max_depth = depth + 1;
   int nullable[5], repeated[5], required[5];
-  for (int d = 0; d < depth; d++) { nullable[d] = list_nullable[d] != 0; repeated[d] = 1; required[d] = 0; }
+  for (int d = 0; d < depth; d++) {
+    const int is_struct = (struct_mask >> d) & 1;
+    nullable[d] = nest_nullable[d] != 0;
+    repeated[d] = !is_struct;
+    required[d] = is_struct;
+  }
   nullable[depth] = item_nullable != 0; repeated[depth] = 0; required[depth] = 0;
   uint32_t cum_sum[6] = {0}, cum_rep[6] = {0};
   for (int d = 0; d < max_depth; d++) {
@@ -1889,7 +1908,7 @@ int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int
       if (!(is_required || right)) continue;
       const int is_valid = nullable[d] && dv > cum_sum[d];
       if (d < depth) {
-        out_offsets[d][n[d]] = (int64_t)n[d + 1];
+        if (repeated[d]) out_offsets[d][n[d]] = (int64_t)n[d + 1];
         if (nullable[d]) {
           if (is_valid) out_bits[d][n[d] >> 3] |= (uint8_t)(1u << (n[d] & 7));
           else out_bits[d][n[d] >> 3] &= (uint8_t)~(1u << (n[d] & 7));
@@ -1918,6 +1937,36 @@ int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int
   for (int d = 0; d <= depth; d++) counts[d] = n[d];
   *out_rows = rows;
   return rc;
+}
+
+/* depth list levels over a leaf (no struct nests) */
+int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int depth, const int* list_nullable,
+                         int item_nullable, int kind, int width, int64_t** out_offsets, uint8_t** out_bits,
+                         uint8_t* out_values, uint8_t* out_leaf_bits, size_t* counts, size_t* out_rows) {
+  return orc_read_nest_page(page, len, num_levels, depth, list_nullable, 0u, item_nullable, kind, width,
+                            out_offsets, out_bits, out_values, out_leaf_bits, counts, out_rows);
+}
+
+/* A nested page from precomputed levels (write_nested, write/serialize.rs:
+ * 133-146, with write_nested_validity :217-232): [u32 rows][u32 rep_len]
+ * [u32 def_len][rep][def] + the leaf's values stream.  Each level stream is
+ * arrow2's write_rep_levels / write_def_levels V2 -- nothing when the max
+ * level is 0, else parquet2 encode_u32 at get_bit_width(max level).  The
+ * levels themselves (arrow2 to_nested + RepLevelsIter / DefLevelsIter) are
+ * made by oracle.nest_levels. */
+int orc_write_levels_page(const uint32_t* rep, const uint32_t* def, size_t n_levels, uint32_t max_rep,
+                          uint32_t max_def, uint32_t rows, orc_buf* out) {
+  orc_buf lv = {0};
+  if (max_rep) encode_levels(rep, n_levels, bit_width_of(max_rep), &lv);
+  const size_t rep_len = lv.len;
+  if (max_def) encode_levels(def, n_levels, bit_width_of(max_def), &lv);
+  const size_t def_len = lv.len - rep_len;
+  buf_u32(out, rows);
+  buf_u32(out, (uint32_t)rep_len);
+  buf_u32(out, (uint32_t)def_len);
+  if (lv.len) buf_put(out, lv.data, lv.len);
+  orc_buf_free(&lv);
+  return ORC_OK;
 }
 
 /* ======================================================================= */

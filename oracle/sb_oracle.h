@@ -134,6 +134,12 @@ int orc_write_list_page(const int64_t* list_offsets, const uint8_t* list_validit
 int orc_read_nested_page(const uint8_t* page, size_t len, size_t num_levels, int depth, const int* list_nullable,
                          int item_nullable, int kind, int width, int64_t** out_offsets, uint8_t** out_bits,
                          uint8_t* out_values, uint8_t* out_leaf_bits, size_t* counts, size_t* out_rows);
+int orc_read_nest_page(const uint8_t* page, size_t len, size_t num_levels, int depth, const int* nest_nullable,
+                       uint32_t struct_mask, int item_nullable, int kind, int width, int64_t** out_offsets,
+                       uint8_t** out_bits, uint8_t* out_values, uint8_t* out_leaf_bits, size_t* counts,
+                       size_t* out_rows);
+int orc_write_levels_page(const uint32_t* rep, const uint32_t* def, size_t n_levels, uint32_t max_rep,
+                          uint32_t max_def, uint32_t rows, orc_buf* out);
 int orc_read_list_page(const uint8_t* page, size_t len, size_t num_levels, int list_nullable, int item_nullable,
                        int kind, int width, int64_t* out_offsets, uint8_t* out_list_bits, uint8_t* out_values,
                        uint8_t* out_leaf_bits, size_t* out_rows, size_t* out_leaves);

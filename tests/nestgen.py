@@ -1,0 +1,145 @@
+"""Nested (Struct / Map / List) columns for the tests: a random array of a
+field spec (oracle.nest.F), the same array as a pyarrow array, and the
+reference's integration shapes (tests/it/io.rs:167-278, 294-341) plus
+nullable-struct variants.
+
+Children of a null struct / list slot are null where they are nullable
+(and lists under them empty): the arrays pyarrow builds from Python None
+are not (`pa.array([None], struct)` keeps valid children), and arrow2's
+level writer (RepLevelsIter / DefLevelsIter) reads the children's own
+validity under a null struct, so only such arrays round-trip through the
+reference writer."""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle.nest import A, F
+
+LEAF_DTYPES = {"i32": np.int32, "i64": np.int64, "f64": np.float64, "u8": np.uint8, "i16": np.int16}
+
+
+def leaf(kind, nullable, name="", large=False):
+    if kind in ("utf8", "binary"):
+        return F("leaf", nullable, leaf="binary", large=large, name=name)
+    if kind == "bool":
+        return F("leaf", nullable, leaf="bool", name=name)
+    return F("leaf", nullable, leaf="fixed", dtype=np.dtype(LEAF_DTYPES[kind]), name=name)
+
+
+def lst(child, nullable, name="", large=False):
+    return F("large_list" if large else "list", nullable, [child], name=name)
+
+
+def struct(children, nullable, name=""):
+    return F("struct", nullable, list(children), name=name)
+
+
+def map_(key, value, nullable, name=""):
+    return F("map", nullable, [struct([key, value], False, "entries")], name=name)
+
+
+def gen(f: F, n: int, rng, parent_valid=None, null_density=0.2, uniq=None) -> A:
+    """A random array of field f with n slots; parent_valid (bool per slot
+    or None) nulls the nullable children of null parents."""
+    pv = np.ones(n, bool) if parent_valid is None else parent_valid
+    validity = None
+    if f.nullable:
+        validity = (rng.random(n) >= null_density) & pv
+    live = pv if validity is None else validity
+    if f.kind == "leaf":
+        if f.leaf == "fixed":
+            dt = f.dtype
+            hi = uniq or max(2, n)
+            if dt.kind == "f":
+                vals = rng.integers(0, hi, n).astype(dt)
+            else:
+                vals = rng.integers(0, min(hi, np.iinfo(dt).max), n).astype(dt)
+            return A("leaf", n, validity, values=vals)
+        if f.leaf == "bool":
+            return A("leaf", n, validity, values=rng.random(n) < 0.5)
+        hi = uniq or max(2, n)
+        strs = [str(int(x)).encode() for x in rng.integers(0, hi, n)]
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum([len(s) for s in strs])
+        return A("leaf", n, validity, values=(offs, b"".join(strs)))
+    if f.kind == "struct":
+        kids = [gen(c, n, rng, live, null_density, uniq) for c in f.children]
+        return A("struct", n, validity, children=kids)
+    # list / map: lengths uniform {0, 1, 2} (io.rs:399-415), null / dead slots empty
+    lens = np.where(live, rng.integers(0, 3, n), 0)
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    child = gen(f.children[0], int(offs[-1]), rng, None, null_density, uniq)
+    return A(f.kind, n, validity, offsets=offs, children=[child])
+
+
+def pa_type(f: F):
+    import pyarrow as pa
+
+    if f.kind == "leaf":
+        if f.leaf == "binary":
+            return pa.large_binary() if f.large else pa.binary()
+        if f.leaf == "bool":
+            return pa.bool_()
+        return pa.from_numpy_dtype(f.dtype)
+    if f.kind == "struct":
+        return pa.struct([pa_field(c) for c in f.children])
+    if f.kind == "map":
+        e = f.children[0]
+        return pa.map_(pa_field(e.children[0]), pa_field(e.children[1]))
+    t = pa_field(f.children[0])
+    return pa.large_list(t) if f.kind == "large_list" else pa.list_(t)
+
+
+def pa_field(f: F):
+    import pyarrow as pa
+
+    return pa.field(f.name or "item", pa_type(f), nullable=f.nullable)
+
+
+def to_pa(f: F, a: A):
+    """The same array in pyarrow (children as they are, nulls and all)."""
+    import pyarrow as pa
+
+    mask = None if a.validity is None else pa.array(~np.asarray(a.validity, bool))
+    if f.kind == "leaf":
+        if f.leaf == "binary":
+            offs, data = a.values
+            vals = [None if (a.validity is not None and not a.validity[i]) else data[offs[i]:offs[i + 1]]
+                    for i in range(a.length)]
+            return pa.array(vals, type=pa_type(f))
+        return pa.array(a.values, type=pa_type(f), mask=None if a.validity is None else ~np.asarray(a.validity, bool))
+    if f.kind == "struct":
+        kids = [to_pa(c, x) for c, x in zip(f.children, a.children)]
+        return pa.StructArray.from_arrays(kids, fields=[pa_field(c) for c in f.children], mask=mask)
+    if f.kind == "map":
+        e, ea = f.children[0], a.children[0]
+        keys, items = to_pa(e.children[0], ea.children[0]), to_pa(e.children[1], ea.children[1])
+        return pa.MapArray.from_arrays(pa.array(a.offsets.astype(np.int32)), keys, items, type=pa_type(f),
+                                       mask=mask)
+    child = to_pa(f.children[0], a.children[0])
+    if f.kind == "large_list":
+        return pa.LargeListArray.from_arrays(pa.array(a.offsets), child, type=pa_type(f), mask=mask)
+    return pa.ListArray.from_arrays(pa.array(a.offsets.astype(np.int32)), child, type=pa_type(f), mask=mask)
+
+
+def shapes():
+    """name -> field: the reference's test_struct / test_map /
+    test_list_struct / test_list_map / test_struct_list (io.rs:167-278) and
+    variants with null structs, structs in structs, Boolean and Float leaves."""
+    name_age = lambda n: struct([leaf("binary", True, "name", large=True), leaf("i32", True, "age")], n)  # noqa: E731
+    kv = lambda n: map_(leaf("i32", False, "key"), leaf("binary", True, "value", large=True), n)  # noqa: E731
+    return {
+        "struct": name_age(False),  # io.rs:168-172, create_struct: validity None
+        "map": kv(True),  # io.rs:189-193, create_map: offsets with nulls
+        "list_struct": lst(name_age(True), False),  # io.rs:216-233
+        "list_map": lst(kv(True), False),  # io.rs:236-253
+        "struct_list": struct([leaf("binary", True, "name", large=True),
+                               lst(leaf("i32", True), True, "age")], False),  # io.rs:256-278
+        "null_struct": name_age(True),
+        "struct_struct": struct([leaf("i64", True, "a"),
+                                 struct([leaf("bool", True, "b"), leaf("f64", False, "c")], True, "s")], True),
+        "list_null_struct_list": lst(struct([lst(leaf("i16", True), True, "l"), leaf("utf8", True, "u")], True), True),
+        "map_of_list": map_(leaf("i32", False, "key"), lst(leaf("i64", True), True, "value"), True),
+        "req_struct_req": struct([leaf("i32", False, "x"), leaf("u8", False, "y")], False),
+    }
