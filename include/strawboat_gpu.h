@@ -194,24 +194,34 @@ uint64_t sb_plan_num_leaves(const sb_plan* plan);
  * + the values streams at their leaf bases. */
 sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* plan, const sb_list_out* out);
 
-/* A primitive leaf under 1..4 list levels (List<List<T>> ...): the general
- * read_validity_nested (read/read_basic.rs:95-164) -- per-level cum_sum /
- * cum_rep over {nullable, repeated}, lists and primitives never "required" --
- * then create_list per level (read/array/list.rs:48), pages concatenated with
- * each level's offsets moved onto its child's running length.  Level 0 is
- * the outermost list.  PageMeta.num_values is the page's level count. */
+/* One leaf column of a nested field under 1..4 nests: the InitNested chain
+ * deserialize_nested builds (read/deserialize.rs:140-233) -- a List /
+ * LargeList / FixedSizeList / Map pushes InitNested::List(nullable), a Struct
+ * InitNested::Struct(nullable) for each of its children's leaves.  The
+ * general read_validity_nested (read/read_basic.rs:95-164): per-nest
+ * cum_sum / cum_rep over {nullable, repeated}, lists and the leaf never
+ * "required", structs always (arrow2 NestedStruct / NestedStructValid: a
+ * null struct pushes a slot into every child); then create_list /
+ * create_map per list nest (read/array/list.rs:48, map.rs) with the pages
+ * concatenated and each list's offsets moved onto its child's running
+ * length.  Nest 0 is the outermost.  PageMeta.num_values is the page's level
+ * count.  A Struct / Map field is several leaf columns (to_leaves order),
+ * each planned on its own; create_struct takes the struct's validity from
+ * its LAST child (read/array/struct_.rs:101-114), and every leaf under a
+ * struct nest yields that nest's entries and validity. */
 #define SB_MAX_NEST 4
 typedef struct {
   int32_t physical_type;                /* leaf type: fixed width, Boolean, Binary / Utf8 (Large too) */
-  int32_t depth;                        /* list levels, 1..SB_MAX_NEST */
-  int32_t list_nullable[SB_MAX_NEST];   /* list level d is nullable */
+  int32_t depth;                        /* nests, 1..SB_MAX_NEST */
+  int32_t list_nullable[SB_MAX_NEST];   /* nest d is nullable (list, map or struct) */
   int32_t item_nullable;                /* the leaf is nullable */
-  int32_t offset_width;                 /* 4 = List, 8 = LargeList (every level) */
+  int32_t offset_width;                 /* 4 = List / Map, 8 = LargeList (every list nest) */
+  int32_t struct_mask;                  /* bit d: nest d is a Struct (no offsets), else a List / Map */
 } sb_nested_desc;
 
-/* d_offsets[d]: sb_plan_nested_count(plan, d) + 1 entries; d_validity[d]
- * over level d's entries (NULL when not nullable); d_leaf_validity over the
- * leaves.  Leaf values: fixed width -- d_values holds
+/* d_offsets[d] (list nests; NULL for struct nests): sb_plan_nested_count(plan,
+ * d) + 1 entries; d_validity[d] over nest d's entries (NULL when not
+ * nullable); d_leaf_validity over the leaves.  Leaf values: fixed width -- d_values holds
  * sb_plan_nested_count(plan, depth) values; Boolean -- d_values is their
  * bitmap; Binary / Utf8 -- d_leaf_offsets holds leaves + 1 offsets (the
  * physical type's width) and d_values values_capacity >=
@@ -395,22 +405,30 @@ void sb_free(void* p);
 /* One leaf of the schema in arrow2's to_leaves order (write/common.rs:68),
  * i.e. the order of the file's columns: its logical type (the IPC Schema.fbs
  * Type union tag), the reader's physical type (0 when no page path exists,
- * e.g. Decimal, Float16), and the list levels above it. */
-#define SB_LEAF_STRUCT 1u          /* a Struct lies on the path (not decoded here) */
-#define SB_LEAF_MAP 2u             /* a Map lies on the path (not decoded here) */
+ * e.g. Decimal, Float16), and the nests above it -- the InitNested chain of
+ * deserialize_nested (read/deserialize.rs:202-230): List / LargeList / Map
+ * (and FixedSizeList) nests and Struct nests, outermost first, each with a
+ * schema-wide id (pre-order) so the leaves of one struct or map can be
+ * grouped back into their field (sb_nested_desc takes depth,
+ * list_nullable and struct_mask as they are here). */
+#define SB_LEAF_STRUCT 1u          /* a Struct lies on the path (a struct nest) */
+#define SB_LEAF_MAP 2u             /* a Map lies on the path (a list nest over its entries struct) */
 #define SB_LEAF_FIXED_SIZE_LIST 4u /* a FixedSizeList lies on the path (not decoded here) */
 #define SB_LEAF_UNION 8u           /* a Union lies on the path (not decoded here) */
-#define SB_LEAF_TOO_DEEP 16u       /* more than SB_MAX_NEST list levels */
+#define SB_LEAF_TOO_DEEP 16u       /* more than SB_MAX_NEST nests */
 typedef struct {
   char name[64];                      /* the leaf field's name (truncated) */
   int32_t arrow_type;                 /* Schema.fbs Type tag: Int 2, FloatingPoint 3, Binary 4, Utf8 5, Bool 6, ... */
   int32_t physical_type;              /* sb_physical_type, 0 = none */
   int32_t nullable;                   /* the leaf field's nullable flag */
-  int32_t depth;                      /* list levels above the leaf */
-  int32_t list_nullable[SB_MAX_NEST]; /* per list level, outermost first */
-  int32_t large_list[SB_MAX_NEST];    /* LargeList (i64 offsets) per level */
+  int32_t depth;                      /* nests above the leaf */
+  int32_t list_nullable[SB_MAX_NEST]; /* per nest, outermost first: the nest field is nullable */
+  int32_t large_list[SB_MAX_NEST];    /* LargeList (i64 offsets) per nest */
   uint32_t flags;                     /* SB_LEAF_* */
   int32_t top_field;                  /* index of the top-level field it belongs to */
+  uint32_t struct_mask;               /* bit d: nest d is a Struct */
+  uint32_t map_mask;                  /* bit d: nest d is a Map (its child nest is the entries struct) */
+  int32_t nest_id[SB_MAX_NEST];       /* per nest: the nest field's pre-order id in the schema */
 } sb_leaf_info;
 
 /* infer_schema (read/reader.rs:227-241) + arrow2 deserialize_schema: the

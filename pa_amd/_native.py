@@ -68,7 +68,8 @@ class LeafInfoC(ctypes.Structure):
     """sb_leaf_info"""
     _fields_ = [("name", ctypes.c_char * 64), ("arrow_type", ctypes.c_int32), ("physical_type", ctypes.c_int32),
                 ("nullable", ctypes.c_int32), ("depth", ctypes.c_int32), ("list_nullable", ctypes.c_int32 * MAX_NEST),
-                ("large_list", ctypes.c_int32 * MAX_NEST), ("flags", ctypes.c_uint32), ("top_field", ctypes.c_int32)]
+                ("large_list", ctypes.c_int32 * MAX_NEST), ("flags", ctypes.c_uint32), ("top_field", ctypes.c_int32),
+                ("struct_mask", ctypes.c_uint32), ("map_mask", ctypes.c_uint32), ("nest_id", ctypes.c_int32 * MAX_NEST)]
 
 
 class PrimitiveOutC(ctypes.Structure):

@@ -983,6 +983,7 @@ static sb_status nest_launch(sb_ctx* ctx, sb_plan* p, const sb_nested_out* out, 
   for (uint64_t d = 0; d < D; d++) L.nullable |= (p->ndesc.list_nullable[d] ? 1u : 0u) << d;
   L.nullable |= (p->ndesc.item_nullable ? 1u : 0u) << D;
   L.offset_width = (uint32_t)p->ndesc.offset_width;
+  L.struct_mask = (uint32_t)p->ndesc.struct_mask;
   L.counts = p->d_nest;
   L.bases = p->d_nest + n * (D + 1);
   L.totals = p->d_nest + 2 * n * (D + 1);
@@ -1010,6 +1011,8 @@ sb_status sb_plan_nested_column(sb_ctx* ctx, const sb_nested_desc* d, const uint
   if (!type_width(t, &is_float) && t != SB_T_BOOLEAN && !leaf_bin)
     return fail(ctx, SB_E_NYI, "nested leaf type %d not supported", t);
   if (d->depth < 1 || d->depth > SB_MAX_NEST) return fail(ctx, SB_E_NYI, "nesting depth %d not supported", d->depth);
+  if (d->struct_mask < 0 || (d->struct_mask >> d->depth) != 0)
+    return fail(ctx, SB_E_ARG, "struct mask 0x%x names nests past depth %d", (unsigned)d->struct_mask, d->depth);
   if (d->offset_width != 4 && d->offset_width != 8) return fail(ctx, SB_E_ARG, "offset width must be 4 or 8");
   if (n_pages > 0xFFFFFFFFull) return fail(ctx, SB_E_ARG, "too many pages");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1099,7 +1102,8 @@ sb_status sb_decode_nested_planned(sb_ctx* ctx, sb_plan* p, const sb_nested_out*
   if (!p->nested) return fail(ctx, SB_E_ARG, "not a nested plan");
   const int D = p->ndesc.depth;
   for (int d = 0; d < D; d++) {
-    if (!out->d_offsets[d]) return fail(ctx, SB_E_ARG, "offsets of level %d are null", d);
+    const bool is_list = !((p->ndesc.struct_mask >> d) & 1);
+    if (is_list && !out->d_offsets[d]) return fail(ctx, SB_E_ARG, "offsets of level %d are null", d);
     if (p->ndesc.list_nullable[d] && p->nest_totals[d] && !out->d_validity[d])
       return fail(ctx, SB_E_ARG, "validity of level %d is null", d);
   }
@@ -1114,7 +1118,9 @@ sb_status sb_decode_nested_planned(sb_ctx* ctx, sb_plan* p, const sb_nested_out*
   if (p->ndesc.item_nullable && p->n_leaves)
     HIP_TRY(ctx, hipMemsetAsync(out->d_leaf_validity, 0, (p->n_leaves + 31) / 32 * 4, ctx->stream));
   if (!p->n_pages) {
-    for (int d = 0; d < D; d++) HIP_TRY(ctx, hipMemsetAsync(out->d_offsets[d], 0, (size_t)p->ndesc.offset_width, ctx->stream));
+    for (int d = 0; d < D; d++)
+      if (!((p->ndesc.struct_mask >> d) & 1))
+        HIP_TRY(ctx, hipMemsetAsync(out->d_offsets[d], 0, (size_t)p->ndesc.offset_width, ctx->stream));
   } else {
     sb_status lst = nest_launch(ctx, p, out, 1);
     if (lst) return lst;
@@ -1123,7 +1129,7 @@ sb_status sb_decode_nested_planned(sb_ctx* ctx, sb_plan* p, const sb_nested_out*
       sb_binary_out bo{out->d_leaf_offsets, (uint8_t*)out->d_values, out->values_capacity, nullptr};
       st = sb_decode_binary_planned(ctx, p->inner, &bo);
     } else {
-      sb_primitive_out vo{out->d_values ? out->d_values : out->d_offsets[0], nullptr};  // (no leaves: nothing written)
+      sb_primitive_out vo{out->d_values, nullptr};  // (no leaves: nothing written)
       st = sb_decode_planned(ctx, p->inner, &vo);
     }
     if (st) return st;

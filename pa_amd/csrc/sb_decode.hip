@@ -5074,20 +5074,27 @@ __global__ __launch_bounds__(NT) void k_list_levels(ListArgs a) {
 }
 
 // ===========================================================================
-// General nesting: a leaf under `depth` list levels (List<List<T>> ...),
+// General nesting: a leaf under `depth` nests (List / Map / Struct chains,
+// the InitNested chain of read/deserialize.rs:140-233),
 // read_validity_nested (read/read_basic.rs:95-164) level by level: nests
-// 0..depth-1 are lists (repeated; nullable per level), nest `depth` the
-// primitive; cum_sum / cum_rep over (nullable + repeated) / repeated; a nest
-// is pushed when rep <= cum_rep[d] && def >= cum_sum[d] (is_required is false
-// for lists and primitives, so the chain rule never fires).  One wave per
-// page, one level per lane per step: ballots give each level's pushes and
-// ranks; a list push's offset is its child's running count; validity bits
-// are compacted to push order and OR-ed into the (zeroed) bitmaps.
+// 0..depth-1 are lists (repeated; nullable per level) or, where bit d of
+// struct_mask is set, structs (not repeated; arrow2's NestedStruct /
+// NestedStructValid are "required"), nest `depth` the primitive; cum_sum /
+// cum_rep over (nullable + repeated) / repeated; a nest is pushed when
+// rep <= cum_rep[d] && def >= cum_sum[d], or when the nest above is a struct
+// that was pushed and is not valid (the is_required chain, :118-137: every
+// child of a null struct gets a slot).  One wave per page, one level per
+// lane per step: each lane runs the chain over its level, ballots give each
+// nest's pushes and ranks; a list push's offset is its child's running
+// count; validity bits are compacted to push order and OR-ed into the
+// (zeroed) bitmaps.  A zero-width level stream (max level 0: a chain of
+// required structs writes none) reads as all zeros, as parquet2's
+// HybridRleDecoder does with num_bits 0.
 // ===========================================================================
 struct NestArgs {
   const uint8_t* chunk;
   const PageDesc* pages;
-  uint32_t n_pages, depth, nullable, ow;
+  uint32_t n_pages, depth, nullable, ow, smask;
   uint64_t* counts;
   const uint64_t* bases;
   const uint64_t* totals;
@@ -5112,6 +5119,14 @@ struct RunWin {
 
 // lane 0: make the window cover levels [l0, lend)
 __device__ bool runwin_advance(const GlbSrc& s, RunWin& R, uint32_t l0, uint32_t lend, uint32_t* err) {
+  if (R.bw == 0) {  // no stream: one RLE run of zeros over every level
+    R.n = 1;
+    R.start[0] = 0;
+    R.arg[0] = 0;
+    R.covered = 0xFFFFFFFFu;
+    R.start[1] = R.covered;
+    return true;
+  }
   uint32_t k = R.n;
   while (k > 0 && R.start[k - 1] > l0) k--;
   if (k > 1) {  // keep the run holding l0
@@ -5198,7 +5213,7 @@ __global__ __launch_bounds__(NT) void k_nest_walk(NestArgs a) {
   uint32_t cum_sum[kMaxNest + 2], cum_rep[kMaxNest + 2];
   cum_sum[0] = cum_rep[0] = 0;
   for (uint32_t d = 0; d <= D; d++) {
-    const uint32_t nl = (a.nullable >> d) & 1, rp = d < D ? 1u : 0u;
+    const uint32_t nl = (a.nullable >> d) & 1, rp = (d < D && !((a.smask >> d) & 1)) ? 1u : 0u;
     cum_sum[d + 1] = cum_sum[d] + nl + rp;
     cum_rep[d + 1] = cum_rep[d] + rp;
   }
@@ -5245,12 +5260,17 @@ __global__ __launch_bounds__(NT) void k_nest_walk(NestArgs a) {
         // consumed: inclusive row count <= rows (read_basic.rs:150-162)
         const bool cons = in && rows_seen + (uint32_t)__popcll(rs & (below | (1ull << lane))) <= rows;
         uint64_t push[kMaxNest + 1];
-        for (uint32_t d = 0; d <= D; d++) push[d] = __ballot(cons && r <= cum_rep[d] && dv >= cum_sum[d]);
+        bool forced = false;  // the is_required chain: the nest above is a struct pushed invalid
+        for (uint32_t d = 0; d <= D; d++) {
+          const bool me = cons && (forced || (r <= cum_rep[d] && dv >= cum_sum[d]));
+          push[d] = __ballot(me);
+          forced = me && ((a.smask >> d) & 1) && !(((a.nullable >> d) & 1) && dv > cum_sum[d]);
+        }
         if (WRITE) {
           for (uint32_t d = 0; d <= D; d++) {
             const bool me = (push[d] >> lane) & 1;
             const uint64_t pos = base[d] + carry[d] + (uint32_t)__popcll(push[d] & below);
-            if (d < D && me) {  // offset = the child's count before this level
+            if (d < D && me && !((a.smask >> d) & 1)) {  // list offset = the child's count before this level
               const uint64_t v = base[d + 1] + carry[d + 1] + (uint32_t)__popcll(push[d + 1] & below);
               bin_put_off(a.out_offsets[d], pos, v, (int)a.ow);
             }
@@ -5281,8 +5301,9 @@ __global__ __launch_bounds__(NT) void k_nest_walk(NestArgs a) {
         const bool ok = err == 0;
         a.vpages[page] = PageDesc{pd.byte_off + (ok ? w.vpos : 0), base[D], ok ? pd.byte_len - w.vpos : 0,
                                   ok ? (uint32_t)carry[D] : 0u, a.vpages[page].reserved};
-        if (page == a.n_pages - 1)  // create_list appends each child's length
-          for (uint32_t d = 0; d < D; d++) bin_put_off(a.out_offsets[d], a.totals[d], a.totals[d + 1], (int)a.ow);
+        if (page == a.n_pages - 1)  // create_list / create_map append each child's length
+          for (uint32_t d = 0; d < D; d++)
+            if (!((a.smask >> d) & 1)) bin_put_off(a.out_offsets[d], a.totals[d], a.totals[d + 1], (int)a.ow);
       }
       a.status[page] = err;
     }
@@ -5520,7 +5541,7 @@ int launch_list(int stage, const ListLaunch& L, void* stream) {
 namespace sb {
 int launch_nest(int stage, const NestLaunch& L, void* stream) {
   if (L.n_pages == 0) return 0;
-  sbk::NestArgs a{L.chunk, L.pages, L.n_pages, L.depth, L.nullable, L.offset_width, L.counts, L.bases, L.totals,
+  sbk::NestArgs a{L.chunk, L.pages, L.n_pages, L.depth, L.nullable, L.offset_width, L.struct_mask, L.counts, L.bases, L.totals,
                   L.vpages, {}, {}, L.out_leaf_validity, L.status, L.vpos};
   for (int d = 0; d < kMaxNest; d++) {
     a.out_offsets[d] = L.out_offsets[d];

@@ -128,6 +128,7 @@ struct Walk {
   Fb& fb;
   std::vector<sb_leaf_info>& out;
   int top = 0;
+  int32_t next_nest = 0;
   bool fail = false;
   uint64_t visits = 0;
 
@@ -142,23 +143,43 @@ struct Walk {
     uint32_t nch = 0;
     const uint64_t ch = fb.vec(f, 5, &nch);
     auto child = [&](uint32_t k) { return fb.deref(ch + 4ull * k); };
+    // a nest of deserialize_nested's InitNested chain (read/deserialize.rs:
+    // 202-230): List / LargeList / FixedSizeList / Map -> InitNested::List,
+    // Struct -> InitNested::Struct; ids number the nest fields in pre-order
+    // so leaves under one struct or map share theirs
+    auto push_nest = [&](bool is_struct) {
+      if (path.depth < SB_MAX_NEST) {
+        path.list_nullable[path.depth] = nullable;
+        path.large_list[path.depth] = tag == kLargeList;
+        path.nest_id[path.depth] = next_nest;
+        if (is_struct) path.struct_mask |= 1u << path.depth;
+        if (tag == kMap) path.map_mask |= 1u << path.depth;
+      }
+      next_nest++;
+      path.depth++;
+    };
     if (tag == kList || tag == kLargeList || tag == kFixedSizeList || tag == kMap) {
       if (nch != 1) {
         fail = true;
         return;
       }
-      if (path.depth < SB_MAX_NEST) {
-        path.list_nullable[path.depth] = nullable;
-        path.large_list[path.depth] = tag == kLargeList;
-      }
-      path.depth++;
+      push_nest(false);
       if (tag == kFixedSizeList) path.flags |= SB_LEAF_FIXED_SIZE_LIST;
       if (tag == kMap) path.flags |= SB_LEAF_MAP;
       field(child(0), path, level + 1);
       return;
     }
-    if (tag == kStruct || tag == kUnion) {
-      path.flags |= tag == kStruct ? SB_LEAF_STRUCT : SB_LEAF_UNION;
+    if (tag == kStruct) {
+      if (nch == 0) {  // a struct without fields has no leaf column (n_columns 0)
+        return;
+      }
+      push_nest(true);
+      path.flags |= SB_LEAF_STRUCT;
+      for (uint32_t k = 0; k < nch && !fail; k++) field(child(k), path, level + 1);
+      return;
+    }
+    if (tag == kUnion) {
+      path.flags |= SB_LEAF_UNION;
       for (uint32_t k = 0; k < nch && !fail; k++) field(child(k), path, level + 1);
       return;
     }

@@ -246,8 +246,9 @@ struct NestLaunch {
   const PageDesc* pages;
   uint32_t n_pages;
   uint32_t depth;
-  uint32_t nullable;       // bit d: list level d nullable (d < depth); bit depth: the leaf
+  uint32_t nullable;       // bit d: nest d nullable (d < depth); bit depth: the leaf
   uint32_t offset_width;
+  uint32_t struct_mask;    // bit d: nest d is a Struct (InitNested::Struct), else a List / Map
   uint64_t* counts;        // [n_pages][depth + 1] entries per level (stage 0 out)
   const uint64_t* bases;   // [n_pages][depth + 1] first entry of each level (stage 1 in)
   const uint64_t* totals;  // [depth + 1]

@@ -40,13 +40,24 @@ class Leaf:
     large_list: List[bool] = field(default_factory=list)
     flags: int = 0
     top_field: int = 0
+    struct_mask: int = 0
+    map_mask: int = 0
+    nest_id: List[int] = field(default_factory=list)
+
+    def nest_kind(self, d: int) -> str:
+        if (self.struct_mask >> d) & 1:
+            return "struct"
+        if (self.map_mask >> d) & 1:
+            return "map"
+        return "large_list" if self.large_list[d] else "list"
 
 
 def _leaf(c: N.LeafInfoC) -> Leaf:
     d = min(c.depth, N.MAX_NEST)
     return Leaf(c.name.decode(errors="replace"), ARROW_TYPE.get(c.arrow_type, str(c.arrow_type)), c.physical_type,
                 bool(c.nullable), c.depth, [bool(c.list_nullable[i]) for i in range(d)],
-                [bool(c.large_list[i]) for i in range(d)], c.flags, c.top_field)
+                [bool(c.large_list[i]) for i in range(d)], c.flags, c.top_field, c.struct_mask, c.map_mask,
+                [int(c.nest_id[i]) for i in range(d)])
 
 
 def parse_schema(schema_bytes: bytes) -> List[Leaf]:
@@ -134,7 +145,7 @@ class StrawboatFile:
             chunk = self.upload(col, ctx)
         metas = self.columns[col].pages
         pt = leaf.physical_type
-        if leaf.flags or not pt:
+        if leaf.flags & ~(LEAF_STRUCT | LEAF_MAP) or not pt:
             raise N.StrawboatError(N.E_NYI, f"leaf {leaf.name}: {leaf.arrow_type} (flags {leaf.flags}) has no page path here")
         binary = pt in (BINARY, LARGE_BINARY, UTF8, LARGE_UTF8)
         dtype = _DTYPE.get(pt, np.uint8)
@@ -142,13 +153,67 @@ class StrawboatFile:
             if binary:
                 return BinaryColumnDecoder(chunk, metas, pt, leaf.nullable, ctx=ctx)
             return ColumnDecoder(chunk, metas, dtype, leaf.nullable, ctx=ctx)
-        large = leaf.large_list[0]
-        if any(x != large for x in leaf.large_list):
+        lists = [leaf.large_list[d] for d in range(leaf.depth) if not (leaf.struct_mask >> d) & 1]
+        large = bool(lists and lists[0])
+        if any(x != large for x in lists):
             raise N.StrawboatError(N.E_NYI, f"leaf {leaf.name}: mixed List / LargeList levels")
-        if leaf.depth == 1 and not binary and pt != N.BOOLEAN:
+        if leaf.depth == 1 and not leaf.struct_mask and not binary and pt != N.BOOLEAN:
             return ListColumnDecoder(chunk, metas, dtype, leaf.list_nullable[0], leaf.nullable, ctx=ctx, large=large)
         return NestedColumnDecoder(chunk, metas, dtype, leaf.list_nullable, leaf.nullable, ctx=ctx, large=large,
-                                   physical_type=pt)
+                                   physical_type=pt, struct_mask=leaf.struct_mask)
+
+    def field(self, top: int):
+        """The pa_amd.Field tree of top-level field `top`, rebuilt from its
+        leaves' nest chains (the nest ids group the leaves of one struct or
+        map) -> (Field, [leaf column indices])."""
+        from .nested import Field
+
+        cols = [c for c, l in enumerate(self.leaves) if l.top_field == top]
+        if not cols:
+            raise N.StrawboatError(N.E_ARG, f"no leaf columns for field {top}")
+
+        def build(cs, d):
+            first = self.leaves[cs[0]]
+            if d == first.depth:
+                assert len(cs) == 1
+                return Field.leaf(first.physical_type, first.nullable, first.name) if first.physical_type not in _DTYPE \
+                    else Field.leaf(_DTYPE[first.physical_type], first.nullable, first.name)
+            kind = first.nest_kind(d)
+            groups = []  # children: consecutive leaves sharing the nest id at d + 1 (or a leaf at d + 1)
+            for c in cs:
+                lf = self.leaves[c]
+                key = lf.nest_id[d + 1] if lf.depth > d + 1 else ("leaf", c)
+                if not groups or groups[-1][0] != key:
+                    groups.append((key, []))
+                groups[-1][1].append(c)
+            kids = [build(g, d + 1) for _, g in groups]
+            if kind != "struct" and len(kids) != 1:
+                raise N.StrawboatError(N.E_OUT_OF_SPEC, "a list nest with several children")
+            return Field(kind, bool(first.list_nullable[d]), kids)
+
+        if any(self.leaves[c].depth > N.MAX_NEST or self.leaves[c].flags & ~(LEAF_STRUCT | LEAF_MAP) for c in cols):
+            raise N.StrawboatError(N.E_NYI, f"field {top} has no page path here")
+        return build(cols, 0), cols
+
+    def read_field(self, top: int, ctx: Optional[Context] = None):
+        """batch_read_array for top-level field `top` (read/batch_read.rs:
+        190-209): a primitive field -> its column decoder's outputs, a nested
+        one -> a pa_amd.DeviceArray tree (FieldDecoder over its leaves)."""
+        from .nested import FieldDecoder
+
+        fld, cols = self.field(top)
+        ctx = resolve_context(ctx, None)
+        if fld.kind == "leaf":
+            dec = self.decoder(cols[0], ctx)
+            try:
+                return dec.decode()
+            finally:
+                dec.close()
+        dec = FieldDecoder(fld, [(self.upload(c, ctx), self.columns[c].pages) for c in cols], ctx)
+        try:
+            return dec.decode()
+        finally:
+            dec.close()
 
     def close(self):
         if getattr(self, "_h", None):

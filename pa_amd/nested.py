@@ -1,10 +1,14 @@
-"""Nested List<primitive> columns (one list level over a primitive leaf).
+"""Nested columns: List<primitive> (one list level over a primitive leaf),
+any List / Map / Struct chain over a leaf, and whole Struct / Map fields.
 
 Reference (b41sh/pa @ 2025-01-17):
   write_nested / write_nested_validity   src/write/serialize.rs:133-146, 217-232
   read_validity_nested                   src/read/read_basic.rs:65-173
   read_nested_integer / _double          src/read/array/integer.rs:240-261, double.rs
   create_list                            src/read/array/list.rs:48
+  deserialize_nested (InitNested chain)  src/read/deserialize.rs:140-233
+  create_struct / MapIterator            src/read/array/struct_.rs:101-114, map.rs
+  read_nested (batch)                    src/read/batch_read.rs:67-180
   encode_chunk (paging by top-level rows) src/write/common.rs:49-119
 
 encode_list_column -> sb_encode_list_column (host encoder)
@@ -14,6 +18,7 @@ batch_read_list    -> one ListArray per column: (offsets, list validity, values,
 from __future__ import annotations
 
 import ctypes
+from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -196,7 +201,7 @@ MAX_NEST = 4
 class NestedDescC(ctypes.Structure):
     _fields_ = [("physical_type", ctypes.c_int32), ("depth", ctypes.c_int32),
                 ("list_nullable", ctypes.c_int32 * MAX_NEST), ("item_nullable", ctypes.c_int32),
-                ("offset_width", ctypes.c_int32)]
+                ("offset_width", ctypes.c_int32), ("struct_mask", ctypes.c_int32)]
 
 
 class NestedOutC(ctypes.Structure):
@@ -223,15 +228,18 @@ def _nested_lib():
 
 
 class NestedColumnDecoder:
-    """A leaf under len(list_nullable) list levels (List<List<T>> ..., level 0
-    outermost): read_validity_nested in its general form (read_basic.rs:95-164)
-    + create_list per level.  decode() -> (offsets per level, validity per
-    level | None, values, leaf validity | None) device tensors; values is a
-    bitmap for a Boolean leaf (dtype bool) and (leaf offsets, value bytes) for
-    a Binary / Utf8 leaf (physical_type=pa_amd.UTF8 ...)."""
+    """A leaf under len(list_nullable) nests (List<List<T>>, List<Struct<..>>,
+    Map<K, V> ..., nest 0 outermost; bit d of struct_mask marks a Struct
+    nest): read_validity_nested in its general form (read_basic.rs:95-164)
+    + create_list per list nest.  decode() -> (offsets per nest | None for
+    struct nests, validity per nest | None, values, leaf validity | None)
+    device tensors; values is a bitmap for a Boolean leaf (dtype bool) and
+    (leaf offsets, value bytes) for a Binary / Utf8 leaf
+    (physical_type=pa_amd.UTF8 ...)."""
 
     def __init__(self, chunk, page_metas: Sequence[PageMeta], dtype, list_nullable, item_nullable: bool,
-                 ctx: Optional[Context] = None, large: bool = False, physical_type: Optional[int] = None):
+                 ctx: Optional[Context] = None, large: bool = False, physical_type: Optional[int] = None,
+                 struct_mask: int = 0):
         import torch
 
         self._torch = torch
@@ -242,6 +250,7 @@ class NestedColumnDecoder:
         if not 1 <= self.depth <= MAX_NEST:
             raise N.StrawboatError(N.E_NYI, f"nesting depth {self.depth} not supported")
         self.item_nullable = bool(item_nullable)
+        self.struct_mask = int(struct_mask)
         self.offset_width = 8 if large else 4
         self.chunk = _as_device_bytes(chunk, self.ctx.device)
         self.metas = list(page_metas)
@@ -250,7 +259,7 @@ class NestedColumnDecoder:
         ln = (ctypes.c_int32 * MAX_NEST)(*([int(x) for x in self.list_nullable] + [0] * (MAX_NEST - self.depth)))
         self.phys = physical_type if physical_type is not None else globals()["physical_type"](self.dtype)
         self.binary = self.phys in (BINARY, UTF8, LARGE_BINARY, LARGE_UTF8)
-        desc = NestedDescC(self.phys, self.depth, ln, int(self.item_nullable), self.offset_width)
+        desc = NestedDescC(self.phys, self.depth, ln, int(self.item_nullable), self.offset_width, self.struct_mask)
         h = ctypes.c_void_p()
         st = L.sb_plan_nested_column(self.ctx._h, ctypes.byref(desc), ctypes.c_void_p(self.chunk.data_ptr()),
                                      self.chunk.numel(), metas, len(self.metas), ctypes.byref(h))
@@ -265,7 +274,8 @@ class NestedColumnDecoder:
         dev = f"cuda:{self.ctx.device}"
         odt = torch.int64 if self.offset_width == 8 else torch.int32
         bm = lambda n: torch.empty(max((n + 31) // 32, 1) * 4, dtype=torch.uint8, device=dev)  # noqa: E731
-        offs = [torch.empty(self.counts[d] + 1, dtype=odt, device=dev) for d in range(self.depth)]
+        offs = [None if self.is_struct(d) else torch.empty(self.counts[d] + 1, dtype=odt, device=dev)
+                for d in range(self.depth)]
         valid = [bm(self.counts[d]) if self.list_nullable[d] else None for d in range(self.depth)]
         nleaf = self.counts[self.depth]
         if self.binary:
@@ -279,6 +289,9 @@ class NestedColumnDecoder:
             values = torch.empty(max(nleaf, 1), dtype=tdt, device=dev)
         leaf = bm(nleaf) if self.item_nullable else None
         return offs, valid, values, leaf
+
+    def is_struct(self, d: int) -> bool:
+        return bool((self.struct_mask >> d) & 1)
 
     def decode(self, outs=None):
         offs, valid, values, leaf = outs or self.alloc_outputs()
@@ -315,3 +328,158 @@ class NestedColumnDecoder:
         except Exception:
             pass
 
+
+
+# ---- whole nested fields: Struct / Map / List trees over several leaves -------
+@dataclass
+class Field:
+    """An arrow2 Field restricted to the codec path (the read/deserialize.rs
+    dispatch).  kind: "list", "large_list", "map", "struct" or "leaf"; a map's
+    one child is its entries struct (key, value); a leaf carries its
+    physical type (pa_amd.read.physical_type(dtype), BOOLEAN, BINARY / UTF8 /
+    LARGE_*) and, for fixed-width leaves, the numpy dtype."""
+    kind: str
+    nullable: bool
+    children: List["Field"] = field(default_factory=list)
+    physical_type: int = 0
+    dtype: object = None
+    name: str = ""
+
+    @staticmethod
+    def leaf(dtype_or_type, nullable: bool, name: str = "") -> "Field":
+        if isinstance(dtype_or_type, (int, np.integer)):
+            return Field("leaf", nullable, physical_type=int(dtype_or_type), name=name)
+        dt = np.dtype(dtype_or_type)
+        return Field("leaf", nullable, physical_type=physical_type(dt), dtype=dt, name=name)
+
+    @staticmethod
+    def list(child: "Field", nullable: bool, large: bool = False, name: str = "") -> "Field":
+        return Field("large_list" if large else "list", nullable, [child], name=name)
+
+    @staticmethod
+    def struct(children, nullable: bool, name: str = "") -> "Field":
+        return Field("struct", nullable, list(children), name=name)
+
+    @staticmethod
+    def map(key: "Field", value: "Field", nullable: bool, name: str = "") -> "Field":
+        return Field("map", nullable, [Field("struct", False, [key, value], name="entries")], name=name)
+
+    def n_columns(self) -> int:
+        """arrow2 n_columns: the leaf columns under this field."""
+        return 1 if self.kind == "leaf" else sum(c.n_columns() for c in self.children)
+
+    def leaf_paths(self, prefix=()):
+        """to_leaves order (write/common.rs:66-71): depth first."""
+        path = prefix + (self,)
+        if self.kind == "leaf":
+            return [path]
+        return [p for c in self.children for p in c.leaf_paths(path)]
+
+
+@dataclass
+class DeviceArray:
+    """A decoded nested array in HBM.  validity: a 32-bit-word Arrow bitmap
+    (uint8 tensor) or None; list / map: offsets and children[0]; struct:
+    children; leaf: values (fixed width: a typed tensor; Boolean: a bitmap;
+    Binary / Utf8: (offsets, bytes))."""
+    kind: str
+    length: int
+    validity: object = None
+    offsets: object = None
+    children: List["DeviceArray"] = field(default_factory=list)
+    values: object = None
+
+
+def init_chain(path):
+    """deserialize_nested's InitNested chain for one leaf path
+    (read/deserialize.rs:140-233) -> (nest nullable, struct_mask, leaf
+    nullable, large list offsets)."""
+    nulls, mask, large = [], 0, set()
+    for d, f in enumerate(path[:-1]):
+        nulls.append(bool(f.nullable))
+        if f.kind == "struct":
+            mask |= 1 << d
+        else:
+            large.add(f.kind == "large_list")
+    if len(large) > 1:
+        raise N.StrawboatError(N.E_NYI, "List and LargeList nests in one chain")
+    return tuple(nulls), mask, bool(path[-1].nullable), large == {True}
+
+
+class FieldDecoder:
+    """batch_read_array / column_iter_to_arrays for a nested field
+    (read/batch_read.rs:67-180, read/deserialize.rs:140-233): one
+    NestedColumnDecoder per leaf column (to_leaves order), each with the
+    leaf's InitNested chain; decode() assembles the array tree, a nest's
+    offsets and validity taken from the LAST leaf under it (create_list /
+    create_map / create_struct pop the last child's NestedState,
+    read/array/struct_.rs:101-114).  Every leaf column of a struct must hold
+    the same rows per page (the writer pages all leaves of a field alike,
+    write/common.rs:73-100); a leaf whose nest counts disagree is OutOfSpec."""
+
+    def __init__(self, fld: Field, columns, ctx: Optional[Context] = None):
+        if fld.kind == "leaf":
+            raise N.StrawboatError(N.E_ARG, "a primitive field is not nested: use ColumnDecoder")
+        self.field = fld
+        self.paths = fld.leaf_paths()
+        if len(columns) != len(self.paths):
+            raise N.StrawboatError(N.E_ARG, f"{len(self.paths)} leaves but {len(columns)} columns")
+        self.ctx = resolve_context(ctx, columns[0][0] if columns else None)
+        self.decoders = []
+        try:
+            for path, (chunk, metas) in zip(self.paths, columns):
+                nulls, mask, leaf_null, large = init_chain(path)
+                lf = path[-1]
+                dtype = lf.dtype if lf.dtype is not None else np.uint8
+                self.decoders.append(NestedColumnDecoder(chunk, metas, dtype, nulls, leaf_null, self.ctx, large=large,
+                                                         physical_type=lf.physical_type, struct_mask=mask))
+        except Exception:
+            self.close()
+            raise
+        for dec, path in zip(self.decoders, self.paths):  # a struct's leaves agree on the nests they share
+            first = self.decoders[0]
+            shared = 0
+            while shared < min(len(path), len(self.paths[0])) - 1 and path[shared] is self.paths[0][shared]:
+                shared += 1
+            if dec.counts[:shared] != first.counts[:shared]:
+                raise N.StrawboatError(N.E_OUT_OF_SPEC, "leaf columns of one field disagree on their rows")
+        self.num_rows = self.decoders[0].counts[0]
+
+    def decode(self) -> DeviceArray:
+        outs = [dec.decode() for dec in self.decoders]
+        return self._assemble(self.field, list(zip(self.decoders, outs)), 0)
+
+    def _assemble(self, f: Field, leaves, d: int) -> DeviceArray:
+        dec, (offs, valid, values, leafv) = leaves[-1]
+        n = dec.counts[d]
+        if f.kind == "leaf":
+            return DeviceArray("leaf", n, leafv, values=values)
+        if f.kind == "struct":
+            kids, k = [], 0
+            for c in f.children:
+                m = c.n_columns()
+                kids.append(self._assemble(c, leaves[k:k + m], d + 1))
+                k += m
+            return DeviceArray("struct", n, valid[d], children=kids)
+        return DeviceArray(f.kind, n, valid[d], offsets=offs[d], children=[self._assemble(f.children[0], leaves, d + 1)])
+
+    def close(self):
+        for dec in getattr(self, "decoders", []):
+            dec.close()
+        self.decoders = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def batch_read_field(fld: Field, columns, ctx: Optional[Context] = None) -> DeviceArray:
+    """batch_read_array for a nested field (List / Map / Struct trees):
+    columns = one (chunk, page metas) per leaf, to_leaves order."""
+    dec = FieldDecoder(fld, columns, ctx)
+    try:
+        return dec.decode()
+    finally:
+        dec.close()

@@ -143,3 +143,40 @@ def shapes():
         "map_of_list": map_(leaf("i32", False, "key"), lst(leaf("i64", True), True, "value"), True),
         "req_struct_req": struct([leaf("i32", False, "x"), leaf("u8", False, "y")], False),
     }
+
+
+def pa_amd_field(f: F):
+    """oracle.nest.F -> pa_amd.Field."""
+    import pa_amd
+    from pa_amd import _native as N
+
+    if f.kind == "leaf":
+        if f.leaf == "binary":
+            return pa_amd.Field.leaf(pa_amd.LARGE_BINARY if f.large else pa_amd.BINARY, f.nullable, f.name)
+        if f.leaf == "bool":
+            return pa_amd.Field.leaf(N.BOOLEAN, f.nullable, f.name)
+        return pa_amd.Field.leaf(f.dtype, f.nullable, f.name)
+    return pa_amd.Field(f.kind, f.nullable, [pa_amd_field(c) for c in f.children], name=f.name)
+
+
+def device_to_host(f: F, d) -> A:
+    """pa_amd.DeviceArray -> oracle.nest.A (bitmaps unpacked)."""
+    n = d.length
+
+    def bits(t, k):
+        return np.unpackbits(t.cpu().numpy().view(np.uint8), bitorder="little")[:k].astype(bool)
+
+    validity = None if d.validity is None else bits(d.validity, n)
+    if f.kind == "leaf":
+        if f.leaf == "fixed":
+            v = d.values.cpu().numpy().view(np.uint8)[: n * f.dtype.itemsize].view(f.dtype)
+        elif f.leaf == "bool":
+            v = bits(d.values, n)
+        else:
+            o = d.values[0].cpu().numpy().astype(np.int64)[: n + 1]
+            v = (o, d.values[1].cpu().numpy().tobytes()[: int(o[-1]) if n else 0])
+        return A("leaf", n, validity, values=v)
+    if f.kind == "struct":
+        return A("struct", n, validity, children=[device_to_host(c, x) for c, x in zip(f.children, d.children)])
+    offs = d.offsets.cpu().numpy().astype(np.int64)[: n + 1]
+    return A(f.kind, n, validity, offsets=offs, children=[device_to_host(f.children[0], d.children[0])])

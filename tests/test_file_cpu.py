@@ -20,18 +20,32 @@ PHYS = {pa.int8(): N.INT8, pa.int16(): N.INT16, pa.int32(): N.INT32, pa.int64():
 
 
 def expected_leaves(schema):
-    """arrow2 to_leaves order, from pyarrow's type tree."""
+    """arrow2 to_leaves order, from pyarrow's type tree, with the InitNested
+    chain of each leaf (read/deserialize.rs:202-230): List / LargeList / Map
+    nests and Struct nests, numbered in pre-order."""
     out = []
+    nid = [0]
 
-    def walk(f, top, lists, flags):
+    def walk(f, top, nests, flags):
         t = f.type
-        if pa.types.is_list(t) or pa.types.is_large_list(t):
-            walk(t.value_field, top, lists + [(f.nullable, pa.types.is_large_list(t))], flags)
+        if pa.types.is_map(t):
+            me = (f.nullable, False, "map", nid[0])
+            nid[0] += 1
+            walk(pa.field("entries", pa.struct([t.key_field, t.item_field]), False), top, nests + [me], flags | 2)
+        elif pa.types.is_list(t) or pa.types.is_large_list(t):
+            me = (f.nullable, pa.types.is_large_list(t), "list", nid[0])
+            nid[0] += 1
+            walk(t.value_field, top, nests + [me], flags)
         elif pa.types.is_struct(t):
+            me = (f.nullable, False, "struct", nid[0])
+            nid[0] += 1
             for i in range(t.num_fields):
-                walk(t.field(i), top, lists, flags | 1)
+                walk(t.field(i), top, nests + [me], flags | 1)
         else:
-            out.append((f.name, PHYS[t], f.nullable, len(lists), [x[0] for x in lists], [x[1] for x in lists], flags, top))
+            sm = sum(1 << d for d, x in enumerate(nests) if x[2] == "struct")
+            mm = sum(1 << d for d, x in enumerate(nests) if x[2] == "map")
+            out.append((f.name, PHYS[t], f.nullable, len(nests), [x[0] for x in nests], [x[1] for x in nests], flags, top,
+                        sm, mm, [x[3] for x in nests]))
 
     for i, f in enumerate(schema):
         walk(f, i, [], 0)
@@ -51,6 +65,11 @@ SCHEMAS = [
                pa.field("L", pa.large_list(pa.bool_()), False)]),
     pa.schema([pa.field("st", pa.struct([pa.field("x", pa.int16()), pa.field("y", pa.list_(pa.float64()))])),
                pa.field("z", pa.uint8())]),
+    pa.schema([pa.field("m", pa.map_(pa.int32(), pa.large_binary()), True),
+               pa.field("lm", pa.list_(pa.field("item", pa.map_(pa.utf8(), pa.struct([pa.field("p", pa.bool_()),
+                                                                                       pa.field("q", pa.int8())])),
+                                                 True)), False),
+               pa.field("ss", pa.struct([pa.field("a", pa.struct([pa.field("b", pa.int64(), False)]), True)]), False)]),
     pa.schema([pa.field("col_%d" % i, pa.int64()) for i in range(300)]),
 ]
 
@@ -62,8 +81,8 @@ def test_parse_schema_matches_pyarrow(k, framing):
     b = s.serialize().to_pybytes()
     if framing == "message":  # arrow2 schema_to_bytes: the Message flatbuffer alone
         b = b[8:]
-    got = [(l.name, l.physical_type, l.nullable, l.depth, l.list_nullable, l.large_list, l.flags, l.top_field)
-           for l in pa_amd.parse_schema(b)]
+    got = [(l.name, l.physical_type, l.nullable, l.depth, l.list_nullable, l.large_list, l.flags, l.top_field,
+            l.struct_mask, l.map_mask, l.nest_id) for l in pa_amd.parse_schema(b)]
     assert got == expected_leaves(s)
 
 
@@ -164,3 +183,40 @@ def test_parse_schema_aliased_children_bounded():
     assert patched == 40
     with pytest.raises(N.StrawboatError):
         pa_amd.parse_schema(bytes(b))
+
+
+def _tree(f):
+    """(kind, nullable, children | physical type) of a pa_amd.Field."""
+    if f.kind == "leaf":
+        return ("leaf", f.nullable, f.physical_type)
+    return (f.kind, f.nullable, [_tree(c) for c in f.children])
+
+
+def test_file_fields_rebuild_struct_map_trees(tmp_path):
+    """StrawboatFile.field(top): the leaves' nest chains (struct / map masks,
+    pre-order nest ids) regroup into each top-level field's tree -- the
+    Field deserialize_nested walks (read/deserialize.rs:140-233)."""
+    from tests import nestgen
+
+    shapes = nestgen.shapes()
+    names = list(shapes)
+    fields = []
+    for k in names:
+        f = shapes[k]
+        f.name = k
+        fields.append(f)
+    schema = pa.schema([nestgen.pa_field(f) for f in fields] + [pa.field("flat", pa.int32(), False)])
+    n_leaves = sum(len(__import__("oracle.nest", fromlist=["x"]).leaf_paths(f)) for f in fields) + 1
+    cols = [(b"", [])] * n_leaves
+    p, _ = _file(tmp_path, cols, schema)
+    with pa_amd.StrawboatFile(p) as sf:
+        assert len(sf.leaves) == n_leaves
+        c0 = 0
+        for top, f in enumerate(fields):
+            got, cols_of = sf.field(top)
+            assert _tree(got) == _tree(nestgen.pa_amd_field(f)), names[top]
+            k = len(cols_of)
+            assert cols_of == list(range(c0, c0 + k))
+            c0 += k
+        got, cols_of = sf.field(len(fields))
+        assert _tree(got) == ("leaf", False, N.INT32) and cols_of == [n_leaves - 1]
