@@ -183,8 +183,8 @@ impl<R: NativeReadBuf + Seek> Iterator for NativeReader<R> {
     }
 }
 
-/// The arrow2 `DataType`s the page path carries (Struct / Map / Union are
-/// out of scope).
+/// The arrow2 `DataType`s the page path carries (Union, FixedSizeList and
+/// Dictionary are out of scope).
 #[derive(Debug, Clone, PartialEq)]
 pub enum DataType {
     Boolean,
@@ -204,6 +204,11 @@ pub enum DataType {
     LargeUtf8,
     List(Box<Field>),
     LargeList(Box<Field>),
+    /// arrow2 `DataType::Struct(Vec<Field>)`
+    Struct(Vec<Field>),
+    /// arrow2 `DataType::Map(entries, keys_sorted)`: `entries` is a
+    /// non-nullable Struct field of the key and value fields
+    Map(Box<Field>, bool),
 }
 
 /// arrow2 `Field`.
@@ -220,6 +225,21 @@ impl Field {
     }
 }
 
+/// arrow2 `n_columns` (io/parquet/read): the leaf columns a field is
+/// written as (to_leaves, write/common.rs:66-71).
+pub fn n_columns(data_type: &DataType) -> usize {
+    match data_type {
+        DataType::List(c) | DataType::LargeList(c) | DataType::Map(c, _) => n_columns(&c.data_type),
+        DataType::Struct(fields) => fields.iter().map(|f| n_columns(&f.data_type)).sum(),
+        _ => 1,
+    }
+}
+
+/// arrow2 `is_primitive`: a field read without levels (is_nested false).
+fn is_primitive(data_type: &DataType) -> bool {
+    !matches!(data_type, DataType::List(_) | DataType::LargeList(_) | DataType::Struct(_) | DataType::Map(_, _))
+}
+
 /// parquet2 `ColumnDescriptor`, reduced to what a leaf reader needs.
 #[derive(Debug, Clone, Copy, PartialEq)]
 pub struct ColumnDescriptor {
@@ -228,12 +248,14 @@ pub struct ColumnDescriptor {
     pub max_rep_level: i16,
 }
 
-/// The Arrow buffers (in HBM) of one decoded column chunk.
+/// The Arrow buffers (in HBM) of one decoded column chunk (or, for a field
+/// with Struct / Map nests, of its leaf chunks).
 pub enum ColumnData {
     Primitive(Primitive),
     Binary(Binary),
     List(List),
     Nested(Nested),
+    Field(FieldNode),
 }
 
 impl ColumnData {
@@ -244,6 +266,60 @@ impl ColumnData {
             ColumnData::Binary(b) => b.len,
             ColumnData::List(l) => l.rows,
             ColumnData::Nested(n) => n.counts[0],
+            ColumnData::Field(f) => f.len,
+        }
+    }
+}
+
+/// A decoded field with Struct / Map nests: a tree of views into the
+/// per-leaf decodes.  A node's offsets and validity are those its LAST leaf
+/// decoded (create_list / create_map / create_struct pop the last child's
+/// NestedState, read/array/struct_.rs:101-114, batch_read.rs:128-180); a
+/// leaf node's values are its leaf column's.
+pub struct FieldNode {
+    pub data_type: DataType,
+    /// entries of this node (rows at the top)
+    pub len: u64,
+    source: Arc<Nested>,
+    depth: usize,
+    pub children: Vec<FieldNode>,
+}
+
+impl FieldNode {
+    fn is_leaf(&self) -> bool {
+        self.depth == self.source.offsets.len()
+    }
+    /// The node's validity bitmap (32-bit words, LSB first), None when the
+    /// field is not nullable.
+    pub fn validity(&self) -> Option<&DeviceBuffer> {
+        if self.is_leaf() {
+            self.source.leaf_validity.as_ref()
+        } else {
+            self.source.validity[self.depth].as_ref()
+        }
+    }
+    /// A List / Map node's offsets (len + 1 entries).
+    pub fn offsets(&self) -> Option<&DeviceBuffer> {
+        if self.is_leaf() {
+            None
+        } else {
+            self.source.offsets[self.depth].as_ref()
+        }
+    }
+    /// A leaf node's values: fixed-width values, a Boolean bitmap, or the
+    /// value bytes of a Binary / Utf8 leaf (with [`FieldNode::leaf_offsets`]).
+    pub fn values(&self) -> Option<&DeviceBuffer> {
+        if self.is_leaf() {
+            Some(&self.source.values)
+        } else {
+            None
+        }
+    }
+    pub fn leaf_offsets(&self) -> Option<&DeviceBuffer> {
+        if self.is_leaf() {
+            self.source.leaf_offsets.as_ref()
+        } else {
+            None
         }
     }
 }
@@ -288,39 +364,85 @@ impl Array {
 /// per page.
 pub type ArrayIter<'a> = Box<dyn Iterator<Item = Result<Array>> + Send + Sync + 'a>;
 
-/// The leaf under a field: its physical type, per list level (outermost
-/// first) the level's nullability and whether it is a LargeList, and the
-/// leaf's own nullability (arrow2 to_leaves + InitNested).
-fn leaf_path(field: &Field) -> Result<(PhysicalType, Vec<bool>, Vec<bool>, bool)> {
+/// One nest of a leaf's InitNested chain (read/deserialize.rs:202-230): a
+/// List / LargeList / Map pushes InitNested::List, a Struct
+/// InitNested::Struct, each with the nest field's nullability.
+#[derive(Debug, Clone, Copy, PartialEq)]
+struct Nest {
+    is_struct: bool,
+    nullable: bool,
+    large: bool,
+}
+
+/// One leaf column of a field: its physical type, its nest chain (outermost
+/// first) and its own nullability.
+#[derive(Debug, Clone, PartialEq)]
+struct LeafChain {
+    ty: PhysicalType,
+    nests: Vec<Nest>,
+    nullable: bool,
+}
+
+fn leaf_type(dt: &DataType) -> PhysicalType {
     use PhysicalType as P;
-    let (mut lists, mut large) = (Vec::new(), Vec::new());
-    let mut f = field;
-    loop {
-        let ty = match &f.data_type {
-            DataType::List(c) | DataType::LargeList(c) => {
-                lists.push(f.is_nullable);
-                large.push(matches!(f.data_type, DataType::LargeList(_)));
-                f = c;
-                continue;
-            }
-            DataType::Boolean => P::Boolean,
-            DataType::Int8 => P::Int8,
-            DataType::Int16 => P::Int16,
-            DataType::Int32 => P::Int32,
-            DataType::Int64 => P::Int64,
-            DataType::UInt8 => P::UInt8,
-            DataType::UInt16 => P::UInt16,
-            DataType::UInt32 => P::UInt32,
-            DataType::UInt64 => P::UInt64,
-            DataType::Float32 => P::Float32,
-            DataType::Float64 => P::Float64,
-            DataType::Binary => P::Binary,
-            DataType::LargeBinary => P::LargeBinary,
-            DataType::Utf8 => P::Utf8,
-            DataType::LargeUtf8 => P::LargeUtf8,
-        };
-        return Ok((ty, lists, large, f.is_nullable));
+    match dt {
+        DataType::Boolean => P::Boolean,
+        DataType::Int8 => P::Int8,
+        DataType::Int16 => P::Int16,
+        DataType::Int32 => P::Int32,
+        DataType::Int64 => P::Int64,
+        DataType::UInt8 => P::UInt8,
+        DataType::UInt16 => P::UInt16,
+        DataType::UInt32 => P::UInt32,
+        DataType::UInt64 => P::UInt64,
+        DataType::Float32 => P::Float32,
+        DataType::Float64 => P::Float64,
+        DataType::Binary => P::Binary,
+        DataType::LargeBinary => P::LargeBinary,
+        DataType::Utf8 => P::Utf8,
+        DataType::LargeUtf8 => P::LargeUtf8,
+        DataType::List(_) | DataType::LargeList(_) | DataType::Struct(_) | DataType::Map(_, _) => {
+            unreachable!("a nest is not a leaf")
+        }
     }
+}
+
+/// deserialize_nested's walk (read/deserialize.rs:140-233): the leaves of
+/// `field` in to_leaves order, each with its InitNested chain.
+fn leaf_chains(field: &Field) -> Vec<LeafChain> {
+    fn walk(f: &Field, nests: &mut Vec<Nest>, out: &mut Vec<LeafChain>) {
+        match &f.data_type {
+            DataType::List(c) | DataType::LargeList(c) | DataType::Map(c, _) => {
+                let large = matches!(f.data_type, DataType::LargeList(_));
+                nests.push(Nest { is_struct: false, nullable: f.is_nullable, large });
+                walk(c, nests, out);
+                nests.pop();
+            }
+            DataType::Struct(fields) => {
+                nests.push(Nest { is_struct: true, nullable: f.is_nullable, large: false });
+                for c in fields {
+                    walk(c, nests, out);
+                }
+                nests.pop();
+            }
+            dt => out.push(LeafChain { ty: leaf_type(dt), nests: nests.clone(), nullable: f.is_nullable }),
+        }
+    }
+    let mut out = Vec::new();
+    walk(field, &mut Vec::new(), &mut out);
+    out
+}
+
+/// The one leaf under a field without Struct / Map nests: its physical type,
+/// per list level (outermost first) the level's nullability and whether it
+/// is a LargeList, and the leaf's own nullability.
+fn leaf_path(field: &Field) -> Result<(PhysicalType, Vec<bool>, Vec<bool>, bool)> {
+    let mut chains = leaf_chains(field);
+    if chains.len() != 1 || chains[0].nests.iter().any(|n| n.is_struct) {
+        return Err(Error::NotYetImplemented(format!("{}: a field with Struct / Map nests has no one-leaf path", field.name)));
+    }
+    let c = chains.pop().unwrap();
+    Ok((c.ty, c.nests.iter().map(|n| n.nullable).collect(), c.nests.iter().map(|n| n.large).collect(), c.nullable))
 }
 
 /// The read/deserialize.rs dispatch over one column chunk in HBM: flat
@@ -343,54 +465,121 @@ fn decode_chunk(ctx: &Context, chunk: &DeviceBuffer, pages: &[PageMeta], field: 
         let c = ListColumn::plan(ctx, chunk, pages, ty, lists[0], leaf_nullable, large[0])?;
         return Ok(ColumnData::List(c.decode()?));
     }
-    let c = NestedColumn::plan(ctx, chunk, pages, ty, &lists, leaf_nullable, large[0])?;
+    let c = NestedColumn::plan(ctx, chunk, pages, ty, &lists, leaf_nullable, large[0], 0)?;
     Ok(ColumnData::Nested(c.decode()?))
 }
 
-/// Column chunk bytes into HBM on the thread's default context, decoded.
-fn decode_host_chunk(bytes: &[u8], pages: &[PageMeta], field: &Field) -> Result<ColumnData> {
-    let ctx = default_context()?;
-    let chunk = ctx.upload(bytes)?;
-    decode_chunk(&ctx, &chunk, pages, field)
+/// A field's leaf chunks in HBM (to_leaves order) decoded: one chunk without
+/// Struct / Map nests through [`decode_chunk`]; otherwise each leaf through
+/// its InitNested chain (sb_plan_nested_column with a struct mask), then the
+/// tree assembled as deserialize_nested does.
+fn decode_field(ctx: &Context, chunks: &[DeviceBuffer], pages: &[Vec<PageMeta>], field: &Field) -> Result<ColumnData> {
+    let chains = leaf_chains(field);
+    if chains.len() != chunks.len() || chunks.len() != pages.len() {
+        return Err(Error::Argument(format!("{}: {} leaf columns, {} chunks, {} page lists", field.name, chains.len(),
+                                           chunks.len(), pages.len())));
+    }
+    if chains.len() == 1 && chains[0].nests.iter().all(|n| !n.is_struct) {
+        return decode_chunk(ctx, &chunks[0], &pages[0], field);
+    }
+    let mut decoded = Vec::with_capacity(chains.len());
+    for ((c, chunk), p) in chains.iter().zip(chunks).zip(pages) {
+        let lists: Vec<bool> = c.nests.iter().filter(|n| !n.is_struct).map(|n| n.large).collect();
+        let large = lists.first().copied().unwrap_or(false);
+        if lists.iter().any(|&l| l != large) {
+            return Err(Error::NotYetImplemented(format!("{}: mixed List / LargeList levels", field.name)));
+        }
+        let nullable: Vec<bool> = c.nests.iter().map(|n| n.nullable).collect();
+        let mask = c.nests.iter().enumerate().filter(|(_, n)| n.is_struct).fold(0u32, |m, (d, _)| m | (1u32 << d));
+        let col = NestedColumn::plan(ctx, chunk, p, c.ty, &nullable, c.nullable, large, mask)?;
+        decoded.push(Arc::new(col.decode()?));
+    }
+    Ok(ColumnData::Field(assemble(field, &decoded, 0)?))
 }
 
-fn one_leaf(leaves: &[ColumnDescriptor], field: &Field) -> Result<()> {
-    if leaves.len() != 1 {
-        return Err(Error::NotYetImplemented(format!("{}: {} leaves (Struct / Map nests)", field.name, leaves.len())));
+/// create_struct / create_map / create_list over the leaf decodes under
+/// `f` (its nest is at `depth` of their chains): the last leaf's nest, after
+/// checking that every leaf under it counted the same entries (StructArray's
+/// children must be as long as it is).
+fn assemble(f: &Field, leaves: &[Arc<Nested>], depth: usize) -> Result<FieldNode> {
+    let last = leaves.last().ok_or_else(|| Error::OutOfSpec(format!("{}: a Struct without fields", f.name)))?;
+    let len = last.counts[depth];
+    if leaves.iter().any(|l| l.counts[depth] != len) {
+        return Err(Error::OutOfSpec(format!("{}: its leaf columns disagree on the entries of a nest", f.name)));
     }
-    let (ty, _, _, _) = leaf_path(field)?;
-    if leaves[0].physical_type != ty {
-        return Err(Error::OutOfSpec(format!("{}: leaf type {:?} against field {:?}", field.name, leaves[0].physical_type, ty)));
+    let children = match &f.data_type {
+        DataType::List(c) | DataType::LargeList(c) | DataType::Map(c, _) => vec![assemble(c, leaves, depth + 1)?],
+        DataType::Struct(fields) => {
+            let mut v = Vec::with_capacity(fields.len());
+            let mut k = 0;
+            for c in fields {
+                let n = n_columns(&c.data_type);
+                if k + n > leaves.len() {
+                    return Err(Error::OutOfSpec(format!("{}: fewer leaf columns than fields", f.name)));
+                }
+                v.push(assemble(c, &leaves[k..k + n], depth + 1)?);
+                k += n;
+            }
+            v
+        }
+        _ => Vec::new(),
+    };
+    Ok(FieldNode { data_type: f.data_type.clone(), len, source: last.clone(), depth, children })
+}
+
+/// A field's leaf chunk bytes into HBM on the thread's default context, decoded.
+fn decode_host_chunks(chunks: &[Vec<u8>], pages: &[Vec<PageMeta>], field: &Field) -> Result<ColumnData> {
+    let ctx = default_context()?;
+    let bufs = chunks.iter().map(|b| ctx.upload(b)).collect::<Result<Vec<_>>>()?;
+    decode_field(&ctx, &bufs, pages, field)
+}
+
+/// The leaves the caller passes must be the field's (to_leaves order).
+fn check_leaves(leaves: &[ColumnDescriptor], field: &Field) -> Result<()> {
+    let chains = leaf_chains(field);
+    if leaves.len() != chains.len() {
+        return Err(Error::OutOfSpec(format!("{}: {} leaves for {} leaf columns", field.name, leaves.len(), chains.len())));
+    }
+    for (l, c) in leaves.iter().zip(&chains) {
+        if l.physical_type != c.ty {
+            return Err(Error::OutOfSpec(format!("{}: leaf type {:?} against field {:?}", field.name, l.physical_type, c.ty)));
+        }
     }
     Ok(())
 }
 
 fn check_nested(is_nested: bool, field: &Field) -> Result<()> {
-    if is_nested != matches!(field.data_type, DataType::List(_) | DataType::LargeList(_)) {
+    if is_nested == is_primitive(&field.data_type) {
         return Err(Error::Argument(format!("{}: is_nested {is_nested} against its data type", field.name)));
     }
     Ok(())
 }
 
 /// `batch_read_array` (src/read/batch_read.rs:190-209): every page of the
-/// column at once, one array.  The chunk's pages are read from the reader
-/// in one read, staged into HBM with one copy and decoded there.
+/// field's leaf columns at once, one array.  Each leaf's pages are read from
+/// its reader in one read, staged into HBM with one copy and decoded there.
 pub fn batch_read_array<R: NativeReadBuf>(
     mut readers: Vec<R>,
     leaves: Vec<ColumnDescriptor>,
     field: Field,
     is_nested: bool,
-    mut page_metas: Vec<Vec<PageMeta>>,
+    page_metas: Vec<Vec<PageMeta>>,
 ) -> Result<Array> {
-    one_leaf(&leaves, &field)?;
+    check_leaves(&leaves, &field)?;
     check_nested(is_nested, &field)?;
-    let mut reader = readers.pop().ok_or_else(|| Error::Argument("no reader".into()))?;
-    let metas = page_metas.pop().ok_or_else(|| Error::Argument("no page metas".into()))?;
-    let len = ColumnMeta { offset: 0, pages: metas.clone() }.total_len()?;
-    let len = usize::try_from(len).map_err(|_| Error::OutOfSpec("column chunk larger than the address space".into()))?;
-    let mut bytes = vec![0u8; len];
-    reader.read_exact(&mut bytes).map_err(io)?;
-    let data = decode_host_chunk(&bytes, &metas, &field)?;
+    if readers.len() != leaves.len() || page_metas.len() != leaves.len() {
+        return Err(Error::Argument(format!("{}: {} readers and {} page lists for {} leaves", field.name, readers.len(),
+                                           page_metas.len(), leaves.len())));
+    }
+    let mut chunks = Vec::with_capacity(readers.len());
+    for (reader, metas) in readers.iter_mut().zip(&page_metas) {
+        let len = ColumnMeta { offset: 0, pages: metas.clone() }.total_len()?;
+        let len = usize::try_from(len).map_err(|_| Error::OutOfSpec("column chunk larger than the address space".into()))?;
+        let mut bytes = vec![0u8; len];
+        reader.read_exact(&mut bytes).map_err(io)?;
+        chunks.push(bytes);
+    }
+    let data = decode_host_chunks(&chunks, &page_metas, &field)?;
     let len = data.rows();
     Ok(Array { data_type: field.data_type, data: Arc::new(data), offset: 0, len })
 }
@@ -405,13 +594,15 @@ fn nested_page_rows(page: &[u8]) -> Result<u64> {
 }
 
 /// The iterator `column_iter_to_arrays` returns.  On the first call it
-/// drains the page reader (handing every page buffer back through
-/// `swap_buffer`), stages the chunk into HBM with one copy and plans and
-/// decodes it once; each page then becomes the row range of the decoded
-/// column it covers.  A read or decode error is returned by that first
-/// call.
+/// drains the page readers (handing every page buffer back through
+/// `swap_buffer`), stages each leaf chunk into HBM with one copy and plans
+/// and decodes the field once; each page then becomes the row range of the
+/// decoded field it covers.  A read or decode error of any page is returned
+/// by that first call -- a deviation from the reference's page-at-a-time
+/// iterator, which returns the arrays of the pages before a bad page first
+/// and holds one page in memory at a time ("Streaming").
 struct PageArrays<I> {
-    reader: Option<I>,
+    readers: Option<Vec<I>>,
     field: Field,
     is_nested: bool,
     pages: VecDeque<(u64, u64)>,
@@ -422,19 +613,30 @@ impl<I> PageArrays<I>
 where
     I: Iterator<Item = Result<(u64, Vec<u8>)>> + PageIterator,
 {
-    fn load(&mut self, reader: &mut I) -> Result<()> {
-        let (mut bytes, mut metas, mut rows) = (Vec::new(), Vec::new(), Vec::new());
-        while let Some(page) = reader.next() {
-            let (num_values, mut buf) = page?;
-            rows.push(if self.is_nested { nested_page_rows(&buf)? } else { num_values });
-            metas.push(PageMeta { length: buf.len() as u64, num_values });
-            bytes.extend_from_slice(&buf);
-            reader.swap_buffer(&mut buf);  // the page buffer back to the reader for reuse
+    fn load(&mut self, readers: Vec<I>) -> Result<()> {
+        let (mut chunks, mut all_metas, mut rows) = (Vec::new(), Vec::new(), Vec::new());
+        for (k, mut reader) in readers.into_iter().enumerate() {
+            let (mut bytes, mut metas, mut r) = (Vec::new(), Vec::new(), Vec::new());
+            while let Some(page) = reader.next() {
+                let (num_values, mut buf) = page?;
+                r.push(if self.is_nested { nested_page_rows(&buf)? } else { num_values });
+                metas.push(PageMeta { length: buf.len() as u64, num_values });
+                bytes.extend_from_slice(&buf);
+                reader.swap_buffer(&mut buf);  // the page buffer back to the reader for reuse
+            }
+            if k == 0 {
+                rows = r;
+            } else if r != rows {
+                // StructIterator zips page k of every child (struct_.rs:63-85)
+                return Err(Error::OutOfSpec(format!("{}: its leaf columns page different rows", self.field.name)));
+            }
+            chunks.push(bytes);
+            all_metas.push(metas);
         }
-        if metas.is_empty() {
+        if rows.is_empty() {
             return Ok(());
         }
-        let data = decode_host_chunk(&bytes, &metas, &self.field)?;
+        let data = decode_host_chunks(&chunks, &all_metas, &self.field)?;
         let mut first = 0u64;
         for r in rows {
             self.pages.push_back((first, r));
@@ -455,8 +657,8 @@ where
     type Item = Result<Array>;
 
     fn next(&mut self) -> Option<Self::Item> {
-        if let Some(mut reader) = self.reader.take() {
-            if let Err(e) = self.load(&mut reader) {
+        if let Some(readers) = self.readers.take() {
+            if let Err(e) = self.load(readers) {
                 self.pages.clear();
                 return Some(Err(e));
             }
@@ -468,9 +670,9 @@ where
 }
 
 /// `column_iter_to_arrays` (src/read/deserialize.rs:237-253): one array per
-/// page of the column.
+/// page of the field (one reader per leaf column, to_leaves order).
 pub fn column_iter_to_arrays<'a, I: 'a>(
-    mut readers: Vec<I>,
+    readers: Vec<I>,
     leaves: Vec<ColumnDescriptor>,
     field: Field,
     is_nested: bool,
@@ -478,10 +680,12 @@ pub fn column_iter_to_arrays<'a, I: 'a>(
 where
     I: Iterator<Item = Result<(u64, Vec<u8>)>> + PageIterator + Send + Sync,
 {
-    one_leaf(&leaves, &field)?;
+    check_leaves(&leaves, &field)?;
     check_nested(is_nested, &field)?;
-    let reader = readers.pop().ok_or_else(|| Error::Argument("no reader".into()))?;
-    Ok(Box::new(PageArrays { reader: Some(reader), field, is_nested, pages: VecDeque::new(), data: None }))
+    if readers.len() != leaves.len() {
+        return Err(Error::Argument(format!("{}: {} readers for {} leaves", field.name, readers.len(), leaves.len())));
+    }
+    Ok(Box::new(PageArrays { readers: Some(readers), field, is_nested, pages: VecDeque::new(), data: None }))
 }
 
 /// `compression::Compression` (src/compression/mod.rs:37-108).
@@ -549,28 +753,38 @@ pub struct WriteOptions {
     pub forbidden_compressions: Vec<Compression>,
 }
 
-/// util/env.rs's debug-build codec overrides, in choose_compressor's order
-/// (compression/integer/mod.rs:236-266, double/mod.rs:236-268): the first
+const FREQ_ENV: (&str, Compression) = ("STRAWBOAT_FREQ_COMPRESSION", Compression::Freq);
+const DICT_ENV: (&str, Compression) = ("STRAWBOAT_DICT_COMPRESSION", Compression::Dict);
+const RLE_ENV: (&str, Compression) = ("STRAWBOAT_RLE_COMPRESSION", Compression::Rle);
+const BITPACK_ENV: (&str, Compression) = ("STRAWBOAT_BITPACK_COMPRESSION", Compression::Bitpacking);
+const PATAS_ENV: (&str, Compression) = ("STRAWBOAT_PATAS_COMPRESSION", Compression::Patas);
+
+/// util/env.rs's debug-build codec overrides, as each type's
+/// choose_compressor checks them, in its order: integers Freq / Dict / Rle /
+/// Bitpacking (compression/integer/mod.rs:236-266), doubles Freq / Dict /
+/// Rle / Patas (double/mod.rs:236-268), binary Freq / Dict
+/// (binary/mod.rs:298-314), Boolean Rle (boolean/mod.rs:199-207).  The first
 /// one set to "1" whose codec is not forbidden becomes the engine's forced
 /// codec (one per column; the reference re-checks them in each nested call).
-fn forced_from_env(forbidden: &[Compression]) -> Option<i32> {
+fn forced_from_env(forbidden: &[Compression], ty: PhysicalType) -> Option<i32> {
     if !cfg!(debug_assertions) {
         return None;
     }
-    const ENV: [(&str, Compression); 5] = [
-        ("STRAWBOAT_FREQ_COMPRESSION", Compression::Freq),
-        ("STRAWBOAT_DICT_COMPRESSION", Compression::Dict),
-        ("STRAWBOAT_RLE_COMPRESSION", Compression::Rle),
-        ("STRAWBOAT_BITPACK_COMPRESSION", Compression::Bitpacking),
-        ("STRAWBOAT_PATAS_COMPRESSION", Compression::Patas),
-    ];
-    ENV.iter()
+    let order: &[(&str, Compression)] = match ty {
+        PhysicalType::Boolean => &[RLE_ENV],
+        t if t.is_binary() => &[FREQ_ENV, DICT_ENV],
+        PhysicalType::Float32 | PhysicalType::Float64 => &[FREQ_ENV, DICT_ENV, RLE_ENV, PATAS_ENV],
+        _ => &[FREQ_ENV, DICT_ENV, RLE_ENV, BITPACK_ENV],
+    };
+    order
+        .iter()
         .find(|(var, c)| std::env::var(var).map_or(false, |v| v == "1") && !forbidden.contains(c))
         .map(|(_, c)| u8::from(*c) as i32)
 }
 
 impl WriteOptions {
-    fn engine(&self) -> crate::WriteOptions {
+    /// The engine's options for a column of physical type `ty`.
+    fn engine(&self, ty: PhysicalType) -> crate::WriteOptions {
         let mut forbidden_mask = 0u32;
         for c in &self.forbidden_compressions {
             forbidden_mask |= 1u32 << u8::from(*c);
@@ -580,7 +794,7 @@ impl WriteOptions {
             default_compress_ratio: self.default_compress_ratio,
             max_page_size: self.max_page_size.map(|p| p as u64),
             forbidden_mask,
-            forced_codec: forced_from_env(&self.forbidden_compressions),
+            forced_codec: forced_from_env(&self.forbidden_compressions, ty),
             seed: 0,
         }
     }
@@ -784,7 +998,7 @@ fn check_offsets(offsets: &[i64], n: u64, limit: u64) -> Result<()> {
 /// what the lengths and offsets promise.
 fn encode_array(a: &HostArray, f: &Field, o: &WriteOptions) -> Result<(Vec<u8>, Vec<PageMeta>)> {
     let (ty, lists, _, leaf_nullable) = leaf_path(f)?;
-    let eo = o.engine();
+    let eo = o.engine(ty);
     let opts = eo.raw();
     let page = eo.max_page_size.unwrap_or(0);
     let mut out: *mut u8 = ptr::null_mut();
@@ -874,6 +1088,40 @@ mod tests {
     }
 
     #[test]
+    fn struct_and_map_chains() {
+        // tests/it/io.rs:294-325 create_map: Map(nullable) of entries {key Int32, value LargeBinary}
+        let entries = Field::new("entries", DataType::Struct(vec![Field::new("key", DataType::Int32, false),
+                                                                     Field::new("value", DataType::LargeBinary, true)]), false);
+        let m = Field::new("m", DataType::Map(Box::new(entries), false), true);
+        assert_eq!(n_columns(&m.data_type), 2);
+        let c = leaf_chains(&m);
+        assert_eq!(c.len(), 2);
+        assert_eq!(c[0].ty, PhysicalType::Int32);
+        assert_eq!(c[1].ty, PhysicalType::LargeBinary);
+        assert_eq!(c[0].nests, vec![Nest { is_struct: false, nullable: true, large: false },
+                                    Nest { is_struct: true, nullable: false, large: false }]);
+        assert!(!c[0].nullable && c[1].nullable);
+        assert!(leaf_path(&m).is_err());
+        assert!(check_nested(false, &m).is_err() && check_nested(true, &m).is_ok());
+        let leaves = vec![ColumnDescriptor { physical_type: PhysicalType::Int32, max_def_level: 2, max_rep_level: 1 }];
+        assert!(check_leaves(&leaves, &m).is_err());
+    }
+
+    #[test]
+    fn env_overrides_follow_the_column_type() {
+        std::env::set_var("STRAWBOAT_PATAS_COMPRESSION", "1");
+        assert_eq!(forced_from_env(&[], PhysicalType::Int32), None);
+        if cfg!(debug_assertions) {
+            assert_eq!(forced_from_env(&[], PhysicalType::Float64), Some(16));
+        }
+        std::env::remove_var("STRAWBOAT_PATAS_COMPRESSION");
+        std::env::set_var("STRAWBOAT_BITPACK_COMPRESSION", "1");
+        assert_eq!(forced_from_env(&[], PhysicalType::Utf8), None);
+        assert_eq!(forced_from_env(&[], PhysicalType::Boolean), None);
+        std::env::remove_var("STRAWBOAT_BITPACK_COMPRESSION");
+    }
+
+    #[test]
     fn writer_state_machine() {
         let schema = Schema { fields: vec![], ipc_bytes: vec![] };
         let mut w = NativeWriter::new(Vec::new(), schema, WriteOptions::default());
@@ -906,7 +1154,7 @@ mod tests {
             max_page_size: Some(8192),
             forbidden_compressions: vec![Compression::Dict, Compression::Freq],
         };
-        let e = o.engine();
+        let e = o.engine(PhysicalType::Int32);
         assert_eq!(e.default_codec, 1);
         assert_eq!(e.forbidden_mask, (1 << 11) | (1 << 13));
         assert_eq!(e.max_page_size, Some(8192));

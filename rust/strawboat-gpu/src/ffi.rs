@@ -14,6 +14,7 @@ pub const SB_MAX_NEST: usize = 4;
 pub struct sb_leaf_info {
     pub name: [c_char; 64], pub arrow_type: i32, pub physical_type: i32, pub nullable: i32, pub depth: i32,
     pub list_nullable: [i32; SB_MAX_NEST], pub large_list: [i32; SB_MAX_NEST], pub flags: u32, pub top_field: i32,
+    pub struct_mask: u32, pub map_mask: u32, pub nest_id: [i32; SB_MAX_NEST],
 }
 
 #[repr(C)] #[derive(Debug, Clone, Copy, PartialEq, Eq)]
@@ -39,7 +40,7 @@ pub struct sb_list_out { pub d_offsets: *mut c_void, pub d_list_validity: *mut u
 
 #[repr(C)] #[derive(Clone, Copy)]
 pub struct sb_nested_desc { pub physical_type: i32, pub depth: i32, pub list_nullable: [i32; 4],
-                            pub item_nullable: i32, pub offset_width: i32 }
+                            pub item_nullable: i32, pub offset_width: i32, pub struct_mask: i32 }
 
 #[repr(C)]
 pub struct sb_nested_out { pub d_offsets: [*mut c_void; 4], pub d_validity: [*mut u8; 4],

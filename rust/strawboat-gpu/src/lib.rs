@@ -424,7 +424,9 @@ impl<'a> ListColumn<'a> {
     }
 }
 
-/// A leaf under 1..=4 list levels of any kind (fixed width, Boolean, Binary / Utf8).
+/// A leaf under 1..=4 nests -- List / LargeList / Map and Struct nests, the
+/// InitNested chain of read/deserialize.rs:140-233 -- of any kind (fixed
+/// width, Boolean, Binary / Utf8).
 pub struct NestedColumn<'a> {
     ctx: &'a Context,
     plan: Plan,
@@ -434,8 +436,9 @@ pub struct NestedColumn<'a> {
 }
 
 pub struct Nested {
-    /// Per list level (outermost first): offsets and optional validity.
-    pub offsets: Vec<DeviceBuffer>,
+    /// Per nest (outermost first): offsets (list / map nests; None for a
+    /// struct nest) and optional validity.
+    pub offsets: Vec<Option<DeviceBuffer>>,
     pub validity: Vec<Option<DeviceBuffer>>,
     /// Leaf values (fixed width), the leaf bitmap (Boolean) or value bytes (Binary / Utf8).
     pub values: DeviceBuffer,
@@ -446,11 +449,16 @@ pub struct Nested {
 }
 
 impl<'a> NestedColumn<'a> {
+    /// `list_nullable[d]`: nest d is nullable; bit d of `struct_mask`: nest d
+    /// is a Struct (else a List / Map).
     pub fn plan(ctx: &'a Context, chunk: &'a DeviceBuffer, pages: &[PageMeta], ty: PhysicalType, list_nullable: &[bool],
-                item_nullable: bool, large: bool) -> Result<Self> {
+                item_nullable: bool, large: bool, struct_mask: u32) -> Result<Self> {
         ctx.check_chunk(chunk)?;
         if list_nullable.is_empty() || list_nullable.len() > ffi::SB_MAX_NEST {
             return Err(Error::NotYetImplemented(format!("nesting depth {}", list_nullable.len())));
+        }
+        if struct_mask >> list_nullable.len() != 0 {
+            return Err(Error::Argument(format!("struct mask {struct_mask:#x} past depth {}", list_nullable.len())));
         }
         let mut ln = [0i32; ffi::SB_MAX_NEST];
         for (d, &x) in list_nullable.iter().enumerate() {
@@ -462,6 +470,7 @@ impl<'a> NestedColumn<'a> {
             list_nullable: ln,
             item_nullable: item_nullable as i32,
             offset_width: if large { 8 } else { 4 },
+            struct_mask: struct_mask as i32,
         };
         let mut raw = ptr::null_mut();
         status(unsafe {
@@ -484,8 +493,8 @@ impl<'a> NestedColumn<'a> {
         let mut offsets = Vec::new();
         let mut validity = Vec::new();
         for d in 0..depth {
-            let o = self.ctx.alloc((counts[d] as usize + 1) * ow)?;
-            out.d_offsets[d] = o.ptr;
+            let o = if (self.desc.struct_mask >> d) & 1 == 0 { Some(self.ctx.alloc((counts[d] as usize + 1) * ow)?) } else { None };
+            out.d_offsets[d] = o.as_ref().map_or(ptr::null_mut(), |b| b.ptr);
             offsets.push(o);
             let v = if self.desc.list_nullable[d] != 0 { Some(self.ctx.alloc(bitmap_bytes(counts[d]))?) } else { None };
             out.d_validity[d] = v.as_ref().map_or(ptr::null_mut(), |b| b.ptr as *mut u8);
@@ -525,6 +534,10 @@ pub struct Leaf {
     pub large_list: Vec<bool>,
     pub flags: u32,
     pub top_field: i32,
+    /// bit d: nest d is a Struct / a Map; nest d's pre-order id in the schema
+    pub struct_mask: u32,
+    pub map_mask: u32,
+    pub nest_id: Vec<i32>,
 }
 
 /// `infer_schema` + arrow2 `deserialize_schema`, flattened to leaves.
@@ -547,6 +560,9 @@ pub fn parse_schema(bytes: &[u8]) -> Result<Vec<Leaf>> {
             large_list: l.large_list[..depth].iter().map(|&x| x != 0).collect(),
             flags: l.flags,
             top_field: l.top_field,
+            struct_mask: l.struct_mask,
+            map_mask: l.map_mask,
+            nest_id: l.nest_id[..depth].to_vec(),
         }
     }).collect())
 }
