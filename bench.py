@@ -745,17 +745,47 @@ class WorkloadC5:
         np.cumsum([len(x) for x in s], out=offs[1:])
         return b"".join(s), offs
 
+    @classmethod
+    def specs(cls):
+        """(dtype | "utf8", value kind) of the table's 64 columns, in order."""
+        return ([(np.int32, k) for k in cls.I32] + [(np.int64, k) for k in cls.I64] +
+                [(np.float64, k) for k in cls.F64] + [("utf8", k) for k in cls.STR] +
+                [(np.bool_, k) for k in cls.BOOL] + [(np.uint32, k) for k in cls.U32])
+
+    @staticmethod
+    def rank_columns(n_columns, world, rank):
+        """The table's columns round-robin over the ranks:
+        this rank builds and decodes columns ci with ci % world == rank."""
+        return [ci for ci in range(n_columns) if ci % world == rank]
+
+    @classmethod
+    def host_column(cls, pa, dt, kind, ci, rows, seed, threads):
+        """Column ci's source values and its host-writer chunk ->
+        (values | (bytes, offsets), validity | None, nullable, opts, chunk, metas, host encode seconds)."""
+        rng = np.random.default_rng([seed, ci])  # each column its own generator
+        nullable = dt != "utf8" and ci % 4 == 3
+        valid = (rng.random(rows) >= 0.1) if nullable else None
+        basic = kind in ("lz4", "none")
+        opts = pa.WriteOptions(default_compression=1 if kind == "lz4" else 0,
+                               default_compress_ratio=None if basic else 2.0, max_page_size=PAGE_ROWS, seed=seed + ci)
+        if dt == "utf8":
+            svals, soffs = cls._strings(kind, rows, rng)
+            t0 = time.perf_counter()
+            chunk, metas = pa.encode_binary_column(svals, soffs, None, False, opts, physical_type=pa.UTF8,
+                                                   n_threads=threads)
+            return (svals, soffs), None, False, opts, chunk, metas, time.perf_counter() - t0
+        v = cls._values(dt, kind, rows, rng)
+        t0 = time.perf_counter()
+        chunk, metas = pa.encode_column(v, valid, nullable, opts, n_threads=threads)
+        return v, valid, nullable, opts, chunk, metas, time.perf_counter() - t0
+
     def __init__(self, torch, pa, rows, seed, device, threads, world=1, rank=0):
         self.rows = rows
         self.threads = threads
         dev = f"cuda:{device}"
-        specs = ([(np.int32, k) for k in self.I32] + [(np.int64, k) for k in self.I64] +
-                 [(np.float64, k) for k in self.F64] + [("utf8", k) for k in self.STR] +
-                 [(np.bool_, k) for k in self.BOOL] + [(np.uint32, k) for k in self.U32])
-        # the table's columns round-robin over the ranks:
-        # this rank builds and decodes columns ci with ci % world == rank
+        specs = self.specs()
         self.n_columns = len(specs)
-        self.col_ids = [ci for ci in range(len(specs)) if ci % world == rank]
+        self.col_ids = self.rank_columns(len(specs), world, rank)
         specs = [specs[ci] for ci in self.col_ids]
         self.cols = []
         self.host = []  # (dt, chunk, metas, nullable, values_len) for the CPU baseline
@@ -767,30 +797,17 @@ class WorkloadC5:
         nb = (rows + 7) // 8
         self.ss = StreamSet(torch, pa, device, 4)
         enc = []  # device encode inputs: (dt, opts, nullable, device tensors)
-        for gi, (dt, kind) in zip(self.col_ids, specs):
-            rng = np.random.default_rng([seed, gi])  # each column its own generator
-            ci = gi
-            nullable = dt != "utf8" and ci % 4 == 3
-            valid = (rng.random(rows) >= 0.1) if nullable else None
-            basic = kind in ("lz4", "none")
-            opts = pa.WriteOptions(default_compression=1 if kind == "lz4" else 0,
-                                   default_compress_ratio=None if basic else 2.0, max_page_size=PAGE_ROWS, seed=seed + ci)
+        for ci, (dt, kind) in zip(self.col_ids, specs):
+            v, valid, nullable, opts, chunk, metas, enc_s = self.host_column(pa, dt, kind, ci, rows, seed, threads)
+            self.encode_s += enc_s
             if dt == "utf8":
-                svals, soffs = self._strings(kind, rows, rng)
-                t0 = time.perf_counter()
-                chunk, metas = pa.encode_binary_column(svals, soffs, None, False, opts, physical_type=pa.UTF8,
-                                                       n_threads=threads)
-                self.encode_s += time.perf_counter() - t0
+                svals, soffs = v
                 raw = len(svals) + 4 * (rows + 1)
                 exp = (torch.from_numpy(soffs.astype(np.int32)).to(dev),
                        torch.from_numpy(np.frombuffer(svals, np.uint8).copy()).to(dev))
                 enc.append((dt, opts, False, (exp[1], torch.from_numpy(soffs).to(dev), None)))
                 self.host.append((dt, chunk, metas, False, len(svals)))
             else:
-                v = self._values(dt, kind, rows, rng)
-                t0 = time.perf_counter()
-                chunk, metas = pa.encode_column(v, valid, nullable, opts, n_threads=threads)
-                self.encode_s += time.perf_counter() - t0
                 raw = nb if dt == np.bool_ else v.nbytes
                 tv = torch.from_numpy(v).to(dev)
                 ev = tv if dt == np.bool_ else tv.view(torch.uint8)

@@ -177,3 +177,126 @@ def test_shard_pages_balanced():
         lens = [s.byte_len for s in sh]
         assert max(lens) - min(lens) <= 2 * 1070
         assert sum(s.rows for s in sh) == 8192 * 1000
+
+
+# ---- world size 4: bench.py's own partitioning, oracle standing in ----------
+def _bench_worker(rank, world, port, q):
+    """One rank of bench.py's N>1 legs on CPU: the C4-shaped List<Int32>
+    column and the C2 column through bench.ShardedColumn (provisional blocks,
+    all-gathered page metas, shard_pages), C5's columns round-robin
+    (WorkloadC5.rank_columns); each rank decodes its part with the oracle and
+    the parts are reassembled on rank 0 against whole-column decodes."""
+    import torch.distributed as dist
+
+    import bench
+    import pa_amd
+    from oracle import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows = 3 * bench.BLOCK_PAGES * 512  # per rank; blocks of 64 pages of PAGE_ROWS rows are too big for CPU
+    out = {}
+    saved = bench.PAGE_ROWS
+    bench.PAGE_ROWS = 512
+    try:
+        def c2_block(b, r0, n):
+            v = bench.gen_c2(n, 7, "mix", r0)
+            opts = pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=bench.PAGE_ROWS, seed=7 + b)
+            chunk, metas = pa_amd.encode_column(v, None, False, opts)
+            return v, chunk, metas
+
+        col = bench.ShardedColumn(pa_amd, dist, world, rank, world * rows, c2_block)
+        vals, _ = O.read_column(col.chunk, [(m.length, m.num_values) for m in col.metas], np.int32)
+        parts = [None] * world
+        dist.all_gather_object(parts, (col.global_shard.row_offset, vals, col.flat_values()))
+        if rank == 0:
+            parts.sort(key=lambda p: p[0])
+            full = np.concatenate([p[1] for p in parts])
+            src = np.concatenate([p[2] for p in parts])
+            out["c2"] = bool(len(full) == world * rows and (full == src).all()
+                             and (full == bench.gen_c2(world * rows, 7, "mix")).all())
+
+        def l_block(b, r0, n):
+            rng = np.random.default_rng([99, b])
+            ln = rng.integers(0, 3, n)
+            lv = rng.random(n) >= 0.1
+            ln[~lv] = 0
+            offs = np.zeros(n + 1, np.int64)
+            np.cumsum(ln, out=offs[1:])
+            child = rng.integers(0, 1 << 16, int(offs[-1])).astype(np.int32)
+            cv = rng.random(len(child)) >= 0.2
+            opts = pa_amd.WriteOptions(default_compress_ratio=1.2, max_page_size=bench.PAGE_ROWS, seed=b)
+            chunk, metas = pa_amd.encode_list_column(offs, child, lv, cv, True, True, opts)
+            return (offs, child, lv, cv), chunk, metas
+
+        col = bench.ShardedColumn(pa_amd, dist, world, rank, world * rows, l_block)
+        m = [(x.length, x.num_values) for x in col.metas]
+        offs, lv, child, cv = O.read_list_column(col.chunk, m, np.int32, True, True)
+        leaf_base = pa_amd.shard_base(len(child), rank)  # the one exchange (setup only)
+        parts = [None] * world
+        dist.all_gather_object(parts, (col.global_shard.row_offset, offs + leaf_base, lv, child, cv))
+        if rank == 0:
+            parts.sort(key=lambda p: p[0])
+            go = np.concatenate([parts[0][1][:1]] + [p[1][1:] for p in parts])
+            nb = (world * rows + bench.BLOCK_PAGES * bench.PAGE_ROWS - 1) // (bench.BLOCK_PAGES * bench.PAGE_ROWS)
+            whole, wm = b"", []
+            for b in range(nb):
+                r0 = b * bench.BLOCK_PAGES * bench.PAGE_ROWS
+                _, ch, mt = l_block(b, r0, min(bench.BLOCK_PAGES * bench.PAGE_ROWS, world * rows - r0))
+                whole += ch
+                wm += [(x.length, x.num_values) for x in mt]
+            eo, elv, ec, ecv = O.read_list_column(whole, wm, np.int32, True, True)
+            out["c4"] = bool((go == eo).all() and (np.concatenate([p[2] for p in parts]) == elv).all()
+                             and (np.concatenate([p[3] for p in parts]) == ec).all()
+                             and (np.concatenate([p[4] for p in parts]) == ecv).all())
+
+        specs = bench.WorkloadC5.specs()
+        mine = bench.WorkloadC5.rank_columns(len(specs), world, rank)
+        n5 = 3000
+        got = {}
+        for ci in mine:
+            dt, kind = specs[ci]
+            v, valid, nullable, _, chunk, metas, _ = bench.WorkloadC5.host_column(pa_amd, dt, kind, ci, n5, 555, 1)
+            m = [(x.length, x.num_values) for x in metas]
+            if dt == "utf8":
+                o, b, _ = O.read_binary_column(chunk, m, False)
+                ok = b == v[0] and (o == v[1]).all()
+            elif dt == np.bool_:
+                bits, vv = O.read_bool_column(chunk, m, nullable)
+                keep = valid if nullable else np.ones(n5, bool)
+                ok = (bits[keep] == v[keep]).all() and (not nullable or (vv == valid).all())
+            else:
+                x, vv = O.read_column(chunk, m, dt, nullable)
+                keep = valid if nullable else np.ones(n5, bool)
+                ok = (x[keep] == v[keep]).all() and (not nullable or (vv == valid).all())
+            got[ci] = bool(ok)
+        parts = [None] * world
+        dist.all_gather_object(parts, got)
+        if rank == 0:
+            allc = {}
+            for d in parts:
+                assert not set(d) & set(allc), "a column decoded on two ranks"
+                allc.update(d)
+            out["c5"] = sorted(allc) == list(range(len(specs))) and all(allc.values())
+    finally:
+        bench.PAGE_ROWS = saved
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_partitions_world(world):
+    """bench.py's C2 / C4 page shards and C5 column round-robin at world
+    size 4 and 8 over gloo (the 4-GPU C4 and 8-GPU C5 splits rehearsed on
+    CPU): the reassembled columns equal the whole-column oracle decodes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == {"c2": True, "c4": True, "c5": True}, res[0]
