@@ -626,6 +626,14 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "plan alloc: look-back");
     }
+    // Utf8 through the fused pass: it flags the pages whose emitted rows are
+    // whole, valid entries (OneValue / Dict / Freq), and the check skips them
+    const bool utf8 = desc->physical_type == SB_T_UTF8 || desc->physical_type == SB_T_LARGE_UTF8;
+    if (p->d_lb && utf8 && !getenv("SB_NO_ENTRY_UTF8") &&
+        (hipMalloc(&p->d_ascii, n_pages) != hipSuccess || hipMemsetAsync(p->d_ascii, 0, n_pages, ctx->stream) != hipSuccess)) {
+      sb_plan_destroy(p);
+      return fail(ctx, SB_E_DEVICE, "plan alloc: entry flags");
+    }
   }
   *out = p;
   return SB_OK;
@@ -652,6 +660,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
                     (uint32_t*)out->d_validity, p->d_status, p->d_jobs, nullptr, p->d_scratch, p->bin_lds, nullptr,
                     (uint32_t*)(p->d_bin + 2 * np + 2), p->bin_grid, p->d_region, nullptr, p->n_big, p->d_lb};
     F.zstd = p->zstd;
+    F.checked = p->d_ascii;
     if (sb::launch_binary(3, p->offset_width, F, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "binary decode launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else {
@@ -687,7 +696,7 @@ sb_status sb_decode_binary_planned(sb_ctx* ctx, sb_plan* p, const sb_binary_out*
     uint32_t* flags = (uint32_t*)(p->d_bin + 2 * np + 1);
     HIP_TRY(ctx, hipMemsetAsync(flags, 0, sizeof(uint32_t), ctx->stream));
     sb::Utf8Launch U{out->d_values, p->values_bytes, (const uint8_t*)out->d_offsets, p->n_rows, p->d_pages,
-                     (uint32_t)np, p->d_bin + np, p->d_status, flags, p->d_lb ? nullptr : p->d_ascii};
+                     (uint32_t)np, p->d_bin + np, p->d_status, flags, p->d_ascii};
     if (sb::launch_utf8_check(p->offset_width, U, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "utf8 check launch failed: %s", hipGetErrorString(hipGetLastError()));
   }

@@ -2666,6 +2666,7 @@ struct BinArgs {
   uint8_t* region;     // big pages' tables (PageDesc.reserved = region offset + 1)
   uint64_t* rneed;     // plan time (k_bin_probe): region bytes per page
   uint64_t* lb;        // fused pass: look-back state per page, then the page counter (zeroed by the host)
+  uint8_t* checked;    // fused pass, Utf8: per page, its rows are whole valid entries (BinLaunch::checked)
 };
 
 enum : uint32_t { BIN_BASIC = 0, BIN_ONE = 12, BIN_DICT = 11, BIN_FREQ = 13 };
@@ -3780,6 +3781,50 @@ __device__ uint64_t lookback(uint64_t* lb, uint32_t page, uint64_t S) {
   return acc;
 }
 
+// RFC 3629 validity of the bytes [pos, pos + len) of a staged page, one
+// thread (simdutf8's rules, as k_utf8_bytes: no overlong forms, no
+// surrogates, nothing past U+10FFFF, no truncated sequence).
+__device__ bool utf8_span_ok(const LdsSrc& s, uint32_t pos, uint32_t len) {
+  auto trail = [](uint32_t b) { return (b & 0xC0u) == 0x80u; };
+  for (uint32_t i = 0; i < len;) {
+    const uint32_t b = s.u8(pos + i);
+    if (b < 0x80u) {
+      i++;
+      continue;
+    }
+    const uint32_t L = b < 0xC2u ? 0u : b < 0xE0u ? 2u : b < 0xF0u ? 3u : b < 0xF5u ? 4u : 0u;
+    if (L == 0 || L > len - i) return false;
+    const uint32_t c1 = s.u8(pos + i + 1);
+    if (!trail(c1) || (b == 0xE0u && c1 < 0xA0u) || (b == 0xEDu && c1 >= 0xA0u) || (b == 0xF0u && c1 < 0x90u) ||
+        (b == 0xF4u && c1 >= 0x90u))
+      return false;
+    if (L >= 3 && !trail(s.u8(pos + i + 2))) return false;
+    if (L == 4 && !trail(s.u8(pos + i + 3))) return false;
+    i += L;
+  }
+  return true;
+}
+
+// Whether every row an Extend page emits is valid UTF-8 by itself: each row
+// is a whole dictionary entry, the top value or an exception (OneValue /
+// Dict / Freq), so checking those entries once is the whole-buffer check of
+// Utf8Array::try_new (read/array/binary.rs:305-306) for the page's bytes --
+// a concatenation of valid strings is valid and every row starts a
+// character.  A page with an invalid entry (referenced or not) returns false
+// and its emitted bytes are checked as they are.  All NT threads.
+__device__ bool extend_entries_utf8(const LdsSrc& s, const BinInfo& bi, TabBase<true> tb, uint32_t n) {
+  bool ok = true;
+  const uint32_t tid = threadIdx.x;
+  if (bi.codec == BIN_ONE) {
+    if (tid == 0 && n) ok = utf8_span_ok(s, bi.top, bi.L);
+  } else {
+    const mptr<true, uint64_t> tab = tb.template at<uint64_t>(bi.otab);
+    for (uint32_t x = tid; x < bi.k; x += NT) ok &= utf8_span_ok(s, (uint32_t)tab[x], (uint32_t)(tab[x] >> 32));
+    if (bi.codec == BIN_FREQ && tid == 0 && bi.k < n) ok &= utf8_span_ok(s, bi.top, bi.L);
+  }
+  return !__syncthreads_or(!ok);
+}
+
 // Pass 2 over the staged pages (FUSED = false: bases from k_bin_size /
 // k_bin_scan), or the whole decode in one pass when every page of the plan
 // is staged (FUSED = true: pages claimed in order from a counter, each sized
@@ -3934,6 +3979,11 @@ __device__ __forceinline__ void bin_decode_pages(BinArgs& a) {
       }
     }
     __syncthreads();
+    if (FUSED && a.checked) {  // Utf8: this page's rows need no byte check when its entries are valid
+      const bool ext = !sh.err && (bi.codec == BIN_ONE || bi.codec == BIN_DICT || bi.codec == BIN_FREQ);
+      const bool ok = ext && extend_entries_utf8(s, bi, tb, n);
+      if (tid == 0) a.checked[page] = ok ? 1 : 0;
+    }
     SB_PHASE(4);
     if (tid == 0) a.status[page] = sh.err;
     __syncthreads();
@@ -5359,7 +5409,7 @@ int launch_binary(int stage, int offset_width, const BinLaunch& L, void* stream)
   const uint32_t lds = L.lds_bytes ? std::min(L.lds_bytes, kDeferredLds) : kDeferredLds;
   sbk::BinArgs a{L.chunk, L.pages, L.n_pages, L.nullable, L.sizes, L.bases, L.total, L.out_offsets, L.out_values,
                  L.values_cap, L.out_validity, L.status, lds, L.jobs, L.job_count, L.scratch, L.lds_need, L.cls,
-                 L.region, L.rneed, L.lb};
+                 L.region, L.rneed, L.lb, L.checked};
   hipStream_t st = (hipStream_t)stream;
   const dim3 block(sbk::NT);
   // staged passes: one workgroup per listed page (grid-stride), as many

@@ -190,6 +190,8 @@ struct BinLaunch {
   uint64_t* lb;           // stage 3: look-back states (n_pages) + page counter
   uint32_t zstd = 1;      // 0: no page has a Zstd stream (the kernels without the decoder, LaunchArgs::zstd);
                           // stage 2 reports it through `total` (bit 0 set by a page with a Zstd stream)
+  uint8_t* checked = nullptr;  // stage 3, Utf8 plans: per page, 1 = every row it emitted is a whole
+                               // entry that is valid UTF-8 (the check skips its bytes), else 0
 };
 // stage 2: plan-time probe (lds_need / rneed per page); stage 3: the fused
 // single pass when every page is staged (sizes, bases, offsets, values).

@@ -227,3 +227,89 @@ def test_nested_utf8_leaf_checked(ctx, tmp_path, valid):
         with pytest.raises(pa_amd.StrawboatError) as e:
             dec.decode()
         assert e.value.status == pa_amd._native.E_OUT_OF_SPEC
+
+
+def _dict_page_with_extra_entry(page: bytes, extra: bytes) -> bytes:
+    """A non-nullable binary Dict page (binary/dict.rs:55-93 layout: [11]
+    [csize][usize] [index stream] [u32 k] k x ([u64 len][bytes])) with one more
+    dictionary entry that no row references."""
+    assert page[0] == O.DICT
+    body = page[9:]
+    ic = int.from_bytes(body[1:5], "little")
+    kpos = 9 + ic
+    k = int.from_bytes(body[kpos:kpos + 4], "little")
+    body = body[:kpos] + (k + 1).to_bytes(4, "little") + body[kpos + 4:] + len(extra).to_bytes(8, "little") + extra
+    return bytes([O.DICT]) + len(body).to_bytes(4, "little") + page[5:9] + body
+
+
+@pytest.mark.parametrize("opt", ["dict", "freq", "one"])
+def test_extend_entries_checked_once(ctx, opt):
+    """Dict / Freq / OneValue pages (the fused pass validates each entry once
+    instead of the emitted rows): valid multi-byte entries decode; an invalid
+    entry any row references -- a dictionary entry, the Freq top value or an
+    exception, the OneValue -- is OutOfSpec on its page, as the reference's
+    check of the emitted values buffer."""
+    import pa_amd
+
+    rng = np.random.default_rng(3)
+    n, page_rows = 6000, 1500
+    pool = text(rng, 40, 8) + ["€uro".encode(), "日本語テキスト".encode()]
+    if opt == "one":
+        strs = ["同じ値".encode()] * n
+        o = dict(default_compress_ratio=2.0)
+    elif opt == "freq":
+        strs = [pool[i] if rng.random() < 0.05 else "共通の値".encode() for i in rng.integers(0, len(pool), n)]
+        o = OPTS["freq"]
+    else:
+        strs = [pool[i] for i in rng.integers(0, len(pool), n)]
+        o = OPTS["dict"]
+    for nullable in (False, True):
+        chunk, metas = encode(strs, nullable, o, pa_amd.UTF8, rng, page_rows)
+        codecs = set(O.page_codec(chunk[sum(m.length for m in metas[:i]):], nullable) for i in range(len(metas)))
+        assert codecs == {{"dict": O.DICT, "freq": O.FREQ, "one": O.ONE_VALUE}[opt]}, codecs
+        dec = pa_amd.BinaryColumnDecoder(chunk, metas, pa_amd.UTF8, nullable, ctx)
+        assert status(ctx, dec) == (0, -1)
+        oo, v, _ = dec.decode()
+        eo, ev, _ = O.read_binary_column(chunk, [(x.length, x.num_values) for x in metas], nullable)
+        assert (oo.cpu().numpy() == eo).all() and v.cpu().numpy()[:len(ev)].tobytes() == ev
+        dec.close()
+    for row in (0, 2999, 5999):
+        bad = list(strs)
+        if opt == "one":
+            bad = [b"ab\xe2\x28\xa1"] * n if row == 0 else bad
+            if row:
+                continue
+        elif opt == "freq" and row == 2999:  # the top value itself
+            bad = [b"\xc3" if s == "共通の値".encode() else s for s in strs]
+        else:
+            bad[row] = b"x\xed\xa0\x80"
+        chunk, metas = encode(bad, False, o, pa_amd.UTF8, rng, page_rows)
+        eo, ev, _ = O.read_binary_column(chunk, [(x.length, x.num_values) for x in metas], False)
+        assert not O.check_utf8(ev, eo)
+        dec = pa_amd.BinaryColumnDecoder(chunk, metas, pa_amd.UTF8, False, ctx)
+        st, page = status(ctx, dec)
+        assert st == pa_amd._native.E_OUT_OF_SPEC, (opt, row, st)
+        if not (opt == "freq" and row == 2999):
+            assert page == row // page_rows, (opt, row, page)
+        dec.close()
+
+
+def test_unreferenced_invalid_dict_entry_is_not_checked(ctx):
+    """An invalid dictionary entry that no row references never reaches the
+    values buffer, so Utf8Array::try_new accepts the array: the page's
+    emitted bytes are then checked as they are, and pass."""
+    import pa_amd
+
+    rng = np.random.default_rng(4)
+    pool = [f"v{i}é".encode() for i in range(20)]
+    strs = [pool[i] for i in rng.integers(0, 20, 800)]
+    chunk, metas = encode(strs, False, OPTS["dict"], pa_amd.UTF8, rng, 800)
+    assert len(metas) == 1
+    page = _dict_page_with_extra_entry(chunk, b"\xff\xfe")
+    m = [pa_amd.PageMeta(len(page), 800)]
+    eo, ev, _ = O.read_binary_column(page, [(len(page), 800)], False)
+    assert O.check_utf8(ev, eo) and ev == b"".join(strs)
+    dec = pa_amd.BinaryColumnDecoder(page, m, pa_amd.UTF8, False, ctx)
+    assert status(ctx, dec) == (0, -1)
+    oo, v, _ = dec.decode()
+    assert (oo.cpu().numpy() == eo).all() and v.cpu().numpy()[:len(ev)].tobytes() == ev
