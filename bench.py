@@ -293,7 +293,39 @@ def encode_gpu(torch, pa, rows: int, device: int, threads: int, steps: int) -> d
                      "encoded_bytes": len(host), "host_writer_GBps": round(v.nbytes / th / 1e9, 2),
                      "host_threads": threads, "byte_identical_to_host": bool(ok)}
         del tv, chunk, dout
+    out["zstd_size_vs_libzstd3"] = zstd_size(torch, pa, device, threads)
     return out
+
+
+def zstd_size(torch, pa, device: int, threads: int, rows: int = 8 * 1024 * 1024) -> dict:
+    """Default-Zstd chunks written on the device (sb_zstdc.h: frames transcoded
+    from the wave LZ4 parse) against the host writer's (libzstd level 3, what
+    the reference's zstd::bulk::compress level 0 writes, basic.rs:122-135),
+    in bytes, on C3's two columns (1024 pages each); LZ4 chunk bytes beside
+    them.  Both decode to the same values (tests/test_gpu_encode_adaptive.py)."""
+    rng = np.random.default_rng(3)
+    f = np.round(rng.standard_normal(rows) * 1e4, 2)
+    svals, soffs = decimal_strings(rng.integers(0, 10**6, rows))
+    dev = f"cuda:{device}"
+    res = {}
+    for name in ("c3_float64", "c3_utf8"):
+        sizes = {}
+        for codec in (2, 1):
+            opts = pa.WriteOptions(default_compression=codec, max_page_size=PAGE_ROWS)
+            if name == "c3_float64":
+                d, _ = pa.encode_column_device(torch.from_numpy(f).to(dev), None, False, opts)
+                h, _ = pa.encode_column(f, None, False, opts, n_threads=threads)
+            else:
+                d, _ = pa.encode_binary_column_device(torch.from_numpy(np.frombuffer(svals, np.uint8).copy()).to(dev),
+                                                      torch.from_numpy(soffs).to(dev), None, False, opts,
+                                                      physical_type=pa.UTF8)
+                h, _ = pa.encode_binary_column(svals, soffs, None, False, opts, physical_type=pa.UTF8,
+                                               n_threads=threads)
+            sizes[codec] = (int(d.numel()), len(h))
+        res[name] = {"device_zstd_bytes": sizes[2][0], "libzstd3_bytes": sizes[2][1],
+                     "device_over_libzstd3": round(sizes[2][0] / sizes[2][1], 3), "lz4_bytes": sizes[1][1],
+                     "lz4_over_libzstd3": round(sizes[1][1] / sizes[2][1], 3)}
+    return res
 
 
 def cpu_info() -> dict:

@@ -71,7 +71,7 @@ struct sb_plan {
   uint8_t* d_scratch = nullptr;      // binary: expanded offsets streams
   uint8_t* d_region = nullptr;       // fixed width: the pages' HBM regions (PageDesc.reserved)
   uint32_t* d_spill = nullptr;       // [2] spilled-leaf job counts (by decode parity)
-  uint32_t* d_sched = nullptr;       // [2][2] k_inflate's job claim counters (zero between launches), two pairs
+  uint32_t* d_sched = nullptr;       // [2][3] k_inflate's job claim counters (zero between launches), two triples
   uint32_t sched_flip = 0;           // the pair the next inflate launch claims from
   uint8_t* d_ascii = nullptr;        // binary: per page, its values stream inflated all ASCII (k_inflate)
   sb::InflateJob* d_spill_jobs = nullptr;
@@ -100,6 +100,7 @@ struct sb_plan {
   uint32_t bin_grid = 0;      // staged-pass workgroups: the plan pass's staged page count
   uint32_t bin_lds = 0;       // dynamic LDS of the binary kernels (the largest page need, from the plan pass)
   uint32_t zstd = 1;          // some page has a Zstd stream (0: the decode kernels without the Zstd decoder)
+  uint32_t patas = 1;         // some page has a Patas stream (0: no k_patas ahead of the inflate launches)
   uint64_t values_bytes = 0;
   uint32_t n_staged = 0, n_global = 0;
   bool staged_identity = false;  // every page staged: no index list
@@ -116,8 +117,8 @@ static void sched_pair(sb_plan* p, sb::InflateLaunch& I) {
   if (!p->d_sched || I.n_jobs == 0) return;
   const uint32_t f = p->sched_flip;
   p->sched_flip ^= 1u;
-  I.sched = p->d_sched + 2 * f;
-  I.sched_spare = p->d_sched + 2 * (f ^ 1u);
+  I.sched = p->d_sched + 3 * f;
+  I.sched_spare = p->d_sched + 3 * (f ^ 1u);
 }
 
 static sb_status fail(sb_ctx* ctx, sb_status st, const char* fmt, ...) {
@@ -452,8 +453,8 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
   if (e == hipSuccess) e = hipMalloc(&p->d_defer, (np + 4) * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemsetAsync(p->d_defer, 0, 4 * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipMalloc(&p->d_jobs, (owidth ? 2 : 1) * np * sizeof(sb::InflateJob));
-  if (e == hipSuccess) e = hipMalloc(&p->d_sched, 4 * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemsetAsync(p->d_sched, 0, 4 * sizeof(uint32_t), ctx->stream);
+  if (e == hipSuccess) e = hipMalloc(&p->d_sched, 6 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(p->d_sched, 0, 6 * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipEventCreate(&p->ev0);
   if (e == hipSuccess) e = hipEventCreate(&p->ev1);
   if (e == hipSuccess && n_pages) {
@@ -484,7 +485,8 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
       sb_plan_destroy(p);
       return fail(ctx, SB_E_DEVICE, "plan zstd scan: %s", hipGetErrorString(e));
     }
-    p->zstd = flag ? 1 : 0;
+    p->zstd = (flag & 1) ? 1 : 0;
+    p->patas = (flag & 2) ? 1 : 0;
     if (is_bool && !p->zstd) p->stage_bytes = std::max<uint32_t>(max_bool_noz, 64);
   }
   if (is_bool && n_pages) {
@@ -765,6 +767,8 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
     sb::InflateLaunch I{p->d_chunk, p->d_jobs, p->d_defer + 2 + a.parity, (uint32_t)p->n_pages,
                         (uint8_t*)out->d_values, nullptr, nullptr, p->d_status, nullptr, p->d_sched};
     sched_pair(p, I);
+    static const bool no_patas_wg = getenv("SB_NO_PATAS_WG") != nullptr;  // A/B: the one-wave Patas decoder
+    I.patas_wg = p->is_float && p->patas && !no_patas_wg ? 1u : 0u;
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))

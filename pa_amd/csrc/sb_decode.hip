@@ -1798,6 +1798,7 @@ __device__ uint32_t patas_wave(const uint8_t* src, uint32_t ilen, uint8_t* dst, 
   return ST_OK;
 }
 
+
 #include "sb_zstd.h"
 
 // One wave expands the general-codec stream [src, src + csize) of `olen`
@@ -2414,7 +2415,7 @@ __global__ __launch_bounds__(NT) void k_decode_spilled(LaunchArgs a) {
 // Plan-time cascade walk of a fixed-width (or Boolean: W 1, one stream) page
 // from HBM, the header walk of decode_page without the tables: bit 0 a Freq
 // in the cascade, bit 1 a general-codec / Patas leaf, bit 2 under a Dict /
-// Freq, bit 3 some stream of the cascade is Zstd.
+// Freq, bit 3 some stream of the cascade is Zstd, bit 4 some stream is Patas.
 __device__ uint32_t fix_cascade(const GlbSrc& s, uint32_t len, uint32_t W, int nullable) {
   uint32_t p = 0, bits = 0;
   auto hdr = [&](uint32_t q, uint32_t* codec, uint32_t* body, uint32_t* cs) {
@@ -2423,6 +2424,7 @@ __device__ uint32_t fix_cascade(const GlbSrc& s, uint32_t len, uint32_t W, int n
     *cs = s.u32(q + 1);
     *body = q + 9;
     if (*codec == 2) bits |= 8;
+    if (*codec == 16) bits |= 16;
     return *cs <= len - *body;
   };
   do {
@@ -2474,17 +2476,19 @@ __global__ __launch_bounds__(NT) void k_fix_probe(const uint8_t* chunk, const Pa
   probe[i] = fix_cascade(GlbSrc{chunk + pd.byte_off}, pd.byte_len, W, nullable);
 }
 
-// Plan time: *flag = 1 when some page has a Zstd stream (the plan then
-// launches the kernels that carry the Zstd decoder).
+// Plan time: *flag |= 1 when some page has a Zstd stream (the plan then
+// launches the kernels that carry the Zstd decoder), |= 2 when some page has
+// a Patas stream (the inflate launches then start with k_patas).
 __global__ __launch_bounds__(NT) void k_zstd_scan(const uint8_t* chunk, const PageDesc* pages, uint32_t n, uint32_t W,
                                                   int nullable, uint32_t* flag) {
   const uint32_t i = blockIdx.x * NT + threadIdx.x;
-  bool z = false;
+  uint32_t c = 0;
   if (i < n) {
     const PageDesc pd = pages[i];
-    z = (fix_cascade(GlbSrc{chunk + pd.byte_off}, pd.byte_len, W, nullable) & 8) != 0;
+    c = fix_cascade(GlbSrc{chunk + pd.byte_off}, pd.byte_len, W, nullable);
   }
-  if (__ballot(z) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+  const uint32_t f = (__ballot(c & 8) ? 1u : 0u) | (__ballot(c & 16) ? 2u : 0u);
+  if (f && (threadIdx.x & 63) == 0) atomicOr(flag, f);
 }
 
 template <int W, bool FLT>
@@ -2543,7 +2547,9 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
   // grid-strided.
   const uint32_t waves = gridDim.x * kInfWaves, part = min(waves, n);
   uint32_t j = blockIdx.x * kInfWaves + wv;
-  if (a.sched_spare && j == 0 && lane < 2) a.sched_spare[lane] = 0;
+  if (a.sched_spare && j == 0 && lane < 3) a.sched_spare[lane] = 0;
+  // every job k_patas's (it counted the others in a.sched[2]): no claims at all
+  if (a.patas_wg && a.sched && __builtin_nontemporal_load(&a.sched[2]) == 0) return;
   if (j >= part) return;
   for (bool first = true;; first = false) {
     if (a.sched) {
@@ -2595,6 +2601,7 @@ __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(Infla
       st = snappy_wave<true>(w, p0, p0 + jb.csize, o);
     } else if ((jb.codec & 0xFF) == 16) {  // Patas leaf: codec 16 | width << 8
       const uint32_t W = jb.codec >> 8;
+      if (a.patas_wg && kind <= 1 && patas_fits(jb.csize, jb.usize / W, W)) continue;  // k_patas's
       st = W == 8 ? patas_wave<8>(src, jb.csize, dst, jb.usize / 8, o.ring, (lds_u8*)&ibufs[wv][0])
                   : patas_wave<4>(src, jb.csize, dst, jb.usize / 4, o.ring, (lds_u8*)&ibufs[wv][0]);
     }
@@ -5532,6 +5539,8 @@ static uint32_t inflate_resident() {
 extern "C" uint32_t sb_debug_inflate_resident() { return inflate_resident(); }
 int launch_inflate(const InflateLaunch& a, void* stream) {
   if (a.n_jobs == 0) return 0;
+  if (a.patas_wg && launch_patas(a, stream))  // Patas leaf pages that fit a workgroup's LDS: k_patas first,
+    return -1;                                // k_inflate skips them
   // A/B switches: SB_INF_STATIC=1 grid-strides the jobs, SB_INF_GRID=n caps the grid
   static const bool stat = getenv("SB_INF_STATIC") != nullptr;
   static const uint32_t gcap = getenv("SB_INF_GRID") ? (uint32_t)atoi(getenv("SB_INF_GRID")) : 0u;

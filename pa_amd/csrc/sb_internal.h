@@ -99,14 +99,35 @@ struct InflateLaunch {
   const uint64_t* bases;
   uint32_t* status;
   uint8_t* offs;  // kDstBinOffs jobs: the column's 32-bit offsets (dword-aligned)
-  uint32_t* sched;  // k_inflate's job claim counters [2], zero between launches (self-resetting), or nullptr
+  // k_inflate's job claim counters [3], zero between launches, or nullptr:
+  // [0] claims, [1] waves done (the last one out resets both), [2] jobs
+  // k_patas left to k_inflate (patas_wg: none -> k_inflate returns at once)
+  uint32_t* sched;
   uint8_t* ascii;   // binary values jobs: per page, 1 = every byte written was ASCII (else 0), or nullptr
   // the other counter pair of the plan (the next launch's): zeroed at entry,
   // so a launch that never reached its own reset cannot leave the plan's
   // next launch a stale count (the plan alternates the pairs), or nullptr
   uint32_t* sched_spare = nullptr;
+  // 1: Patas leaf jobs whose page fits a workgroup's LDS decode one
+  // workgroup a page (k_patas, launched first); k_inflate takes the rest
+  uint32_t patas_wg = 0;
 };
 int launch_inflate(const InflateLaunch& a, void* stream);
+// Patas leaf pages, one workgroup a page (k_patas, sb_patas.hip): the stream,
+// the rows and the walk tables in dynamic LDS.  Pages that do not fit
+// (patas_fits) stay with k_inflate's one-wave decoder.
+constexpr uint32_t kPatE = 10;        // entry offsets of a segment (a record is <= 10 bytes)
+constexpr uint32_t kPatLds = 155 * 1024;
+constexpr uint32_t kPatMaxRows = 8192;  // rows of a page k_patas takes (C5's and the writer's default page)
+__host__ __device__ inline uint32_t patas_lds_need(uint32_t ilen, uint32_t n, uint32_t W) {
+  const uint32_t ib = ((ilen + 62) + 15) & ~15u;  // the stream's 16-byte blocks (+ two for the tail)
+  const uint32_t refs = ((n + 1) * 2 + 15) & ~15u, sizes = (n + 1) * 2 >= ilen + 16 ? 0u : ((ilen + 16) + 15) & ~15u;
+  return ib + (((n + 1) * W + 15) & ~15u) + refs + sizes;
+}
+__host__ __device__ inline bool patas_fits(uint32_t ilen, uint32_t n, uint32_t W) {
+  return n >= 1 && n <= kPatMaxRows && ilen >= W && patas_lds_need(ilen, n, W) <= kPatLds;
+}
+int launch_patas(const InflateLaunch& a, void* stream);
 // Zstd jobs (codec 2) of the same list: one wave per frame, tables in LDS, output in HBM.
 int launch_zinflate(const InflateLaunch& a, void* stream);
 constexpr uint32_t kInflateGrid = 2048;  // 4-wave workgroups: 8 waves per SIMD on 256 CUs

@@ -19,6 +19,7 @@ tools/wlbench.py)."""
 import collections
 import csv
 import json
+import os
 import sys
 
 
@@ -55,6 +56,7 @@ def tag(names):
 
 def main():
     wl, fcsv, wcsv, bjson, out, commit = sys.argv[1:7]
+    rnd = int(sys.argv[7]) if len(sys.argv) > 7 else int(os.environ.get("SB_ROUND", "5"))
     by = json.load(open(bjson))
     f, fn = per_dispatch(fcsv, "FETCH_SIZE")
     w, wn = per_dispatch(wcsv, "WRITE_SIZE")
@@ -78,7 +80,7 @@ def main():
         step_f += fb
         step_w += wb
     alg = by["in_bytes"] + by["out_bytes"]
-    res = {"workload": wl, "commit": commit, "round": 3,
+    res = {"workload": wl, "commit": commit, "round": rnd,
            "window": f"{steps} steps between two marker launches",
            "correction": "fetch = 2 x FETCH_SIZE x 1 KiB (calibrated, profiles/r03_pmc_calibration.json); "
                          "write = WRITE_SIZE x 1 KiB",
