@@ -101,6 +101,7 @@ struct sb_plan {
   uint32_t bin_lds = 0;       // dynamic LDS of the binary kernels (the largest page need, from the plan pass)
   uint32_t zstd = 1;          // some page has a Zstd stream (0: the decode kernels without the Zstd decoder)
   uint32_t patas = 1;         // some page has a Patas stream (0: no k_patas ahead of the inflate launches)
+  uint32_t lz4like = 1;       // some page has an LZ4 / Snappy stream (k_inflate jobs beside the Patas ones)
   uint64_t values_bytes = 0;
   uint32_t n_staged = 0, n_global = 0;
   bool staged_identity = false;  // every page staged: no index list
@@ -487,6 +488,7 @@ static sb_status plan_pages(sb_ctx* ctx, const sb_column_desc* desc, const uint8
     }
     p->zstd = (flag & 1) ? 1 : 0;
     p->patas = (flag & 2) ? 1 : 0;
+    p->lz4like = (flag & 4) ? 1 : 0;
     if (is_bool && !p->zstd) p->stage_bytes = std::max<uint32_t>(max_bool_noz, 64);
   }
   if (is_bool && n_pages) {
@@ -768,7 +770,12 @@ sb_status sb_decode_planned(sb_ctx* ctx, sb_plan* p, const sb_primitive_out* out
                         (uint8_t*)out->d_values, nullptr, nullptr, p->d_status, nullptr, p->d_sched};
     sched_pair(p, I);
     static const bool no_patas_wg = getenv("SB_NO_PATAS_WG") != nullptr;  // A/B: the one-wave Patas decoder
-    I.patas_wg = p->is_float && p->patas && !no_patas_wg ? 1u : 0u;
+    // k_patas when the plan has no LZ4 / Snappy jobs: those are latency-bound
+    // one-wave jobs, and one-wave Patas jobs in the same k_inflate launch
+    // overlap them for free, where k_patas (a CU a workgroup) ahead of them
+    // adds its time, and beside them on a second stream found no CU free
+    // (C5's Float64 group with an LZ4 column: 1.39 / 1.38 vs 1.01 ms)
+    I.patas_wg = p->is_float && p->patas && !p->lz4like && !no_patas_wg ? 1u : 0u;
     if (sb::launch_inflate(I, ctx->stream))
       return fail(ctx, SB_E_DEVICE, "inflate launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (p->has_zstd_big && sb::launch_zinflate(I, ctx->stream))

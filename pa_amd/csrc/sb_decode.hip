@@ -2415,7 +2415,8 @@ __global__ __launch_bounds__(NT) void k_decode_spilled(LaunchArgs a) {
 // Plan-time cascade walk of a fixed-width (or Boolean: W 1, one stream) page
 // from HBM, the header walk of decode_page without the tables: bit 0 a Freq
 // in the cascade, bit 1 a general-codec / Patas leaf, bit 2 under a Dict /
-// Freq, bit 3 some stream of the cascade is Zstd, bit 4 some stream is Patas.
+// Freq, bit 3 some stream of the cascade is Zstd, bit 4 some stream is Patas,
+// bit 5 some stream is LZ4 / Snappy.
 __device__ uint32_t fix_cascade(const GlbSrc& s, uint32_t len, uint32_t W, int nullable) {
   uint32_t p = 0, bits = 0;
   auto hdr = [&](uint32_t q, uint32_t* codec, uint32_t* body, uint32_t* cs) {
@@ -2425,6 +2426,7 @@ __device__ uint32_t fix_cascade(const GlbSrc& s, uint32_t len, uint32_t W, int n
     *body = q + 9;
     if (*codec == 2) bits |= 8;
     if (*codec == 16) bits |= 16;
+    if (*codec == 1 || *codec == 3) bits |= 32;
     return *cs <= len - *body;
   };
   do {
@@ -2478,7 +2480,8 @@ __global__ __launch_bounds__(NT) void k_fix_probe(const uint8_t* chunk, const Pa
 
 // Plan time: *flag |= 1 when some page has a Zstd stream (the plan then
 // launches the kernels that carry the Zstd decoder), |= 2 when some page has
-// a Patas stream (the inflate launches then start with k_patas).
+// a Patas stream (the inflate launches then start with k_patas), |= 4 when
+// some page has an LZ4 / Snappy stream.
 __global__ __launch_bounds__(NT) void k_zstd_scan(const uint8_t* chunk, const PageDesc* pages, uint32_t n, uint32_t W,
                                                   int nullable, uint32_t* flag) {
   const uint32_t i = blockIdx.x * NT + threadIdx.x;
@@ -2487,7 +2490,7 @@ __global__ __launch_bounds__(NT) void k_zstd_scan(const uint8_t* chunk, const Pa
     const PageDesc pd = pages[i];
     c = fix_cascade(GlbSrc{chunk + pd.byte_off}, pd.byte_len, W, nullable);
   }
-  const uint32_t f = (__ballot(c & 8) ? 1u : 0u) | (__ballot(c & 16) ? 2u : 0u);
+  const uint32_t f = (__ballot(c & 8) ? 1u : 0u) | (__ballot(c & 16) ? 2u : 0u) | (__ballot(c & 32) ? 4u : 0u);
   if (f && (threadIdx.x & 63) == 0) atomicOr(flag, f);
 }
 

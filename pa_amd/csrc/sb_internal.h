@@ -108,8 +108,9 @@ struct InflateLaunch {
   // so a launch that never reached its own reset cannot leave the plan's
   // next launch a stale count (the plan alternates the pairs), or nullptr
   uint32_t* sched_spare = nullptr;
-  // 1: Patas leaf jobs whose page fits a workgroup's LDS decode one
-  // workgroup a page (k_patas, launched first); k_inflate takes the rest
+  // 1: Patas leaf jobs whose page fits a workgroup's LDS (patas_fits)
+  // decode one workgroup a page (k_patas, launched first on the stream; it
+  // counts k_inflate's jobs in sched[2]); k_inflate takes the rest
   uint32_t patas_wg = 0;
 };
 int launch_inflate(const InflateLaunch& a, void* stream);
@@ -117,15 +118,15 @@ int launch_inflate(const InflateLaunch& a, void* stream);
 // the rows and the walk tables in dynamic LDS.  Pages that do not fit
 // (patas_fits) stay with k_inflate's one-wave decoder.
 constexpr uint32_t kPatE = 10;        // entry offsets of a segment (a record is <= 10 bytes)
-constexpr uint32_t kPatLds = 155 * 1024;
+constexpr uint32_t kPatLds = 128 * 1024;  // (leaves a CU room for other kernels' workgroups beside it)
 constexpr uint32_t kPatMaxRows = 8192;  // rows of a page k_patas takes (C5's and the writer's default page)
 __host__ __device__ inline uint32_t patas_lds_need(uint32_t ilen, uint32_t n, uint32_t W) {
   const uint32_t ib = ((ilen + 62) + 15) & ~15u;  // the stream's 16-byte blocks (+ two for the tail)
-  const uint32_t refs = ((n + 1) * 2 + 15) & ~15u, sizes = (n + 1) * 2 >= ilen + 16 ? 0u : ((ilen + 16) + 15) & ~15u;
-  return ib + (((n + 1) * W + 15) & ~15u) + refs + sizes;
+  const uint32_t rows = (n + 1) * W > ilen + 16 ? (n + 1) * W : ilen + 16;  // (first the record size table)
+  return ib + ((rows + 15) & ~15u) + (((n + 1) * 2 + 15) & ~15u);
 }
 __host__ __device__ inline bool patas_fits(uint32_t ilen, uint32_t n, uint32_t W) {
-  return n >= 1 && n <= kPatMaxRows && ilen >= W && patas_lds_need(ilen, n, W) <= kPatLds;
+  return n >= 1 && n <= kPatMaxRows && ilen >= W && ilen <= 65535 && patas_lds_need(ilen, n, W) <= kPatLds;
 }
 int launch_patas(const InflateLaunch& a, void* stream);
 // Zstd jobs (codec 2) of the same list: one wave per frame, tables in LDS, output in HBM.

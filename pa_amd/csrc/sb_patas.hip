@@ -163,17 +163,17 @@ __device__ uint32_t patas_block(const uint8_t* src, uint32_t ilen, uint8_t* dst,
   __shared__ uint64_t s_wmap[NW];
   __shared__ uint32_t s_wsum[NW], s_err_row, s_err_code;
   // LDS: the stream (16-byte aligned window) | rows (n + 1: row n is the
-  // resolved sentinel; first the rows' record starts as u32) | references
+  // resolved sentinel; first the record size table) | references (first the
+  // rows' record starts, u16: the stream is < 64 KiB)
   const uint32_t sb0 = (uint32_t)((uintptr_t)src & 15);
   const uint32_t nb = (sb0 + ilen + 15) >> 4;           // 16-byte blocks holding the stream
   const uint32_t ib_bytes = ((ilen + 62) + 15) & ~15u;  // >= (nb + 2) * 16
+  const uint32_t rows_bytes = (max((n + 1) * W, ilen + 16) + 15) & ~15u;
   lds_u8* ib = lds;
   lds_t* vals = (lds_t*)(lds + ib_bytes);
-  lds_u32* starts = (lds_u32*)vals;
-  lds_u16* ptr = (lds_u16*)(lds + ib_bytes + (((n + 1) * W + 15) & ~15u));
-  // the record size table: in the references' area while it is free (until
-  // the terms), or after it (patas_lds_need)
-  lds_u8* sz = (n + 1) * 2 >= ilen + 16 ? (lds_u8*)ptr : (lds_u8*)ptr + (((n + 1) * 2 + 15) & ~15u);
+  lds_u8* sz = (lds_u8*)vals;
+  lds_u16* ptr = (lds_u16*)(lds + ib_bytes + rows_bytes);
+  lds_u16* starts = ptr;
 #ifdef SB_PAT_PHASES
   uint64_t tph = __builtin_amdgcn_s_memtime();
 #endif
@@ -264,7 +264,7 @@ __device__ uint32_t patas_block(const uint8_t* src, uint32_t ilen, uint8_t* dst,
     uint32_t x = s0 + entry;
     const uint32_t m = base < rows_ok ? min(cnt, rows_ok - base) : 0u;
     for (uint32_t k = 0; k < m; k++) {
-      starts[base + k] = x;
+      starts[base + k] = (uint16_t)x;
       x += sz[x];
     }
   }
@@ -381,7 +381,8 @@ __device__ uint32_t patas_block(const uint8_t* src, uint32_t ilen, uint8_t* dst,
 
 // Patas leaf jobs whose page fits (patas_fits), one workgroup each; k_inflate
 // skips them (InflateLaunch::patas_wg).
-__global__ __launch_bounds__(kPatT) void k_patas(InflateLaunch a) {
+// (three waves a SIMD's worth of VGPRs: a CU keeps room for k_inflate waves beside it)
+__global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(3))) void k_patas(InflateLaunch a) {
   extern __shared__ u32x4 pat_dyn[];
   const uint32_t n = a.count ? *a.count : a.n_jobs;
   for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
