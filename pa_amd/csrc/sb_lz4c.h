@@ -230,9 +230,29 @@ __device__ inline uint32_t lz4_wave_incl_scan(uint32_t v) {  // DPP row shifts +
 typedef __attribute__((address_space(3))) uint8_t lz4_lds8;
 constexpr uint32_t kLz4WaveLds = 16384 + 8192;  // position table + per-batch hash owners
 
+// The input of lz4_compress_wave: in HBM (a plain pointer), or staged in LDS
+// (every hash, candidate compare and match extension of the parse is a
+// dependent read: ~100 cycles from LDS instead of an L2 / HBM round trip).
+struct Lz4GSrc {
+  const uint8_t* p;
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
+  __device__ __forceinline__ uint32_t u32(uint32_t i) const { return lz4_ld32(p + i); }
+};
+struct Lz4LSrc {
+  const lz4_lds8* p;  // 4-aligned
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
+  __device__ __forceinline__ uint32_t u32(uint32_t i) const {
+    typedef const __attribute__((address_space(3))) uint32_t l32;
+    const l32* q = (const l32*)(p + (i & ~3u));
+    const uint32_t sh = i & 3, lo = q[0];
+    return sh ? __builtin_amdgcn_alignbyte(q[1], lo, sh) : lo;
+  }
+};
+
 // `lds`: kLz4WaveLds bytes, the first 16 KiB zeroed (the position table:
 // 8192 u16 below LZ4_64Klimit, 4096 u32 above), then 8 KiB of scratch.
-__device__ inline uint32_t lz4_compress_wave(const uint8_t* src, uint32_t n, uint8_t* dst, lz4_lds8* lds) {
+template <class Src>
+__device__ inline uint32_t lz4_compress_wave(const Src src, uint32_t n, uint8_t* dst, lz4_lds8* lds) {
   const uint32_t lane = threadIdx.x & 63;
   const bool u16 = n < kLz4_64Klimit;
   typedef __attribute__((address_space(3))) uint16_t l16;
@@ -248,8 +268,8 @@ __device__ inline uint32_t lz4_compress_wave(const uint8_t* src, uint32_t n, uin
     else t32[h] = v;
   };
   auto hash_at = [&](uint32_t pos) -> uint32_t {
-    if (u16) return (lz4_ld32(src + pos) * 2654435761u) >> (32 - 13);
-    const uint64_t v = (uint64_t)lz4_ld32(src + pos) | ((uint64_t)lz4_ld32(src + pos + 4) << 32);
+    if (u16) return (src.u32(pos) * 2654435761u) >> (32 - 13);
+    const uint64_t v = (uint64_t)src.u32(pos) | ((uint64_t)src.u32(pos + 4) << 32);
     return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - 12));
   };
   // the run-length bytes of len (all 255 but the last), at dst + at
@@ -259,7 +279,7 @@ __device__ inline uint32_t lz4_compress_wave(const uint8_t* src, uint32_t n, uin
     return nb;
   };
   auto copy = [&](uint32_t to, uint32_t from, uint32_t len) {
-    for (uint32_t i = lane; i < len; i += 64) dst[to + i] = src[from + i];
+    for (uint32_t i = lane; i < len; i += 64) dst[to + i] = (uint8_t)src.u8(from + i);
   };
   uint32_t op = 0, anchor = 0;
   if (n >= 13) {
@@ -281,7 +301,7 @@ __device__ inline uint32_t lz4_compress_wave(const uint8_t* src, uint32_t n, uin
         }
         const uint32_t h = hash_at(c), mi = tget(h);
         if (lane == 0) tput(h, c);
-        if ((u16 || mi + 65535 >= c) && lz4_ld32(src + mi) == lz4_ld32(src + c)) {
+        if ((u16 || mi + 65535 >= c) && src.u32(mi) == src.u32(c)) {
           mpos = c;
           mmatch = mi;
           found = true;
@@ -317,7 +337,7 @@ __device__ inline uint32_t lz4_compress_wave(const uint8_t* src, uint32_t n, uin
             todo = false;
           }
         }
-        const bool ok = live && (u16 || mi + 65535 >= pos) && lz4_ld32(src + mi) == lz4_ld32(src + q);
+        const bool ok = live && (u16 || mi + 65535 >= pos) && src.u32(mi) == src.u32(q);
         const uint64_t okm = __ballot(ok);
         const uint32_t M = okm ? (uint32_t)__builtin_ctzll(okm) : 64u;
         const uint32_t upto = min(M + 1, E);
@@ -337,7 +357,7 @@ __device__ inline uint32_t lz4_compress_wave(const uint8_t* src, uint32_t n, uin
       uint32_t ipp = mpos, mt = mmatch;
       for (;;) {  // catch up
         const uint32_t k = min(min(ipp - anchor, mt), 64u);
-        const uint64_t ne = __ballot(lane < k && src[ipp - 1 - lane] != src[mt - 1 - lane]);
+        const uint64_t ne = __ballot(lane < k && src.u8(ipp - 1 - lane) != src.u8(mt - 1 - lane));
         const uint32_t j = ne ? (uint32_t)__builtin_ctzll(ne) : k;
         ipp -= j;
         mt -= j;
@@ -363,7 +383,7 @@ __device__ inline uint32_t lz4_compress_wave(const uint8_t* src, uint32_t n, uin
         uint32_t a = ipp + 4, b = mt + 4;
         for (;;) {  // LZ4_count
           const uint32_t k = min(a < matchlimit ? matchlimit - a : 0u, 64u);
-          const uint64_t ne = __ballot(lane < k && src[a + lane] != src[b + lane]);
+          const uint64_t ne = __ballot(lane < k && src.u8(a + lane) != src.u8(b + lane));
           const uint32_t j = ne ? (uint32_t)__builtin_ctzll(ne) : k;
           a += j;
           b += j;
@@ -388,7 +408,7 @@ __device__ inline uint32_t lz4_compress_wave(const uint8_t* src, uint32_t n, uin
         const uint32_t h = hash_at(ipp);
         const uint32_t mi = tget(h);
         if (lane == 0) tput(h, ipp);
-        if ((u16 || mi + 65535 >= ipp) && lz4_ld32(src + mi) == lz4_ld32(src + ipp)) {
+        if ((u16 || mi + 65535 >= ipp) && src.u32(mi) == src.u32(ipp)) {
           mt = mi;
           tpos = op++;
           token = 0;

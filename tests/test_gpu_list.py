@@ -176,3 +176,35 @@ def test_list_malformed_pages(ctx):
             gpu_list(ctx, page, [(len(page), nl)], np.int32, False, False)
         with pytest.raises(O.OracleError):
             O.read_list_column(page, [(len(page), nl)], np.int32, False, False)
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.float64, np.uint8], ids=lambda d: np.dtype(d).name)
+def test_list_mixed_none_and_cascade_pages(ctx, dtype):
+    """Pages whose values stream is None (the levels pass copies them and
+    marks them done for the values plan) next to pages the values plan
+    decodes (Dict, LZ4, Bitpacking), in one column, odd page sizes so the
+    values start at every alignment."""
+    rng = np.random.default_rng(31)
+    opts = [O.WriteOptions.make(), O.WriteOptions.make(ratio=2.0, forced=O.DICT),
+            O.WriteOptions.make(default_codec=O.LZ4), O.WriteOptions.make(ratio=2.0, forced=O.BITPACKING)]
+    chunks, metas = [], []
+    for k, op in enumerate(opts * 2):
+        offs, lv, child, cv = make_lists(3000 + 37 * k, rng, dtype=dtype, vmax=200)
+        if k % 4 == 3 and dtype == np.float64:
+            op = O.WriteOptions.make()
+        ch, me, _ = O.write_list_column(offs, lv, child, cv, True, True, 1001 + 2 * k, op)
+        chunks.append(ch)
+        metas += list(me)
+    chunk = b"".join(chunks)
+    eo, el, ev, ef = O.read_list_column(chunk, metas, np.dtype(dtype), True, True)
+    go, gl, gv, gf = gpu_list(ctx, chunk, metas, np.dtype(dtype), True, True)
+    assert (go == eo).all() and (gl == el).all() and (gf == ef).all()
+    assert gv.tobytes() == ev.tobytes()
+    # and decoded twice from one plan (the done marks are per decode)
+    import pa_amd
+
+    dec = pa_amd.ListColumnDecoder(chunk, [pa_amd.PageMeta(l, n) for l, n in metas], np.dtype(dtype), True, True, ctx)
+    for _ in range(2):
+        _, _, vals, _ = dec.decode()
+        assert vals.cpu().numpy().view(np.uint8)[: len(ev) * np.dtype(dtype).itemsize].tobytes() == ev.tobytes()
+    dec.close()
