@@ -395,6 +395,26 @@ sb_status sb_encode_binary_column_device(sb_ctx* ctx, int32_t physical_type, con
                                          uint64_t max_page_rows, uint8_t* d_out, uint64_t out_capacity,
                                          uint64_t* out_len, sb_page_meta* h_metas, uint64_t metas_cap,
                                          uint64_t* n_pages);
+/* encode_chunk for one List<primitive> leaf on the device (write/common.rs:
+ * 49-119 with slice_parquet_array per page, write_nested serialize.rs:133-146),
+ * byte-identical to sb_encode_list_column with the same options: per page of
+ * max_page_rows (<= 16384) top-level rows, the rep / def level streams (one
+ * bit-packed hybrid run each) and the sliced child values through the device
+ * cascade (sb_encode_column_device's page kernels; the child validity feeds
+ * the statistics, no validity prefix).  d_offsets = n_rows + 1 absolute int64
+ * positions into d_child; d_list_validity over the rows, d_child_validity over
+ * the child values (device LSB bitmaps).  d_out holds at least
+ * sb_encode_list_device_bound(.., n_child = d_offsets[n_rows] - d_offsets[0],
+ * ..) bytes; PageMeta.num_values = the page's level count.  Synchronizes the
+ * context's stream. */
+uint64_t sb_encode_list_device_bound(int32_t physical_type, uint64_t n_rows, uint64_t n_child, int32_t item_nullable,
+                                     uint64_t max_page_rows);
+sb_status sb_encode_list_column_device(sb_ctx* ctx, int32_t physical_type, const int64_t* d_offsets,
+                                       const uint8_t* d_list_validity, int32_t list_nullable, const void* d_child,
+                                       const uint8_t* d_child_validity, int32_t item_nullable, uint64_t n_rows,
+                                       const sb_write_options* opts, uint64_t max_page_rows, uint8_t* d_out,
+                                       uint64_t out_capacity, uint64_t* out_len, sb_page_meta* h_metas,
+                                       uint64_t metas_cap, uint64_t* n_pages);
 /* NativeWriter::finish (write/writer.rs:128-167) footer bytes. */
 sb_status sb_write_footer(const uint8_t* h_schema, uint64_t schema_len, const uint64_t* h_col_offsets,
                           const uint64_t* h_col_npages, uint64_t n_cols, const sb_page_meta* h_pages,

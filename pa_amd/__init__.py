@@ -22,6 +22,6 @@ from .binary import (  # noqa: F401,E402
     encode_binary_column_device,
 )
 from .nested import (DeviceArray, Field, FieldDecoder, ListColumnDecoder, NestedColumnDecoder,  # noqa: F401,E402
-                     batch_read_field, batch_read_list, encode_list_column)
+                     batch_read_field, batch_read_list, encode_list_column, encode_list_column_device)
 from .file import Leaf, StrawboatFile, parse_schema  # noqa: F401,E402
 from .table import ColumnGroupDecoder  # noqa: F401,E402

@@ -32,6 +32,7 @@ EXPORTED = [
     "sb_plan_nested_count", "sb_decode_nested_planned", "sb_parse_schema", "sb_file_open", "sb_file_close",
     "sb_file_last_error", "sb_file_num_columns", "sb_file_column", "sb_file_schema", "sb_file_upload",
     "sb_decode_page_validity", "sb_decode_page_levels", "sb_plan_column_at",
+    "sb_encode_list_device_bound", "sb_encode_list_column_device",
 ]
 
 MAX_NEST = 4
@@ -152,6 +153,12 @@ def lib():
     L.sb_encode_column_device.argtypes = [P, I32, P, P, U64, I32, ctypes.POINTER(WriteOptionsC), U64, P, U64,
                                           ctypes.POINTER(U64), ctypes.POINTER(PageMetaC), U64, ctypes.POINTER(U64)]
     L.sb_encode_column_device.restype = I32
+    L.sb_encode_list_device_bound.argtypes = [I32, U64, U64, I32, U64]
+    L.sb_encode_list_device_bound.restype = U64
+    L.sb_encode_list_column_device.argtypes = [P, I32, P, P, I32, P, P, I32, U64, ctypes.POINTER(WriteOptionsC), U64,
+                                               P, U64, ctypes.POINTER(U64), ctypes.POINTER(PageMetaC), U64,
+                                               ctypes.POINTER(U64)]
+    L.sb_encode_list_column_device.restype = I32
     L.sb_page_seed.argtypes = [U64, U64]
     L.sb_page_seed.restype = U64
     L.sb_write_footer.argtypes = [P, U64, P, P, U64, P, PU8, ctypes.POINTER(U64)]

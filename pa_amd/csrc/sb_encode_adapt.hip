@@ -1148,7 +1148,34 @@ struct AdArgs {
   uint64_t parent_len;      // the array's whole values length (stats and the Extend header)
   int ow;                   // offset width 4 / 8
   const uint64_t* slot_offs;  // per page of the batch: slot start (variable slots), [n_batch] = end
+  // List values (sb_encode_list_column_device): page p holds the child values
+  // [rows_at[p], rows_at[p + 1]) and starts with its level header (heads + p *
+  // head_slot, head_len[p] bytes) in place of a validity prefix
+  const uint64_t* rows_at = nullptr;
+  const uint8_t* heads = nullptr;
+  uint64_t head_slot = 0;
+  const uint32_t* head_len = nullptr;
 };
+
+// Page p's rows: [p * P, min((p + 1) * P, n_rows)), or a List page's child values
+__device__ __forceinline__ void page_rows(const AdArgs& A, uint32_t p, uint64_t* r0, uint32_t* n) {
+  if (A.rows_at) {
+    *r0 = A.rows_at[p];
+    *n = (uint32_t)(A.rows_at[p + 1] - *r0);
+  } else {
+    *r0 = (uint64_t)p * A.P;
+    *n = (uint32_t)min<uint64_t>(A.P, A.n_rows - *r0);
+  }
+}
+
+// A List page's level header, copied to the page's start by the threads of
+// `nt`; returns its length
+__device__ __forceinline__ uint32_t put_head(const AdArgs& A, uint32_t p, uint8_t* out, uint32_t nt) {
+  const uint32_t hl = A.head_len[p];
+  const uint8_t* h = A.heads + (uint64_t)p * A.head_slot;
+  for (uint32_t j = threadIdx.x; j < hl; j += nt) out[j] = h[j];
+  return hl;
+}
 
 __device__ __forceinline__ uint8_t* slot_of(const AdArgs& A, uint32_t b) {
   return A.slot_offs ? A.slots + A.slot_offs[b] : A.slots + (uint64_t)b * A.slot_bytes;
@@ -1333,13 +1360,14 @@ __global__ __launch_bounds__(NT) void k_enc_adaptive(AdArgs A) {
   __shared__ Sh sh;
   const uint32_t tid = threadIdx.x;
   const uint32_t p = A.page0 + blockIdx.x;
-  const uint64_t r0 = (uint64_t)p * A.P;
-  const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
+  uint64_t r0;
+  uint32_t n;
+  page_rows(A, p, &r0, &n);
   Ctx c;
   ctx_init(c, sh, A, p);
   set_work(c, A, lds);
   const bool has_vb = A.nullable && A.validity;
-  uint32_t pos = write_prefix(c, A, r0, n);
+  uint32_t pos = A.heads ? put_head(A, p, c.out, NT) : write_prefix(c, A, r0, n);
   const Av a{A.values + r0 * W, has_vb ? A.validity : nullptr, r0, n};
   __syncthreads();
   pos = enc_stream<W, FLT, SGN, 0, ZS>(c, sh, a, A.o.forbidden, pos);
@@ -1368,15 +1396,19 @@ __global__ __launch_bounds__(64) void k_enc_basic_wave(AdArgs A) {
   extern __shared__ uint32_t lds[];
   const uint32_t lane = threadIdx.x;
   const uint32_t p = A.page0 + blockIdx.x;
-  const uint64_t r0 = (uint64_t)p * A.P;
-  const uint32_t n = (uint32_t)min<uint64_t>(A.P, A.n_rows - r0);
+  uint64_t r0;
+  uint32_t n;
+  page_rows(A, p, &r0, &n);
   uint8_t* out = slot_of(A, blockIdx.x);
   const uint64_t cap = slot_cap(A, blockIdx.x);
   const int codec = A.o.dflt;
   sbc::lz4_lds8* tab = (sbc::lz4_lds8*)lds;
   uint32_t err = E_OK;
   uint32_t pos = 0;
-  if (A.nullable) {  // write_prefix (serialize.rs:200-215), one wave
+  if (A.heads) {  // a List page: its level header (no validity prefix)
+    pos = put_head(A, p, out, 64);
+    __threadfence_block();
+  } else if (A.nullable) {  // write_prefix (serialize.rs:200-215), one wave
     const uint32_t nb = (n + 7) / 8;
     uint64_t h = ((uint64_t)nb << 1) | 1;
     const uint32_t hl = uleb_len(h);
@@ -1819,6 +1851,116 @@ __global__ __launch_bounds__(NT) void k_enc_compact(AdArgs A) {
   for (uint64_t j = head + body * 16 + threadIdx.x; j < len; j += NT) dst[j] = src[j];
 }
 
+// ---------------------------------------------------------------------------
+// List<primitive> pages (write_nested, serialize.rs:133-146; RepLevelsIter /
+// DefLevelsIter of one list level, nested/rep.rs, nested/def.rs): one
+// workgroup per page of `step` top-level rows writes the page's level header
+// -- [rows u32][rep_len u32][def_len u32][rep stream][def stream], each
+// stream one bit-packed hybrid run: ULEB128((ceil(L / 8) << 1) | 1), then
+// ceil(L * bw / 8) bytes of 32-level chunks.  The writer packs the last,
+// partial chunk from its reused 32-value buffer, so the spare bits of its
+// last byte hold level i - 32 (zero when there is no earlier chunk): the
+// host writer's encode_levels_u32 (sb_encode.cpp), bit for bit.  A row is
+// one level (rep 0) when the list is null (def 0) or empty (def nl), else
+// one per item (rep 0 for the first, 1 after; def max_def, or max_def - 1
+// under a null item).  LDS: the rows' level prefix (dynamic, rows + 1 u32).
+// ---------------------------------------------------------------------------
+struct ListLv {
+  const int64_t* offsets;   // n_rows + 1 absolute child positions
+  const uint8_t* lvalid;    // list validity (rows) or nullptr
+  const uint8_t* cvalid;    // child validity (child values) or nullptr
+  uint64_t n_rows;
+  uint32_t step, nl, ni;
+  uint8_t* heads;           // page p's header at heads + p * head_slot
+  uint64_t head_slot;
+  uint32_t* head_len;
+  uint64_t* levels;         // [n_pages] level counts (PageMeta.num_values)
+};
+
+__device__ __forceinline__ bool bit_at(const uint8_t* bm, uint64_t i) { return (bm[i >> 3] >> (i & 7)) & 1; }
+
+__global__ __launch_bounds__(NT) void k_enc_list_levels(ListLv a) {
+  extern __shared__ uint32_t lpre[];  // [m + 1]: the rows' first level
+  __shared__ uint32_t s_red[NW];
+  const uint32_t p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t r0 = (uint64_t)p * a.step;
+  const uint32_t m = (uint32_t)min<uint64_t>(a.step, a.n_rows - r0);
+  const uint32_t max_def = a.nl + 1 + a.ni, bwd = 32 - __clz(max_def);
+  auto row_levels = [&](uint32_t r) -> uint32_t {
+    if (a.nl && a.lvalid && !bit_at(a.lvalid, r0 + r)) return 1u;
+    const int64_t len = a.offsets[r0 + r + 1] - a.offsets[r0 + r];
+    return len > 0 ? (uint32_t)len : 1u;
+  };
+  // 1. the level prefix over the rows (chunks of consecutive rows per thread)
+  const uint32_t ch = (m + NT - 1) / NT, b0 = min(m, tid * ch), b1 = min(m, b0 + ch);
+  uint32_t sum = 0;
+  for (uint32_t r = b0; r < b1; r++) sum += row_levels(r);
+  uint32_t x = sum;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_red[wv] = x;
+  __syncthreads();
+  uint32_t pre = x - sum, L = 0;
+  for (uint32_t k = 0; k < NW; k++) {
+    pre += k < wv ? s_red[k] : 0u;
+    L += s_red[k];
+  }
+  for (uint32_t r = b0; r < b1; r++) {
+    lpre[r] = pre;
+    pre += row_levels(r);
+  }
+  if (tid == 0) lpre[m] = L;
+  __syncthreads();
+  // level i's (rep, def); the spare bits past L hold level i - 32 (or 0)
+  auto level = [&](uint32_t i) -> uint32_t {  // rep | def << 1
+    if (i >= L) {
+      if (i < 32) return 0u;
+      i -= 32;
+    }
+    uint32_t lo = 0, hi = m;  // the last row with lpre[row] <= i
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (lpre[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t j = i - lpre[lo];
+    if (a.nl && a.lvalid && !bit_at(a.lvalid, r0 + lo)) return 0u;
+    const int64_t b = a.offsets[r0 + lo], len = a.offsets[r0 + lo + 1] - b;
+    if (len <= 0) return a.nl << 1;
+    const uint32_t def = a.ni ? (!a.cvalid || bit_at(a.cvalid, (uint64_t)b + j) ? max_def : max_def - 1) : max_def;
+    return (j > 0 ? 1u : 0u) | (def << 1);
+  };
+  uint64_t h = ((uint64_t)((L + 7) / 8) << 1) | 1;
+  uint32_t hl = 1;
+  for (uint64_t t = h; t >= 0x80; t >>= 7) hl++;
+  const uint32_t rb = (L + 7) / 8, db = (L * bwd + 7) / 8;
+  uint8_t* out = a.heads + (uint64_t)p * a.head_slot;
+  if (tid == 0) {
+    const uint32_t w[3] = {m, hl + rb, hl + db};
+    for (uint32_t k = 0; k < 12; k++) out[k] = (uint8_t)(w[k / 4] >> (8 * (k % 4)));
+    for (uint32_t k = 0; k < hl; k++) {
+      const uint8_t c = (uint8_t)((h >> (7 * k)) & 0x7F) | (k + 1 < hl ? 0x80 : 0);
+      out[12 + k] = c;
+      out[12 + hl + rb + k] = c;
+    }
+    a.head_len[p] = 12 + 2 * hl + rb + db;
+    a.levels[p] = L;
+  }
+  for (uint32_t k = tid; k < rb; k += NT) {  // rep: 8 levels a byte
+    uint32_t v = 0;
+    for (uint32_t b = 0; b < 8; b++) v |= (level(8 * k + b) & 1u) << b;
+    out[12 + hl + k] = (uint8_t)v;
+  }
+  const uint32_t per = 8 / bwd;
+  for (uint32_t k = tid; k < db; k += NT) {  // def: 8 / bw levels a byte
+    uint32_t v = 0;
+    for (uint32_t b = 0; b < per; b++) v |= (level(per * k + b) >> 1) << (b * bwd);
+    out[12 + 2 * hl + rb + k] = (uint8_t)v;
+  }
+}
+
 }  // namespace sba
 
 // ===========================================================================
@@ -1918,9 +2060,18 @@ static void launch_bin(const sba::AdArgs& a, uint32_t lds, hipStream_t st) {
 }
 
 // Encodes every page of a fixed-width column; returns SB status.
+// List pages (encode_list_device): each page's child-value range and level header
+struct ListPart {
+  const uint64_t* rows_at;  // device [np + 1]
+  const uint8_t* heads;
+  uint64_t head_slot;
+  const uint32_t* head_len;
+  const uint64_t* h_levels;  // host [np]: PageMeta.num_values
+};
+
 int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_t* d_validity, uint64_t n_rows,
                     int nullable, const sb_write_options* opts, uint64_t P, uint8_t* d_out, uint64_t out_cap,
-                    uint64_t* out_len, sb_page_meta* h_metas, uint64_t np) {
+                    uint64_t* out_len, sb_page_meta* h_metas, uint64_t np, const ListPart* lp) {
   sba::Opts o{opts->default_codec, opts->has_ratio, opts->ratio, opts->forbidden_mask, opts->forced_codec};
   uint32_t w = 0;
   bool flt = false, sgn = false;
@@ -1945,7 +2096,8 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
   const bool stats = sba::needs_stats(o, o.forbidden);
   const bool big = P > sba::kMaxRows;
   if (big && (P * w > 0xFFFFFFF0ull || P > 0x7FFFFFFFull)) return SB_E_NYI;
-  const uint64_t slot = adaptive_slot_bytes(P, w, nullable);
+  if (lp && phys == SB_T_BOOLEAN) return SB_E_NYI;
+  const uint64_t slot = adaptive_slot_bytes(P, w, lp ? 0 : nullable) + (lp ? lp->head_slot : 0);
   const uint64_t scr = is_bool ? 256 : ((P > 65535 ? 3 : 2) * P * 8 + 255) & ~255ull;  // (wide: roaring rows, level 2)
   const uint64_t gwb = !big ? 0 : is_bool ? sba::bool_work_bytes(P) : big_work_bytes(P, stats);
   const uint32_t batch = batch_pages(np, slot + scr + gwb);
@@ -1968,6 +2120,12 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
     sba::AdArgs a{d_values, d_validity, n_rows, (uint32_t)P, (uint32_t)b0, (uint32_t)std::min<uint64_t>(batch, np - b0),
                   nullable, o, opts->seed, slots, slot, scratch, scr, work, gwork, gwb, sizes, status, offs, d_out, out_cap,
                   (uint32_t)np, nullptr, 0, 0, nullptr};
+    if (lp) {
+      a.rows_at = lp->rows_at;
+      a.heads = lp->heads;
+      a.head_slot = lp->head_slot;
+      a.head_len = lp->head_len;
+    }
     if (is_bool) {
       if (o.dflt == sba::C_ZSTD) {
         ensure_lds_attr(sba::k_enc_bool<true>, (int)lds);
@@ -2007,8 +2165,77 @@ int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_
     if (stv[p]) return SB_E_OUT_OF_SPEC;
   }
   *out_len = sz[np + np];
-  for (uint64_t p = 0; p < np; p++) h_metas[p] = sb_page_meta{sz[p], std::min<uint64_t>(P, n_rows - p * P)};
+  for (uint64_t p = 0; p < np; p++)
+    h_metas[p] = sb_page_meta{sz[p], lp ? lp->h_levels[p] : std::min<uint64_t>(P, n_rows - p * P)};
   return SB_OK;
+}
+
+// encode_chunk of one List<primitive> leaf on the device (write/common.rs:
+// 49-119 with slice_parquet_array per page of `step` top-level rows,
+// write_nested serialize.rs:133-146): the level headers (k_enc_list_levels),
+// then each page's child values through the adaptive page kernels (the
+// writer's compress_* over the sliced child array: its validity feeds the
+// statistics, no prefix) behind its header.  Byte-identical to
+// sb_encode_list_column.
+__global__ void k_list_rows_at(const int64_t* offs, uint64_t n_rows, uint64_t step, uint64_t np, uint64_t* out) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p <= np) out[p] = (uint64_t)offs[std::min<uint64_t>(p * step, n_rows)];
+}
+
+int encode_list_device(sb_ctx* ctx, int phys, const int64_t* d_offsets, const uint8_t* d_list_validity,
+                       int list_nullable, const void* d_child, const uint8_t* d_child_validity, int item_nullable,
+                       uint64_t n_rows, const sb_write_options* opts, uint64_t step, uint8_t* d_out, uint64_t out_cap,
+                       uint64_t* out_len, sb_page_meta* h_metas, uint64_t np) {
+  hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
+  uint64_t* d_rows_at = nullptr;
+  uint8_t* d_heads = nullptr;
+  uint32_t* d_hlen = nullptr;
+  uint64_t* d_levels = nullptr;
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(st);
+    if (d_rows_at) (void)hipFree(d_rows_at);
+    if (d_heads) (void)hipFree(d_heads);
+    if (d_hlen) (void)hipFree(d_hlen);
+    if (d_levels) (void)hipFree(d_levels);
+  };
+  std::vector<uint64_t> rows_at(np + 1), levels(np);
+  if (hipMalloc(&d_rows_at, (np + 1) * 8) != hipSuccess || hipMalloc(&d_hlen, np * 4) != hipSuccess ||
+      hipMalloc(&d_levels, np * 8) != hipSuccess) {
+    cleanup();
+    return ctx_fail(ctx, SB_E_DEVICE, "device list encode alloc");
+  }
+  hipLaunchKernelGGL(k_list_rows_at, dim3((uint32_t)((np + 256) / 256)), dim3(256), 0, st, d_offsets, n_rows, step, np,
+                     d_rows_at);
+  if (hipMemcpyAsync(rows_at.data(), d_rows_at, (np + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    cleanup();
+    return ctx_fail(ctx, SB_E_DEVICE, "device list encode step 1");
+  }
+  uint64_t P = 1;
+  for (uint64_t q = 0; q < np; q++) P = std::max<uint64_t>(P, rows_at[q + 1] - rows_at[q]);
+  // a page's levels: <= rows + values; header: 12 + two ULEB128 runs + the packed levels
+  const uint64_t lmax = step + P;
+  const uint64_t head_slot = (12 + 2 * 10 + (lmax + 7) / 8 + (2 * lmax + 7) / 8 + 15) & ~15ull;
+  if (hipMalloc(&d_heads, np * head_slot) != hipSuccess) {
+    cleanup();
+    return ctx_fail(ctx, SB_E_DEVICE, "device list encode alloc");
+  }
+  sba::ListLv L{d_offsets, list_nullable ? d_list_validity : nullptr, item_nullable ? d_child_validity : nullptr,
+                n_rows, (uint32_t)step, list_nullable ? 1u : 0u, item_nullable ? 1u : 0u, d_heads, head_slot, d_hlen,
+                d_levels};
+  const uint32_t lds = (uint32_t)((step + 1) * 4);
+  ensure_lds_attr(sba::k_enc_list_levels, (int)lds);
+  hipLaunchKernelGGL(sba::k_enc_list_levels, dim3((uint32_t)np), dim3(sba::NT), lds, st, L);
+  if (hipMemcpyAsync(levels.data(), d_levels, np * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    cleanup();
+    return ctx_fail(ctx, SB_E_DEVICE, "device list encode step 2");
+  }
+  const ListPart lp{d_rows_at, d_heads, head_slot, d_hlen, levels.data()};
+  const int rc = encode_adaptive(ctx, phys, (const uint8_t*)d_child, item_nullable ? d_child_validity : nullptr,
+                                 rows_at[np], item_nullable, opts, P, d_out, out_cap, out_len, h_metas, np, &lp);
+  cleanup();
+  return rc;
 }
 
 

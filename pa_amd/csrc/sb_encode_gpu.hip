@@ -250,10 +250,15 @@ static uint32_t type_width(int32_t t) {
 }
 
 namespace sb {
+struct ListPart;
 uint64_t adaptive_slot_bytes(uint64_t P, uint32_t w, int nullable);
 int encode_adaptive(sb_ctx* ctx, int phys, const uint8_t* d_values, const uint8_t* d_validity, uint64_t n_rows,
                     int nullable, const sb_write_options* opts, uint64_t P, uint8_t* d_out, uint64_t out_cap,
-                    uint64_t* out_len, sb_page_meta* h_metas, uint64_t np);
+                    uint64_t* out_len, sb_page_meta* h_metas, uint64_t np, const ListPart* lp);
+int encode_list_device(sb_ctx* ctx, int phys, const int64_t* d_offsets, const uint8_t* d_list_validity,
+                       int list_nullable, const void* d_child, const uint8_t* d_child_validity, int item_nullable,
+                       uint64_t n_rows, const sb_write_options* opts, uint64_t step, uint8_t* d_out, uint64_t out_cap,
+                       uint64_t* out_len, sb_page_meta* h_metas, uint64_t np);
 }  // namespace sb
 
 extern "C" uint64_t sb_encode_device_bound(int32_t physical_type, uint64_t n_rows, int32_t nullable,
@@ -294,7 +299,7 @@ extern "C" sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type,
   if (is_bool || opts->has_ratio || opts->default_codec != SB_CODEC_NONE || forced_other || P > sbe::kMaxPageRows ||
       (P % 128 && P < n_rows) || 2 * P * w + 8192 > sbe::kLds)
     return (sb_status)sb::encode_adaptive(ctx, physical_type, (const uint8_t*)d_values, d_validity, n_rows, nullable,
-                                          opts, P, d_out, out_capacity, out_len, h_metas, np);
+                                          opts, P, d_out, out_capacity, out_len, h_metas, np, nullptr);
   if (out_capacity < sb_encode_device_bound(physical_type, n_rows, nullable, P)) return SB_E_ARG;
   hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
   const bool bp = forced_bp && (physical_type == SB_T_INT32 || physical_type == SB_T_UINT32);
@@ -326,4 +331,40 @@ extern "C" sb_status sb_encode_column_device(sb_ctx* ctx, int32_t physical_type,
   if (e != hipSuccess) return SB_E_DEVICE;
   for (uint64_t p = 0; p < np; p++) h_metas[p] = sb_page_meta{sz[p], std::min<uint64_t>(P, n_rows - p * P)};
   return SB_OK;
+}
+
+// encode_chunk for one List<primitive> leaf on the device
+// (include/strawboat_gpu.h; byte-identical to sb_encode_list_column).
+extern "C" uint64_t sb_encode_list_device_bound(int32_t physical_type, uint64_t n_rows, uint64_t n_child,
+                                                int32_t item_nullable, uint64_t max_page_rows) {
+  const uint64_t w = type_width(physical_type);
+  const uint64_t P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
+  if (!w || !P) return 0;
+  const uint64_t pages = (n_rows + P - 1) / P, vmax = std::max<uint64_t>(n_child, 1);
+  // per page: the level header (<= 12 + 20 + (rows + values) * 3 / 8) + the child values' page
+  return pages * (((12 + 20 + (P + vmax) * 3 / 8 + 16 + 15) & ~15ull) + sb::adaptive_slot_bytes(vmax, (uint32_t)w, 0));
+}
+
+extern "C" sb_status sb_encode_list_column_device(sb_ctx* ctx, int32_t physical_type, const int64_t* d_offsets,
+                                                  const uint8_t* d_list_validity, int32_t list_nullable,
+                                                  const void* d_child, const uint8_t* d_child_validity,
+                                                  int32_t item_nullable, uint64_t n_rows,
+                                                  const sb_write_options* opts, uint64_t max_page_rows, uint8_t* d_out,
+                                                  uint64_t out_capacity, uint64_t* out_len, sb_page_meta* h_metas,
+                                                  uint64_t metas_cap, uint64_t* n_pages) {
+  if (!ctx || !opts || !out_len || !n_pages || !d_offsets) return SB_E_ARG;
+  if (!type_width(physical_type)) return SB_E_NYI;
+  if ((list_nullable && !d_list_validity) || (item_nullable && !d_child_validity) || (n_rows && !d_out))
+    return SB_E_ARG;
+  const uint64_t step = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
+  const uint64_t np = step ? (n_rows + step - 1) / step : 0;
+  *n_pages = np;
+  if (np > metas_cap || (h_metas == nullptr && np)) return SB_E_ARG;
+  *out_len = 0;
+  if (!np) return SB_OK;
+  if (step > sbe::kMaxPageRows) return SB_E_NYI;  // (the level prefix of a page lives in LDS)
+  if (hipSetDevice(sb_ctx_device(ctx)) != hipSuccess) return SB_E_DEVICE;
+  return (sb_status)sb::encode_list_device(ctx, physical_type, d_offsets, d_list_validity, list_nullable, d_child,
+                                           d_child_validity, item_nullable, n_rows, opts, step, d_out, out_capacity,
+                                           out_len, h_metas, np);
 }

@@ -90,6 +90,64 @@ def encode_list_column(offsets: np.ndarray, child: np.ndarray, list_validity=Non
     return _take(out, olen.value), pm
 
 
+def encode_list_column_device(offsets, child, list_validity=None, child_validity=None, list_nullable: bool = False,
+                              item_nullable: bool = False, options=None, ctx=None):
+    """encode_chunk for one List<T> leaf on the GPU
+    (sb_encode_list_column_device): offsets (n + 1 absolute int64
+    positions), child, list_validity (over the rows) and child_validity (over
+    the child values) are device tensors; returns (device uint8 tensor of the
+    column chunk, page metas), byte-identical to encode_list_column with the
+    same options."""
+    import torch
+
+    from .read import resolve_context
+    from .write import WriteOptions
+
+    L = _lib()
+    options = options or WriteOptions()
+    ctx = resolve_context(ctx, child)
+    offs = offsets.to(torch.int64).contiguous()
+    child = child.contiguous()
+    n = offs.numel() - 1
+    tdt = {torch.int8: np.int8, torch.int16: np.int16, torch.int32: np.int32, torch.int64: np.int64,
+           torch.uint8: np.uint8, torch.uint16: np.uint16, torch.uint32: np.uint32, torch.uint64: np.uint64,
+           torch.float32: np.float32, torch.float64: np.float64}[child.dtype]
+    phys = physical_type(np.dtype(tdt))
+
+    def pack(bits, m):  # bool device tensor -> LSB-first bitmap bytes (at least one byte)
+        bits = bits.to(device=child.device, dtype=torch.bool).reshape(-1)
+        pad = (-m) % 8
+        if pad:
+            bits = torch.cat([bits, torch.zeros(pad, dtype=torch.bool, device=bits.device)])
+        if not m:
+            return torch.zeros(1, dtype=torch.uint8, device=child.device)
+        w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=child.device)
+        return (bits.view(-1, 8).to(torch.uint8) * w).sum(1, dtype=torch.uint8)
+
+    nc = child.numel()
+    lvb = pack(list_validity if list_validity is not None else torch.ones(n, dtype=torch.bool), n) \
+        if list_nullable else None
+    cvb = pack(child_validity if child_validity is not None else torch.ones(nc, dtype=torch.bool), nc) \
+        if item_nullable else None
+    if nc == 0:
+        child = torch.zeros(1, dtype=child.dtype, device=child.device)
+    P = min(options.max_page_size or n, n)
+    n_child = int(offs[-1].item() - offs[0].item()) if n else 0
+    cap = L.sb_encode_list_device_bound(phys, n, n_child, int(item_nullable), P)
+    out = torch.empty(max(cap, 16), dtype=torch.uint8, device=child.device)
+    npages = (n + P - 1) // P if n else 0
+    metas = (N.PageMetaC * max(npages, 1))()
+    olen, npg = ctypes.c_uint64(), ctypes.c_uint64()
+    opts = options.c()
+    vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = L.sb_encode_list_column_device(ctx._h, phys, vp(offs), vp(lvb), int(list_nullable), vp(child), vp(cvb),
+                                        int(item_nullable), n, ctypes.byref(opts), P, vp(out), out.numel(),
+                                        ctypes.byref(olen), metas, max(npages, 1), ctypes.byref(npg))
+    if st:
+        raise N.StrawboatError(st, "encode_list_column_device: " + ctx.error())
+    return out[: olen.value], [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
+
+
 class ListColumnDecoder:
     """A planned List<T> column chunk: rows and leaves are sized on the device
     at plan time; decode() re-runs the sizing pass, the levels pass and the

@@ -113,6 +113,14 @@ extern "C" {
                                           max_page_rows: u64, d_out: *mut u8, out_capacity: u64,
                                           out_len: *mut u64, metas: *mut sb_page_meta, metas_cap: u64,
                                           n_pages: *mut u64) -> i32;
+    pub fn sb_encode_list_device_bound(physical_type: i32, n_rows: u64, n_child: u64, item_nullable: i32,
+                                       max_page_rows: u64) -> u64;
+    pub fn sb_encode_list_column_device(ctx: *mut sb_ctx, physical_type: i32, d_offsets: *const i64,
+                                        d_list_validity: *const u8, list_nullable: i32, d_child: *const c_void,
+                                        d_child_validity: *const u8, item_nullable: i32, n_rows: u64,
+                                        opts: *const sb_write_options, max_page_rows: u64, d_out: *mut u8,
+                                        out_capacity: u64, out_len: *mut u64, metas: *mut sb_page_meta,
+                                        metas_cap: u64, n_pages: *mut u64) -> i32;
     pub fn sb_encode_page(physical_type: i32, values: *const c_void, validity: *const u8, n: u64,
                           nullable: i32, opts: *const sb_write_options, seed: u64, out: *mut *mut u8,
                           out_len: *mut u64) -> i32;
