@@ -293,8 +293,46 @@ def encode_gpu(torch, pa, rows: int, device: int, threads: int, steps: int) -> d
                      "encoded_bytes": len(host), "host_writer_GBps": round(v.nbytes / th / 1e9, 2),
                      "host_threads": threads, "byte_identical_to_host": bool(ok)}
         del tv, chunk, dout
+    out["c4_list_int32_adaptive_ratio1.2"] = encode_list_gpu(torch, pa, rows // 2, device, threads, steps)
     out["zstd_size_vs_libzstd3"] = zstd_size(torch, pa, device, threads)
     return out
+
+
+def encode_list_gpu(torch, pa, rows: int, device: int, threads: int, steps: int) -> dict:
+    """Device List encode (sb_encode_list_column_device) of a C4-shaped
+    column (List<Int32>, nullable lists and items, lengths in {0, 1, 2},
+    ratio 1.2, 8192-row pages): level headers and child values on the GPU,
+    byte for byte against the host writer (sb_encode_list_column); input
+    GB/s = offsets + child values + both bitmaps per call."""
+    rng = np.random.default_rng(11)
+    lens = rng.integers(0, 3, rows)
+    lv = rng.random(rows) >= 0.1
+    lens[~lv] = 0
+    offs = np.zeros(rows + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    child = rng.integers(0, 1 << 16, int(offs[-1])).astype(np.int32)
+    cv = rng.random(len(child)) >= 0.2
+    opts = pa.WriteOptions(default_compress_ratio=1.2, max_page_size=PAGE_ROWS, seed=7)
+    t0 = time.perf_counter()
+    host, hm = pa.encode_list_column(offs, child, lv, cv, True, True, opts, n_threads=threads)
+    th = time.perf_counter() - t0
+    dev = lambda a: torch.from_numpy(a).to(f"cuda:{device}")  # noqa: E731
+    do, dc, dl, dv = dev(offs), dev(child), dev(lv), dev(cv)
+    chunk, dm = pa.encode_list_column_device(do, dc, dl, dv, True, True, opts)
+    ok = chunk.cpu().numpy().tobytes() == bytes(host) and [(m.length, m.num_values) for m in dm] == \
+        [(m.length, m.num_values) for m in hm]
+    torch.cuda.synchronize()
+    k = max(3, steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        pa.encode_list_column_device(do, dc, dl, dv, True, True, opts)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    nbytes = offs.nbytes + child.nbytes + (rows + 7) // 8 + (len(child) + 7) // 8
+    return {"rows": rows, "leaves": int(len(child)), "input_GBps": round(nbytes / dt / 1e9, 1),
+            "ms_per_call": round(dt * 1e3, 3), "encoded_bytes": len(host), "host_writer_GBps": round(nbytes / th / 1e9, 2),
+            "host_threads": threads, "byte_identical_to_host": bool(ok),
+            "call": "pa_amd.encode_list_column_device (bitmaps packed on the device, metas read back)"}
 
 
 def zstd_size(torch, pa, device: int, threads: int, rows: int = 8 * 1024 * 1024) -> dict:

@@ -340,9 +340,12 @@ extern "C" uint64_t sb_encode_list_device_bound(int32_t physical_type, uint64_t 
   const uint64_t w = type_width(physical_type);
   const uint64_t P = max_page_rows ? std::min(max_page_rows, n_rows) : n_rows;
   if (!w || !P) return 0;
-  const uint64_t pages = (n_rows + P - 1) / P, vmax = std::max<uint64_t>(n_child, 1);
-  // per page: the level header (<= 12 + 20 + (rows + values) * 3 / 8) + the child values' page
-  return pages * (((12 + 20 + (P + vmax) * 3 / 8 + 16 + 15) & ~15ull) + sb::adaptive_slot_bytes(vmax, (uint32_t)w, 0));
+  const uint64_t pages = (n_rows + P - 1) / P;
+  // the level headers (<= 12 + 20 + (rows + values) * 3 / 8 + 1 a page) and
+  // the child values' pages: adaptive_slot_bytes is affine in the rows, so
+  // the pages' slots sum to <= pages x slot(1) + slot(n_child)
+  return pages * (48 + 16 + sb::adaptive_slot_bytes(1, (uint32_t)w, 0)) + (n_rows + n_child) * 3 / 8 +
+         sb::adaptive_slot_bytes(std::max<uint64_t>(n_child, 1), (uint32_t)w, 0);
 }
 
 extern "C" sb_status sb_encode_list_column_device(sb_ctx* ctx, int32_t physical_type, const int64_t* d_offsets,
