@@ -55,7 +55,7 @@ uint64_t sb_snappy_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst) {
 uint64_t sb_zstd_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst) {
   if (!n) return sbz::zstd_empty(dst);
   std::vector<uint8_t> table(sbc::kLz4TableBytes), lz(sbc::lz4_bound(sbz::kZChunk));
-  std::vector<uint64_t> recs(sbz::kZSeqPerBlock);
+  std::vector<uint64_t> recs(sbz::kZScratchU64);
   uint64_t op = sbz::zstd_frame_header(dst, (uint32_t)n);
   for (uint64_t off = 0; off < n; off += sbz::kZChunk) {
     const uint32_t cl = (uint32_t)std::min<uint64_t>(sbz::kZChunk, n - off);

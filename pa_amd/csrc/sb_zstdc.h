@@ -12,8 +12,10 @@
 //     checksum; the input in 128 KiB chunks, each parsed by LZ4 on its own
 //     (matches stay inside the chunk);
 //   * a chunk's sequences go out in compressed blocks of at most
-//     kZSeqPerBlock sequences: Raw_Literals_Block (3-byte header) with the
-//     block's literal bytes, then the sequences under the Predefined_Mode FSE
+//     kZSeqPerBlock sequences: the block's literals (zstd_literals: a
+//     Huffman-coded 4-stream Compressed_Literals_Block with a directly
+//     represented table when that is smaller, an RLE block for one repeated
+//     byte, else Raw), then the sequences under the Predefined_Mode FSE
 //     tables of literal lengths, match lengths and offsets (RFC 8878
 //     §3.1.1.3.2.2), every offset a new one (Offset_Value = offset + 3, no
 //     repeat codes), encoded last sequence first as libzstd's
@@ -188,16 +190,193 @@ SB_HD inline uint32_t zstd_frame_header(uint8_t* d, uint32_t n) {
 
 SB_HD inline void put24(uint8_t* d, uint32_t v) { d[0] = (uint8_t)v, d[1] = (uint8_t)(v >> 8), d[2] = (uint8_t)(v >> 16); }
 
+// Scratch of zstd_transcode: the sequence records, then the literals' Huffman
+// work area (u32): histogram [256], codes [256] (value | bits << 16), tree
+// node weights [257], parents [257] and the present symbols [129].
+constexpr uint32_t kZScratchU64 = kZSeqPerBlock + 1024;  // 24 KiB
+constexpr uint32_t kHufMaxBits = 11;
+
+// Code lengths (<= kHufMaxBits) of the symbols counted in h[0..256) into
+// len[0..256) (0: absent), a complete prefix code; m >= 2 symbols present.
+// Plain Huffman (two smallest active nodes merged, O(m^2): m <= 129), then,
+// past kHufMaxBits, lengths clamped and the Kraft sum restored by lengthening
+// the longest codes under the limit and shortening where it stays <= 1.
+SB_HD inline uint32_t huf_lengths(const uint32_t* h, uint32_t* len, uint32_t* wt, uint32_t* par) {
+  uint32_t* sym_of = par + 260;  // [129]
+  uint32_t nn = 0;
+  for (uint32_t s = 0; s < 256; s++) {
+    len[s] = 0;
+    if (h[s]) {
+      sym_of[nn] = s;
+      wt[nn] = h[s];
+      nn++;
+    }
+  }
+  const uint32_t m = nn;
+  for (uint32_t k = 0; k < m; k++) par[k] = 0x7FFFFFFFu;  // active (not merged), no parent
+  for (uint32_t step = 0; step + 1 < m; step++) {
+    uint32_t a = 0xFFFFFFFFu, b = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < nn; k++) {
+      if (par[k] != 0x7FFFFFFFu) continue;  // merged already
+      if (a == 0xFFFFFFFFu || wt[k] < wt[a]) {
+        b = a;
+        a = k;
+      } else if (b == 0xFFFFFFFFu || wt[k] < wt[b]) {
+        b = k;
+      }
+    }
+    wt[nn] = wt[a] + wt[b];
+    par[nn] = 0x7FFFFFFFu;
+    par[a] = nn;
+    par[b] = nn;
+    nn++;
+  }
+  uint32_t maxl = 0;
+  for (uint32_t k = 0; k < m; k++) {
+    uint32_t d = 0;
+    for (uint32_t x = k; par[x] != 0x7FFFFFFFu; x = par[x]) d++;
+    len[sym_of[k]] = d;
+    maxl = d > maxl ? d : maxl;
+  }
+  if (maxl <= kHufMaxBits) return maxl;
+  // limit: clamp, then bring the Kraft sum (in units of 2^-kHufMaxBits) back to 2^kHufMaxBits
+  uint32_t K = 0;
+  for (uint32_t k = 0; k < m; k++) {
+    uint32_t& l = len[sym_of[k]];
+    if (l > kHufMaxBits) l = kHufMaxBits;
+    K += 1u << (kHufMaxBits - l);
+  }
+  const uint32_t full = 1u << kHufMaxBits;
+  while (K > full) {  // lengthen the longest code below the limit (the rarest among them)
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < m; k++) {
+      const uint32_t l = len[sym_of[k]];
+      if (l < kHufMaxBits && (best == 0xFFFFFFFFu || l > len[sym_of[best]] ||
+                              (l == len[sym_of[best]] && h[sym_of[k]] < h[sym_of[best]])))
+        best = k;
+    }
+    K -= 1u << (kHufMaxBits - len[sym_of[best]] - 1);
+    len[sym_of[best]]++;
+  }
+  while (K < full) {  // shorten the longest code whose shortening keeps the sum <= 1 (the most frequent among them)
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < m; k++) {
+      const uint32_t l = len[sym_of[k]];
+      if (l > 1 && K + (1u << (kHufMaxBits - l)) <= full &&
+          (best == 0xFFFFFFFFu || l > len[sym_of[best]] || (l == len[sym_of[best]] && h[sym_of[k]] > h[sym_of[best]])))
+        best = k;
+    }
+    if (best == 0xFFFFFFFFu) break;
+    K += 1u << (kHufMaxBits - len[sym_of[best]]);
+    len[sym_of[best]]--;
+  }
+  return kHufMaxBits;
+}
+
+// The block's literals section at d (RFC 8878 §3.1.1.3.1) from the n staged
+// literal bytes at lit; returns its length.  Huffman (Literals_Block_Type 2,
+// four streams, Size_Format 10 / 11) when every literal is <= 128 (a directly
+// represented weight table: 4 bits a symbol below the largest, whose weight
+// is implied) and the section comes out smaller; RLE for one repeated byte;
+// else Raw.  Codes as the decoder assigns them (HUF_buildCTable): per length,
+// consecutive values in symbol order, longer codes below; each stream is the
+// bit stream of its symbols added last to first (HUF_compress1X_usingCTable)
+// with the end mark.
+SB_HD inline uint32_t zstd_literals(const uint8_t* lit, uint32_t n, uint8_t* d, uint32_t* hw) {
+  uint32_t* h = hw;
+  uint32_t* code = hw + 256;
+  uint32_t* wt = hw + 512;
+  uint32_t* par = hw + 800;
+  for (uint32_t s = 0; s < 256; s++) h[s] = 0;
+  for (uint32_t i = 0; i < n; i++) h[lit[i]]++;
+  uint32_t m = 0, last = 0;
+  for (uint32_t s = 0; s < 256; s++)
+    if (h[s]) {
+      m++;
+      last = s;
+    }
+  if (n >= 2 && m == 1) {  // RLE_Literals_Block, Size_Format 11
+    put24(d, (n << 4) | 0xDu);
+    d[3] = lit[0];
+    return 4;
+  }
+  if (n >= 256 && m >= 2 && last <= 128) {
+    uint32_t* len = code;  // (lengths first, then the codes in place)
+    const uint32_t maxb = huf_lengths(h, len, wt, par);
+    // the streams' sizes: bits of each quarter + the end mark
+    const uint32_t seg = (n + 3) / 4;
+    uint32_t sbytes[4], tot = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t a = k * seg < n ? k * seg : n, b = (k + 1) * seg < n && k < 3 ? (k + 1) * seg : n;
+      uint64_t bits = 1;
+      for (uint32_t i = a; i < b; i++) bits += len[lit[i]];
+      sbytes[k] = (uint32_t)((bits + 7) / 8);
+      tot += sbytes[k];
+    }
+    const uint32_t tree = 1 + (last + 1) / 2, csize = tree + 6 + tot, hdr = (n < 16384 && csize < 16384) ? 4 : 5;
+    bool fits = sbytes[0] < 65536 && sbytes[1] < 65536 && sbytes[2] < 65536;
+    if (fits && hdr + csize < 3 + n) {
+      // codes: nbPerRank / valPerRank (HUF_buildCTable)
+      uint32_t per[kHufMaxBits + 2] = {}, val[kHufMaxBits + 2] = {};
+      for (uint32_t s = 0; s <= last; s++) per[len[s]]++;
+      uint32_t mn = 0;
+      for (uint32_t b = maxb; b > 0; b--) {
+        val[b] = mn;
+        mn += per[b];
+        mn >>= 1;
+      }
+      // header
+      if (hdr == 4) {
+        const uint32_t v = 2u | (2u << 2) | (n << 4) | (csize << 18);
+        for (uint32_t k = 0; k < 4; k++) d[k] = (uint8_t)(v >> (8 * k));
+      } else {
+        const uint64_t v = 2ull | (3ull << 2) | ((uint64_t)n << 4) | ((uint64_t)csize << 22);
+        for (uint32_t k = 0; k < 5; k++) d[k] = (uint8_t)(v >> (8 * k));
+      }
+      uint8_t* q = d + hdr;
+      // the weight table: 127 + (symbols below `last`), 4 bits each, first in the high nibble
+      q[0] = (uint8_t)(127 + last);
+      for (uint32_t s = 0; s < last; s += 2) {
+        const uint32_t w0 = len[s] ? maxb + 1 - len[s] : 0, w1 = s + 1 < last && len[s + 1] ? maxb + 1 - len[s + 1] : 0;
+        q[1 + s / 2] = (uint8_t)((w0 << 4) | w1);
+      }
+      q += tree;
+      for (uint32_t s = 0; s <= last; s++) code[s] = len[s] ? (val[len[s]]++ | (len[s] << 16)) : 0u;
+      for (uint32_t k = 0; k < 3; k++) {
+        q[2 * k] = (uint8_t)sbytes[k];
+        q[2 * k + 1] = (uint8_t)(sbytes[k] >> 8);
+      }
+      q += 6;
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t a = k * seg < n ? k * seg : n, b = (k + 1) * seg < n && k < 3 ? (k + 1) * seg : n;
+        BitW bw{q, 0, 0};
+        for (uint32_t i = b; i > a; i--) {
+          const uint32_t c = code[lit[i - 1]];
+          bw.add(c & 0xFFFFu, c >> 16);
+        }
+        bw.close();
+        q = bw.p;
+      }
+      return (uint32_t)(q - d);
+    }
+  }
+  put24(d, (n << 4) | 0xCu);  // Raw_Literals_Block, Size_Format 11 (20-bit size)
+  for (uint32_t i = 0; i < n; i++) d[3 + i] = lit[i];
+  return 3 + n;
+}
+
 // The Zstd blocks of one chunk (clen input bytes at src, its LZ4 block lz of
-// lzlen bytes) at dst; recs = kZSeqPerBlock records of scratch.  The last
-// block carries Last_Block when `last`.  Returns the bytes written.
-SB_HD inline uint32_t zstd_transcode(const uint8_t* lz, uint32_t lzlen, const uint8_t* src, uint32_t clen, uint8_t* dst,
+// lzlen bytes) at dst; recs = kZScratchU64 words of scratch.  A block's
+// literals are staged in lz itself, compacted behind the parse (the write
+// index never passes the read index).  The last block carries Last_Block
+// when `last`.  Returns the bytes written.
+SB_HD inline uint32_t zstd_transcode(uint8_t* lz, uint32_t lzlen, const uint8_t* src, uint32_t clen, uint8_t* dst,
                                      uint64_t* recs, bool last) {
   uint32_t p = 0, op = 0, out0 = 0;
   bool end = false;
   do {
     uint8_t* bh = dst + op;
-    uint8_t* lit = bh + 6;  // block header, literals header (3 bytes each)
+    uint8_t* lit = lz + p;  // the block's literals, staged
     uint32_t nlit = 0, ns = 0, dec = 0;
     while (ns < kZSeqPerBlock) {
       if (p >= lzlen) {
@@ -235,7 +414,8 @@ SB_HD inline uint32_t zstd_transcode(const uint8_t* lz, uint32_t lzlen, const ui
       dec += ml;
     }
     if (p >= lzlen) end = true;
-    uint8_t* q = lit + nlit;  // Sequences_Section_Header
+    uint8_t* q = bh + 3 + zstd_literals(lit, nlit, bh + 3, (uint32_t*)(recs + kZSeqPerBlock));
+    // Sequences_Section_Header
     if (ns < 128) {
       *q++ = (uint8_t)ns;
     } else {
@@ -277,7 +457,6 @@ SB_HD inline uint32_t zstd_transcode(const uint8_t* lz, uint32_t lzlen, const ui
       op += 3 + dec;
     } else {
       put24(bh, (content << 3) | (2u << 1) | (lb ? 1u : 0u));
-      put24(bh + 3, (nlit << 4) | 0xCu);  // Raw_Literals_Block, Size_Format 11 (20-bit size)
       op += 3 + content;
     }
     out0 += dec;
