@@ -1445,7 +1445,7 @@ __global__ __launch_bounds__(64) void k_enc_basic_wave(AdArgs A) {
       __builtin_amdgcn_wave_barrier();
       // (the input stays in HBM: staging a page's 64 KiB in LDS measured 21.3
       // -> 11.9 GB/s on C5's encode -- one wave a CU instead of six)
-      cs = sbc::lz4_compress_wave(sbc::Lz4GSrc{src}, len, out + body, tab);
+      cs = sbc::lz4_compress_wave(sbc::Lz4GSrc{src}, len, out + body, tab, 1023);  // (kLz4WaveLdsMin)
     } else if constexpr (ZS) {
       const uint64_t zb = sbz::zstd_bound(len);
       if ((uint64_t)body + zb + sbc::lz4_bound(min(len, sbz::kZChunk)) + 16 > cap) {
@@ -2024,9 +2024,9 @@ static void launch_wave_basic(const sba::AdArgs& a, hipStream_t st) {
   if (a.o.dflt == sba::C_ZSTD) {
     ensure_lds_attr(sba::k_enc_basic_wave<W, BIN, true>, (int)lds);
     hipLaunchKernelGGL((sba::k_enc_basic_wave<W, BIN, true>), dim3(a.n_batch), dim3(64), lds, st, a);
-  } else {
-    ensure_lds_attr(sba::k_enc_basic_wave<W, BIN, false>, (int)lds);
-    hipLaunchKernelGGL((sba::k_enc_basic_wave<W, BIN, false>), dim3(a.n_batch), dim3(64), lds, st, a);
+  } else {  // LZ4: the compressor's smallest area (more page-waves a CU)
+    ensure_lds_attr(sba::k_enc_basic_wave<W, BIN, false>, (int)sbc::kLz4WaveLdsMin);
+    hipLaunchKernelGGL((sba::k_enc_basic_wave<W, BIN, false>), dim3(a.n_batch), dim3(64), sbc::kLz4WaveLdsMin, st, a);
   }
 }
 

@@ -229,6 +229,12 @@ __device__ inline uint32_t lz4_wave_incl_scan(uint32_t v) {  // DPP row shifts +
 
 typedef __attribute__((address_space(3))) uint8_t lz4_lds8;
 constexpr uint32_t kLz4WaveLds = 16384 + 8192;  // position table + per-batch hash owners
+// The smallest area the compressor runs in: the position table + 1 KiB of
+// hash owners indexed by the hash's low bits (k_enc_basic_wave: 17 KiB a
+// page-wave, nine a CU instead of six).  An owner slot shared by two hashes
+// only sends both lanes through the clash loop, which groups lanes by the
+// exact hash, so the parse is the same.
+constexpr uint32_t kLz4WaveLdsMin = 16384 + 1024;
 
 // The input of lz4_compress_wave: in HBM (a plain pointer), or staged in LDS
 // (every hash, candidate compare and match extension of the parse is a
@@ -252,7 +258,8 @@ struct Lz4LSrc {
 // `lds`: kLz4WaveLds bytes, the first 16 KiB zeroed (the position table:
 // 8192 u16 below LZ4_64Klimit, 4096 u32 above), then 8 KiB of scratch.
 template <class Src>
-__device__ inline uint32_t lz4_compress_wave(const Src src, uint32_t n, uint8_t* dst, lz4_lds8* lds) {
+__device__ inline uint32_t lz4_compress_wave(const Src src, uint32_t n, uint8_t* dst, lz4_lds8* lds,
+                                             uint32_t own_mask = 8191) {
   const uint32_t lane = threadIdx.x & 63;
   const bool u16 = n < kLz4_64Klimit;
   typedef __attribute__((address_space(3))) uint16_t l16;
@@ -323,8 +330,8 @@ __device__ inline uint32_t lz4_compress_wave(const Src src, uint32_t n, uint8_t*
         // one, and only the last of them (up to the match) enters the table.
         // A plain byte write per lane finds the clashes, one ballot per
         // clashing hash groups them.
-        if (live) own[h] = (uint8_t)lane;
-        bool todo = live && own[h] != lane;
+        if (live) own[h & own_mask] = (uint8_t)lane;
+        bool todo = live && own[h & own_mask] != lane;
         uint64_t grp = 1ull << lane;
         for (uint64_t lm = __ballot(todo); lm; lm = __ballot(todo)) {
           const uint32_t H = __shfl(h, (uint32_t)__builtin_ctzll(lm), 64);
