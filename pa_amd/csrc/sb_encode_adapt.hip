@@ -267,27 +267,6 @@ __device__ uint32_t bexcl_max(Sh& sh, uint32_t v, uint32_t* tot) {
   *tot = t;
   return max(pre, lane ? xl : 0u);
 }
-// inclusive prefix max over threads
-__device__ uint32_t bscan_max(Sh& sh, uint32_t v, uint32_t* tot) {
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x = max(x, y);
-  }
-  if (lane == 63) sh.redu[wv] = x;
-  __syncthreads();
-  uint32_t pre = 0, t = 0;
-#pragma unroll
-  for (int k = 0; k < NW; k++) {
-    if ((uint32_t)k < wv) pre = max(pre, sh.redu[k]);
-    t = max(t, sh.redu[k]);
-  }
-  __syncthreads();
-  *tot = t;
-  return max(pre, x);
-}
 
 __device__ __forceinline__ void put8(uint8_t* o, uint64_t v, uint32_t nb) {
   for (uint32_t j = 0; j < nb; j++) o[j] = (uint8_t)(v >> (8 * j));
@@ -858,22 +837,16 @@ __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
   for (uint32_t r = tid; r < n; r += NT)
     if (ins(r)) idx[r] = tab_insert(tab, S, r, dv(r), dv);  // the slot, for now
   __syncthreads();
-  // ids: first rows in row order
-  uint32_t carry = 0;
-  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
-    const uint32_t r = t0 + tid;
-    bool f = false;
-    uint32_t slot = 0;
-    if (r < n && ins(r)) {
-      slot = idx[r];
-      f = tab.row1(slot) == r + 1;
-    }
-    uint32_t tot;
-    const uint32_t ex = bscan(sh, f ? 1u : 0u, &tot);
-    if (f) row_of[carry + ex] = r;
-    carry += tot;
-  }
-  const uint32_t k = carry;
+  // ids: first rows in row order -- one block scan over thread chunks of
+  // consecutive rows (a scan per 256 rows cost 32 barriers pairs a page)
+  const uint32_t ch = (n + NT - 1) / NT, c0 = min(n, tid * ch), c1 = min(n, c0 + ch);
+  auto first = [&](uint32_t r) { return ins(r) && tab.row1(idx[r]) == r + 1; };
+  uint32_t nf = 0;
+  for (uint32_t r = c0; r < c1; r++) nf += first(r) ? 1u : 0u;
+  uint32_t k;
+  uint32_t wpos = bscan(sh, nf, &k);
+  for (uint32_t r = c0; r < c1; r++)
+    if (first(r)) row_of[wpos++] = r;
   __syncthreads();
   for (uint32_t j = tid; j < k; j += NT) {
     const uint32_t r = row_of[j];
@@ -885,16 +858,15 @@ __device__ uint32_t dict_body(Ctx& c, Sh& sh, const Av& a, uint32_t fm, uint32_t
     if (ins(r)) idx[r] = tab.hi(idx[r]);
   __syncthreads();
   // null rows take the id of the last inserted row before them
-  uint32_t carry_last = 0;
-  for (uint32_t t0 = 0; t0 < n; t0 += NT) {
-    const uint32_t r = t0 + tid;
-    const bool in = r < n && ins(r);
-    uint32_t tmax;
-    const uint32_t incl = bscan_max(sh, in ? r + 1 : 0u, &tmax);
-    const uint32_t last = max(incl, carry_last);
-    if (r < n && !in) idx[r] = idx[last - 1];
-    carry_last = max(carry_last, tmax);
-    __syncthreads();
+  // (same chunks; row 0 is always inserted)
+  uint32_t lastc = 0;
+  for (uint32_t r = c0; r < c1; r++)
+    if (ins(r)) lastc = r + 1;
+  uint32_t tmax;
+  uint32_t last = bexcl_max(sh, lastc, &tmax);
+  for (uint32_t r = c0; r < c1; r++) {
+    if (ins(r)) last = r + 1;
+    else idx[r] = idx[last - 1];
   }
   __syncthreads();
   const Av ia{(const uint8_t*)idx, nullptr, 0, n};
@@ -1695,33 +1667,31 @@ __global__ __launch_bounds__(NT) void k_enc_binary(AdArgs A) {
     for (uint32_t r = tid; r < n; r += NT)
       if (ins(r)) idx[r] = tab_insert_h(tab, Sl, r, hsh[r], [&](uint32_t o) { return same(o, r); });
     __syncthreads();
-    uint32_t carry = 0;
-    for (uint32_t t0 = 0; t0 < n; t0 += NT) {
-      const uint32_t r = t0 + tid;
-      const bool f = r < n && ins(r) && tab.row1(idx[r]) == r + 1;
-      uint32_t tot;
-      const uint32_t ex = bscan(sh, f ? 1u : 0u, &tot);
-      if (f) row_of[carry + ex] = r;
-      carry += tot;
-    }
-    const uint32_t k = carry;
+    // ids over thread chunks of consecutive rows, as dict_body
+    const uint32_t ch = (n + NT - 1) / NT, c0 = min(n, tid * ch), c1 = min(n, c0 + ch);
+    auto first = [&](uint32_t r) { return ins(r) && tab.row1(idx[r]) == r + 1; };
+    uint32_t nf = 0;
+    for (uint32_t r = c0; r < c1; r++) nf += first(r) ? 1u : 0u;
+    uint32_t k;
+    uint32_t wpos = bscan(sh, nf, &k);
+    for (uint32_t r = c0; r < c1; r++)
+      if (first(r)) row_of[wpos++] = r;
     __syncthreads();
     for (uint32_t j = tid; j < k; j += NT) tab.set(idx[row_of[j]], j, row_of[j] + 1);
     __syncthreads();
     for (uint32_t r = tid; r < n; r += NT)
       if (ins(r)) idx[r] = tab.hi(idx[r]);
     __syncthreads();
-    uint32_t carry_last = 0;
-    for (uint32_t t0 = 0; t0 < n; t0 += NT) {
-      const uint32_t r = t0 + tid;
-      const bool in = r < n && ins(r);
-      uint32_t tmax;
-      const uint32_t incl = bscan_max(sh, in ? r + 1 : 0u, &tmax);
-      const uint32_t last = max(incl, carry_last);
-      if (r < n && !in) idx[r] = idx[last - 1];
-      carry_last = max(carry_last, tmax);
-      __syncthreads();
+    uint32_t lastc = 0;
+    for (uint32_t r = c0; r < c1; r++)
+      if (ins(r)) lastc = r + 1;
+    uint32_t tmax;
+    uint32_t last = bexcl_max(sh, lastc, &tmax);
+    for (uint32_t r = c0; r < c1; r++) {
+      if (ins(r)) last = r + 1;
+      else idx[r] = idx[last - 1];
     }
+    __syncthreads();
     // the index stream cascades (Dict forbidden) at depth 1 (its scratch: region 1)
     const Av ia{(const uint8_t*)idx, nullptr, 0, n};
     const uint32_t p2 = enc_stream<4, false, false, 1, ZS>(c, sh, ia, fm | (1u << C_DICT), body);
