@@ -348,6 +348,34 @@ sb_status sb_encode_list_column(int32_t physical_type, const int64_t* h_offsets,
                                 int32_t item_nullable, uint64_t n_rows, const sb_write_options* opts,
                                 uint64_t max_page_rows, int32_t n_threads, uint8_t** h_out, uint64_t* out_len,
                                 sb_page_meta** h_metas, uint64_t* n_pages);
+/* One nest of a leaf path for the writer (outermost first, as in
+ * sb_nested_desc): a List / LargeList / Map nest gives entries + 1 absolute
+ * int64 positions into the next nest's entries (or the leaf's slots); a
+ * Struct nest gives no offsets (its children hold one slot per struct slot).
+ * h_validity: LSB-first bitmap over the nest's entries, NULL = all valid. */
+typedef struct {
+  const int64_t* h_offsets;
+  const uint8_t* h_validity;
+} sb_nest_in;
+/* encode_chunk for one leaf column of ANY nested field (write/common.rs:
+ * 60-115: to_nested + to_leaves, then slice_parquet_array per page of
+ * max_page_rows top-level rows; write_nested, serialize.rs:135-198, with the
+ * rep / def levels of write_nested_validity :217-232 -- no stream for a max
+ * level of 0).  desc is the leaf's InitNested chain (depth, per-nest
+ * nullable, struct_mask, item_nullable, physical_type; offset_width is not
+ * used: the levels do not depend on it).  The leaf: fixed width -- h_values
+ * holds its slots; Boolean -- h_values is the LSB-first bitmap of its slots;
+ * Binary / Utf8 (Large too) -- h_leaf_offsets = slots + 1 absolute int64
+ * positions into h_values (values_len bytes, the whole buffer the Extend
+ * header and stats use).  h_leaf_validity over the slots (NULL = none).  A
+ * Struct / Map field is written by one call per leaf, in to_leaves order.
+ * PageMeta.num_values = the page's level count.  Page p samples with
+ * sb_page_seed(opts->seed, p).  SB_E_ARG for decreasing offsets. */
+sb_status sb_encode_nested_column(const sb_nested_desc* desc, const sb_nest_in* h_nests, const void* h_values,
+                                  const int64_t* h_leaf_offsets, uint64_t values_len, const uint8_t* h_leaf_validity,
+                                  uint64_t n_rows, const sb_write_options* opts, uint64_t max_page_rows,
+                                  int32_t n_threads, uint8_t** h_out, uint64_t* out_len, sb_page_meta** h_metas,
+                                  uint64_t* n_pages);
 uint64_t sb_page_seed(uint64_t seed, uint64_t page);
 /* The block compressors the device encoder runs for the Basic codecs
  * (CommonCompression::compress, basic.rs:108-152), built for the host:

@@ -202,8 +202,10 @@ def compress_binary(values: bytes, offsets, validity, opts, offset_width=4, pare
     return data
 
 
-def compress_bool(values, validity, opts) -> bytes:
-    """compress_boolean (compression/boolean/mod.rs:23-61) of one leaf slice."""
+def compress_bool(bits: np.ndarray, off: int, n: int, validity, opts) -> bytes:
+    """compress_boolean (compression/boolean/mod.rs:23-61) of the leaf slice
+    [off, off + n) of the bitmap `bits`: the Basic codecs take the parent's
+    bytes when off % 8 == 0 (Bitmap::as_slice), a rebuilt bitmap otherwise."""
     import ctypes
 
     L = O.lib()
@@ -212,12 +214,11 @@ def compress_bool(values, validity, opts) -> bytes:
         L.orc_compress_boolean.argtypes = [P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.POINTER(O.WriteOptions),
                                            ctypes.POINTER(O._Buf)]
         L._cbool_ready = True
-    bits = O._pack(values)
     if len(bits) == 0:
         bits = np.zeros(1, np.uint8)
     vb = None if validity is None else O._pack(validity)
     buf = O._Buf()
-    rc = L.orc_compress_boolean(O._ptr(bits), 0, O._ptr(vb), len(values), ctypes.byref(opts), ctypes.byref(buf))
+    rc = L.orc_compress_boolean(O._ptr(bits), off, O._ptr(vb), n, ctypes.byref(opts), ctypes.byref(buf))
     data = O._take(buf)
     O._check(rc, "compress_boolean")
     return data
@@ -229,17 +230,19 @@ def leaf_stream(leaf_f: F, leaf_a: A, j0: int, j1: int, opts) -> bytes:
     val = None if leaf_a.validity is None else np.asarray(leaf_a.validity[j0:j1], bool)
     if leaf_f.leaf == "fixed":
         return O.compress(np.ascontiguousarray(leaf_a.values[j0:j1]), val, opts)
-    if leaf_f.leaf == "bool":
-        return compress_bool(np.asarray(leaf_a.values[j0:j1], bool), val, opts)
+    if leaf_f.leaf == "bool":  # write_bitmap over the sliced leaf: the leaf's bitmap at bit offset j0
+        return compress_bool(O._pack(np.asarray(leaf_a.values, bool)), j0, j1 - j0, val, opts)
     offs, data = leaf_a.values
     b, e = int(offs[j0]), int(offs[j1])
     return compress_binary(data[b:e], np.asarray(offs[j0:j1 + 1], np.int64) - b, val, opts,
                            8 if leaf_f.large else 4, parent_values_len=len(data))
 
 
-def write_field(f: F, arr: A, page_rows: int, opts=None):
+def write_field(f: F, arr: A, page_rows: int, opts=None, page_seed=None):
     """encode_chunk for one nested field -> one (chunk, [(length,
-    num_levels)]) per leaf, to_leaves order."""
+    num_levels)]) per leaf, to_leaves order.  page_seed(p), when given, is
+    the sampler seed of page p (the product writer's sb_page_seed(opts.seed,
+    p)); otherwise every page samples with opts.seed."""
     opts = opts or O.WriteOptions.make()
     rows = arr.length
     step = min(page_rows or rows, rows) if rows else 1
@@ -248,10 +251,14 @@ def write_field(f: F, arr: A, page_rows: int, opts=None):
         max_rep, max_def = _max_levels(path)
         leaf_a = _arrays_on_path(arr, path)[-1]
         chunk, metas = [], []
-        for r0 in range(0, rows, step):
+        for p, r0 in enumerate(range(0, rows, step)):
             r1 = min(rows, r0 + step)
+            po = opts
+            if page_seed is not None:
+                po = O.WriteOptions(opts.default_codec, opts.has_ratio, opts.ratio, opts.forbidden_mask,
+                                    opts.forced_codec, page_seed(p))
             rep, dfl, j0, j1 = levels(arr, path, r0, r1)
-            page = _levels_page(rep, dfl, max_rep, max_def, r1 - r0) + leaf_stream(path[-1], leaf_a, j0, j1, opts)
+            page = _levels_page(rep, dfl, max_rep, max_def, r1 - r0) + leaf_stream(path[-1], leaf_a, j0, j1, po)
             chunk.append(page)
             metas.append((len(page), len(rep)))
         out.append((b"".join(chunk), metas))

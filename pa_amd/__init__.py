@@ -21,7 +21,8 @@ from .binary import (  # noqa: F401,E402
     BINARY, LARGE_BINARY, LARGE_UTF8, UTF8, BinaryColumnDecoder, batch_read_binary, encode_binary_column,
     encode_binary_column_device,
 )
-from .nested import (DeviceArray, Field, FieldDecoder, ListColumnDecoder, NestedColumnDecoder,  # noqa: F401,E402
-                     batch_read_field, batch_read_list, encode_list_column, encode_list_column_device)
+from .nested import (DeviceArray, Field, FieldDecoder, HostArray, ListColumnDecoder, NestedColumnDecoder,  # noqa: F401,E402
+                     batch_read_field, batch_read_list, encode_field, encode_list_column, encode_list_column_device)
 from .file import Leaf, StrawboatFile, parse_schema  # noqa: F401,E402
 from .table import ColumnGroupDecoder  # noqa: F401,E402
+from .stream import PageArray, decode_columns, iter_page_arrays, to_host  # noqa: F401,E402

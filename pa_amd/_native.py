@@ -32,7 +32,7 @@ EXPORTED = [
     "sb_plan_nested_count", "sb_decode_nested_planned", "sb_parse_schema", "sb_file_open", "sb_file_close",
     "sb_file_last_error", "sb_file_num_columns", "sb_file_column", "sb_file_schema", "sb_file_upload",
     "sb_decode_page_validity", "sb_decode_page_levels", "sb_plan_column_at",
-    "sb_encode_list_device_bound", "sb_encode_list_column_device",
+    "sb_encode_list_device_bound", "sb_encode_list_column_device", "sb_encode_nested_column",
 ]
 
 MAX_NEST = 4

@@ -701,6 +701,95 @@ int encode_list_page(int phys, const int64_t* offsets, const uint8_t* list_valid
   return compress_values(phys, (const uint8_t*)child + v0 * ts, child_valid ? vb.data() : nullptr, nv, opt, rng, out);
 }
 
+// ---- any nest chain over any leaf: encode_chunk's to_nested / to_leaves
+// (write/common.rs:60-115) for one leaf path, slice_parquet_array over rows
+// [r0, r0 + rows), then write_nested (serialize.rs:135-198) with
+// write_nested_validity (:217-232).  The levels are the Dremel encoding
+// arrow2's RepLevelsIter / DefLevelsIter produce for one leaf: a null nest
+// or an empty list emits one level and stops; a struct passes its slot
+// through (its children hold one slot per struct slot, null or not); a list
+// slot's children repeat at the list's cumulative repetition level.
+namespace {
+struct LevelWalk {
+  const NestLevel* nests;
+  int depth;
+  const NestLeaf* leaf;
+  uint32_t cum_rep[8];  // d + 1 <= SB_MAX_NEST (masked so the inlined recursion stays in bounds)
+  std::vector<uint32_t> rep, def;
+
+  void walk(int d, uint64_t i, uint32_t r, uint32_t dl) {
+    if (d == depth) {
+      rep.push_back(r);
+      def.push_back(dl + (leaf->nullable && bit(leaf->validity, (size_t)i)));
+      return;
+    }
+    const NestLevel& n = nests[d];
+    if (n.nullable && !bit(n.validity, (size_t)i)) { rep.push_back(r); def.push_back(dl); return; }
+    dl += n.nullable;
+    if (n.is_struct) { walk(d + 1, i, r, dl); return; }
+    const int64_t b = n.offsets[i], e = n.offsets[i + 1];
+    if (b == e) { rep.push_back(r); def.push_back(dl); return; }
+    for (int64_t j = b; j < e; j++) walk(d + 1, (uint64_t)j, j == b ? r : cum_rep[(d + 1) & 7], dl + 1);
+  }
+};
+
+void rebase_bits(const uint8_t* bm, uint64_t at, uint64_t n, std::vector<uint8_t>& out) {
+  out.assign((n + 7) / 8 + 1, 0);
+  for (uint64_t i = 0; i < n; i++)
+    if ((bm[(at + i) >> 3] >> ((at + i) & 7)) & 1) out[i >> 3] |= (uint8_t)(1u << (i & 7));
+}
+}  // namespace
+
+int nested_max_levels(const NestLevel* nests, int depth, bool leaf_nullable, uint32_t* max_rep, uint32_t* max_def) {
+  if (depth < 1 || depth > SB_MAX_NEST) return SB_E_NYI;
+  uint32_t mr = 0, md = leaf_nullable;
+  for (int d = 0; d < depth; d++) {
+    mr += !nests[d].is_struct;
+    md += nests[d].nullable + !nests[d].is_struct;
+  }
+  *max_rep = mr;
+  *max_def = md;
+  return 0;
+}
+
+int encode_nested_page(const NestLevel* nests, int depth, const NestLeaf& leaf, uint64_t r0, uint64_t rows,
+                       const Opts& opt, uint64_t seed, Bytes& out, uint64_t* num_levels) {
+  uint32_t max_rep, max_def;
+  if (int rc = nested_max_levels(nests, depth, leaf.nullable, &max_rep, &max_def)) return rc;
+  LevelWalk w{nests, depth, &leaf, {0}, {}, {}};
+  for (int d = 0; d < depth; d++) w.cum_rep[d + 1] = w.cum_rep[d] + !nests[d].is_struct;
+  for (uint64_t i = r0; i < r0 + rows; i++) w.walk(0, i, 0, 0);
+  // write_rep_and_def V2: no stream for a max level of 0
+  Bytes lv;
+  if (max_rep) encode_levels_u32(w.rep, 32 - (uint32_t)__builtin_clz(max_rep), lv);
+  const size_t rep_len = lv.size();
+  if (max_def) encode_levels_u32(w.def, 32 - (uint32_t)__builtin_clz(max_def), lv);
+  put<uint32_t>(out, (uint32_t)rows);
+  put<uint32_t>(out, (uint32_t)rep_len);
+  put<uint32_t>(out, (uint32_t)(lv.size() - rep_len));
+  out.insert(out.end(), lv.begin(), lv.end());
+  *num_levels = w.rep.size();
+  // slice_parquet_array: the leaf slots of the page's rows, through each list nest
+  uint64_t j0 = r0, j1 = r0 + rows;
+  for (int d = 0; d < depth; d++)
+    if (!nests[d].is_struct) { j0 = (uint64_t)nests[d].offsets[j0]; j1 = (uint64_t)nests[d].offsets[j1]; }
+  const uint64_t m = j1 - j0;
+  std::vector<uint8_t> vb;
+  if (leaf.validity) rebase_bits(leaf.validity, j0, m, vb);
+  const uint8_t* valid = leaf.validity ? vb.data() : nullptr;
+  if (leaf.phys == SB_T_BOOLEAN)  // write_bitmap over the sliced leaf: the bitmap at bit offset j0
+    return encode_bool_page((const uint8_t*)leaf.values, (size_t)j0, valid, (size_t)m, false, opt, seed, out);
+  if (leaf.phys >= SB_T_BINARY && leaf.phys <= SB_T_LARGE_UTF8) {
+    const int ow = (leaf.phys == SB_T_BINARY || leaf.phys == SB_T_UTF8) ? 4 : 8;
+    return encode_binary_page((const uint8_t*)leaf.values, leaf.offsets + j0, valid, (size_t)m, false, ow,
+                              leaf.values_len, opt, seed, out);
+  }
+  const int ts = type_size(leaf.phys);
+  if (!ts) return SB_E_NYI;
+  Rng rng{seed};
+  return compress_values(leaf.phys, (const uint8_t*)leaf.values + j0 * ts, valid, (size_t)m, opt, rng, out);
+}
+
 // ---- boolean pages: compress_boolean (compression/boolean/mod.rs:22-61),
 // gen_stats (:178-220), choose_compressor (:222-280), RLE over the bits as u8
 // (boolean/rle.rs:31-39), OneValue (boolean/one_value.rs:44-52).

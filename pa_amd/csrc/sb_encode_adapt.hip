@@ -1143,7 +1143,7 @@ __device__ __forceinline__ void page_rows(const AdArgs& A, uint32_t p, uint64_t*
 // A List page's level header, copied to the page's start by the threads of
 // `nt`; returns its length
 __device__ __forceinline__ uint32_t put_head(const AdArgs& A, uint32_t p, uint8_t* out, uint32_t nt) {
-  const uint32_t hl = A.head_len[p];
+  const uint32_t hl = (uint32_t)min<uint64_t>(A.head_len[p], A.head_slot);  // never past the header's slot
   const uint8_t* h = A.heads + (uint64_t)p * A.head_slot;
   for (uint32_t j = threadIdx.x; j < hl; j += nt) out[j] = h[j];
   return hl;
@@ -1861,10 +1861,19 @@ __global__ __launch_bounds__(NT) void k_enc_list_levels(ListLv a) {
     const int64_t len = a.offsets[r0 + r + 1] - a.offsets[r0 + r];
     return len > 0 ? (uint32_t)len : 1u;
   };
-  // 1. the level prefix over the rows (chunks of consecutive rows per thread)
+  // 1. the level prefix over the rows (chunks of consecutive rows per thread);
+  // a decreasing offset pair (a negative list length) fails the page
+  __shared__ uint32_t s_bad;
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
   const uint32_t ch = (m + NT - 1) / NT, b0 = min(m, tid * ch), b1 = min(m, b0 + ch);
   uint32_t sum = 0;
-  for (uint32_t r = b0; r < b1; r++) sum += row_levels(r);
+  bool bad = false;
+  for (uint32_t r = b0; r < b1; r++) {
+    sum += row_levels(r);
+    bad |= a.offsets[r0 + r + 1] < a.offsets[r0 + r];
+  }
+  if (bad) atomicOr(&s_bad, 1u);
   uint32_t x = sum;
   for (uint32_t d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(x, d, 64);
@@ -1883,6 +1892,13 @@ __global__ __launch_bounds__(NT) void k_enc_list_levels(ListLv a) {
   }
   if (tid == 0) lpre[m] = L;
   __syncthreads();
+  if (s_bad) {  // every thread sees the flag after the barrier: the page is refused whole
+    if (tid == 0) {
+      a.head_len[p] = 0;
+      a.levels[p] = ~0ull;
+    }
+    return;
+  }
   // level i's (rep, def); the spare bits past L hold level i - 32 (or 0)
   auto level = [&](uint32_t i) -> uint32_t {  // rep | def << 1
     if (i >= L) {
@@ -2157,55 +2173,48 @@ int encode_list_device(sb_ctx* ctx, int phys, const int64_t* d_offsets, const ui
                        uint64_t n_rows, const sb_write_options* opts, uint64_t step, uint8_t* d_out, uint64_t out_cap,
                        uint64_t* out_len, sb_page_meta* h_metas, uint64_t np) {
   hipStream_t st = (hipStream_t)sb_ctx_stream(ctx);
-  uint64_t* d_rows_at = nullptr;
-  uint8_t* d_heads = nullptr;
-  uint32_t* d_hlen = nullptr;
-  uint64_t* d_levels = nullptr;
-  auto cleanup = [&]() {
-    (void)hipStreamSynchronize(st);
-    if (d_rows_at) (void)hipFree(d_rows_at);
-    if (d_heads) (void)hipFree(d_heads);
-    if (d_hlen) (void)hipFree(d_hlen);
-    if (d_levels) (void)hipFree(d_levels);
-  };
+  // rows_at [np + 1] u64 | levels [np] u64 | head_len [np] u32 in one grow-only
+  // context slot, the page headers in another (encode_adaptive uses 0..4)
+  const size_t meta_bytes = (np + 1) * 8 + np * 8 + np * 4;
+  uint8_t* meta = (uint8_t*)ctx_scratch(ctx, meta_bytes, 5);
+  if (!meta) return ctx_fail(ctx, SB_E_DEVICE, "device list encode alloc");
+  uint64_t* d_rows_at = (uint64_t*)meta;
+  uint64_t* d_levels = d_rows_at + np + 1;
+  uint32_t* d_hlen = (uint32_t*)(d_levels + np);
   std::vector<uint64_t> rows_at(np + 1), levels(np);
-  if (hipMalloc(&d_rows_at, (np + 1) * 8) != hipSuccess || hipMalloc(&d_hlen, np * 4) != hipSuccess ||
-      hipMalloc(&d_levels, np * 8) != hipSuccess) {
-    cleanup();
-    return ctx_fail(ctx, SB_E_DEVICE, "device list encode alloc");
-  }
   hipLaunchKernelGGL(k_list_rows_at, dim3((uint32_t)((np + 256) / 256)), dim3(256), 0, st, d_offsets, n_rows, step, np,
                      d_rows_at);
+  if (const hipError_t e = hipGetLastError(); e != hipSuccess)
+    return ctx_fail(ctx, SB_E_DEVICE, "device list encode launch (step 1)", (int)e);
   if (hipMemcpyAsync(rows_at.data(), d_rows_at, (np + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess) {
-    cleanup();
+      hipStreamSynchronize(st) != hipSuccess)
     return ctx_fail(ctx, SB_E_DEVICE, "device list encode step 1");
-  }
+  // the host writer's check: offsets must not decrease (else P and the slot sizes wrap)
+  for (uint64_t q = 0; q < np; q++)
+    if (rows_at[q + 1] < rows_at[q] || (int64_t)rows_at[q] < 0) return ctx_fail(ctx, SB_E_ARG, "decreasing list offsets");
   uint64_t P = 1;
   for (uint64_t q = 0; q < np; q++) P = std::max<uint64_t>(P, rows_at[q + 1] - rows_at[q]);
   // a page's levels: <= rows + values; header: 12 + two ULEB128 runs + the packed levels
   const uint64_t lmax = step + P;
   const uint64_t head_slot = (12 + 2 * 10 + (lmax + 7) / 8 + (2 * lmax + 7) / 8 + 15) & ~15ull;
-  if (hipMalloc(&d_heads, np * head_slot) != hipSuccess) {
-    cleanup();
-    return ctx_fail(ctx, SB_E_DEVICE, "device list encode alloc");
-  }
+  uint8_t* d_heads = (uint8_t*)ctx_scratch(ctx, np * head_slot, 6);
+  if (!d_heads) return ctx_fail(ctx, SB_E_DEVICE, "device list encode alloc");
   sba::ListLv L{d_offsets, list_nullable ? d_list_validity : nullptr, item_nullable ? d_child_validity : nullptr,
                 n_rows, (uint32_t)step, list_nullable ? 1u : 0u, item_nullable ? 1u : 0u, d_heads, head_slot, d_hlen,
                 d_levels};
   const uint32_t lds = (uint32_t)((step + 1) * 4);
   ensure_lds_attr(sba::k_enc_list_levels, (int)lds);
   hipLaunchKernelGGL(sba::k_enc_list_levels, dim3((uint32_t)np), dim3(sba::NT), lds, st, L);
+  if (const hipError_t e = hipGetLastError(); e != hipSuccess)
+    return ctx_fail(ctx, SB_E_DEVICE, "device list encode launch (step 2)", (int)e);
   if (hipMemcpyAsync(levels.data(), d_levels, np * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess) {
-    cleanup();
+      hipStreamSynchronize(st) != hipSuccess)
     return ctx_fail(ctx, SB_E_DEVICE, "device list encode step 2");
-  }
+  for (uint64_t q = 0; q < np; q++)
+    if (levels[q] == ~0ull) return ctx_fail(ctx, SB_E_ARG, "decreasing list offsets");
   const ListPart lp{d_rows_at, d_heads, head_slot, d_hlen, levels.data()};
-  const int rc = encode_adaptive(ctx, phys, (const uint8_t*)d_child, item_nullable ? d_child_validity : nullptr,
-                                 rows_at[np], item_nullable, opts, P, d_out, out_cap, out_len, h_metas, np, &lp);
-  cleanup();
-  return rc;
+  return encode_adaptive(ctx, phys, (const uint8_t*)d_child, item_nullable ? d_child_validity : nullptr, rows_at[np],
+                         item_nullable, opts, P, d_out, out_cap, out_len, h_metas, np, &lp);
 }
 
 

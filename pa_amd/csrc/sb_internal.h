@@ -13,7 +13,7 @@ namespace sb {
 
 // Grow-only device scratch owned by a context (slot < kCtxScratchSlots),
 // reused across calls on its stream; nullptr if the allocation fails.
-constexpr int kCtxScratchSlots = 5;
+constexpr int kCtxScratchSlots = 7;
 void* ctx_scratch(sb_ctx* ctx, size_t bytes, int slot);
 // Records a failure message on the context (sb_last_error) and returns st.
 int ctx_fail(sb_ctx* ctx, int st, const char* what, int hip_error = -1);

@@ -264,6 +264,85 @@ sb_status sb_encode_list_column(int32_t phys, const int64_t* h_offsets, const ui
   return SB_OK;
 }
 
+// encode_chunk for one leaf of any nested field (write/common.rs:60-115:
+// to_nested + to_leaves, slice_parquet_array per page of max_page_rows
+// top-level rows; write_nested serialize.rs:135-198).  The nests' offsets
+// must be non-decreasing over the entries the rows reach (SB_E_ARG
+// otherwise: slice_parquet_array would read past the child arrays).
+sb_status sb_encode_nested_column(const sb_nested_desc* desc, const sb_nest_in* h_nests, const void* h_values,
+                                  const int64_t* h_leaf_offsets, uint64_t values_len, const uint8_t* h_leaf_validity,
+                                  uint64_t n_rows, const sb_write_options* opts, uint64_t max_page_rows,
+                                  int32_t n_threads, uint8_t** h_out, uint64_t* out_len, sb_page_meta** h_metas,
+                                  uint64_t* n_pages) {
+  if (!desc || !h_nests || !h_out || !out_len || !h_metas || !n_pages) return SB_E_ARG;
+  const int depth = desc->depth, phys = desc->physical_type;
+  if (depth < 1 || depth > SB_MAX_NEST) return SB_E_NYI;
+  const bool binary = phys >= SB_T_BINARY && phys <= SB_T_LARGE_UTF8;
+  if (!binary && phys != SB_T_BOOLEAN && !sb::enc::type_size(phys)) return SB_E_NYI;
+  sb::enc::NestLevel nests[SB_MAX_NEST];
+  uint64_t count = n_rows;  // entries of the current nest
+  for (int d = 0; d < depth; d++) {
+    const bool is_struct = (desc->struct_mask >> d) & 1;
+    nests[d] = sb::enc::NestLevel{h_nests[d].h_offsets, h_nests[d].h_validity, desc->list_nullable[d] != 0, is_struct};
+    if (is_struct) continue;
+    const int64_t* o = h_nests[d].h_offsets;
+    if (!o) return SB_E_ARG;
+    for (uint64_t i = 0; i < count; i++)
+      if (o[i + 1] < o[i] || o[i] < 0) return SB_E_ARG;
+    count = (uint64_t)o[count];
+  }
+  if (count && !h_values) return SB_E_ARG;
+  if (binary) {
+    if (!h_leaf_offsets) return SB_E_ARG;
+    for (uint64_t i = 0; i < count; i++)
+      if (h_leaf_offsets[i + 1] < h_leaf_offsets[i] || h_leaf_offsets[i] < 0) return SB_E_ARG;
+    if ((uint64_t)h_leaf_offsets[count] > values_len) return SB_E_ARG;
+  }
+  const sb::enc::NestLeaf leaf{phys, h_values, h_leaf_offsets, values_len, h_leaf_validity, desc->item_nullable != 0};
+  const uint64_t step = max_page_rows ? std::min<uint64_t>(max_page_rows, n_rows) : n_rows;
+  const uint64_t np = step ? (n_rows + step - 1) / step : 0;
+  std::vector<std::vector<uint8_t>> pages(np);
+  std::vector<uint64_t> levels(np, 0);
+  std::vector<int> rcs(np, 0);
+  const Opts o = to_opts(opts);
+  const uint64_t seed = opts ? opts->seed : 0;
+  std::atomic<uint64_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const uint64_t p = next.fetch_add(1);
+      if (p >= np) return;
+      const uint64_t r0 = p * step, m = std::min(step, n_rows - r0);
+      rcs[p] = sb::enc::encode_nested_page(nests, depth, leaf, r0, m, o, sb::enc::page_seed(seed, p), pages[p],
+                                           &levels[p]);
+    }
+  };
+  int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  nt = (int)std::min<uint64_t>((uint64_t)nt, std::max<uint64_t>(np, 1));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; t++) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  size_t total = 0;
+  for (uint64_t p = 0; p < np; p++) {
+    if (rcs[p]) return (sb_status)rcs[p];
+    total += pages[p].size();
+  }
+  uint8_t* buf = (uint8_t*)std::malloc(total ? total : 1);
+  sb_page_meta* metas = (sb_page_meta*)std::malloc((np ? np : 1) * sizeof(sb_page_meta));
+  if (!buf || !metas) { std::free(buf); std::free(metas); return SB_E_ARG; }
+  size_t at = 0;
+  for (uint64_t p = 0; p < np; p++) {
+    if (!pages[p].empty()) std::memcpy(buf + at, pages[p].data(), pages[p].size());
+    at += pages[p].size();
+    metas[p] = sb_page_meta{pages[p].size(), levels[p]};
+  }
+  *h_out = buf;
+  *out_len = total;
+  *h_metas = metas;
+  *n_pages = np;
+  return SB_OK;
+}
+
 // NativeWriter::finish (writer.rs:128-167): schema | meta | u32 schema_size |
 // u32 meta_size | FF FF FF FF 00 00 00 00; the body starts with
 // b"ARROW2" 00 00 (writer.rs:97-100).  Column chunks are given back to back.

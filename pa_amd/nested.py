@@ -494,14 +494,24 @@ class FieldDecoder:
         except Exception:
             self.close()
             raise
-        for dec, path in zip(self.decoders, self.paths):  # a struct's leaves agree on the nests they share
-            first = self.decoders[0]
-            shared = 0
-            while shared < min(len(path), len(self.paths[0])) - 1 and path[shared] is self.paths[0][shared]:
-                shared += 1
-            if dec.counts[:shared] != first.counts[:shared]:
-                raise N.StrawboatError(N.E_OUT_OF_SPEC, "leaf columns of one field disagree on their rows")
+        self._check_counts(self.field, self.decoders, 0)
         self.num_rows = self.decoders[0].counts[0]
+
+    def _check_counts(self, f: Field, decs, d: int):
+        """Every leaf under a nest agrees with the last one on that nest's
+        entries (create_struct's child-length check, StructArray::try_new),
+        at every node of the tree -- not only against the first leaf."""
+        n = decs[-1].counts[d]
+        if any(x.counts[d] != n for x in decs):
+            raise N.StrawboatError(N.E_OUT_OF_SPEC, "leaf columns of one field disagree on their rows")
+        if f.kind == "struct":
+            k = 0
+            for c in f.children:
+                m = c.n_columns()
+                self._check_counts(c, decs[k:k + m], d + 1)
+                k += m
+        elif f.kind != "leaf":
+            self._check_counts(f.children[0], decs, d + 1)
 
     def decode(self) -> DeviceArray:
         outs = [dec.decode() for dec in self.decoders]
@@ -531,6 +541,120 @@ class FieldDecoder:
             self.close()
         except Exception:
             pass
+
+
+# ---- the writer half: any nested field through sb_encode_nested_column -------
+@dataclass
+class HostArray:
+    """A host array of a nested Field, shaped like arrow2's arrays (the
+    writer's input, NativeWriter::write, write/writer.rs:113-143).
+    validity: bool per slot or None; list / large_list / map: offsets (int64,
+    length + 1, absolute positions into children[0]); struct: children (each
+    with one slot per struct slot); leaf: values -- fixed width: a numpy
+    array; Boolean: bool per slot; Binary / Utf8: (int64 offsets, bytes)."""
+    kind: str
+    length: int
+    validity: object = None
+    offsets: object = None
+    children: List["HostArray"] = field(default_factory=list)
+    values: object = None
+
+
+class NestInC(ctypes.Structure):
+    _fields_ = [("h_offsets", ctypes.c_void_p), ("h_validity", ctypes.c_void_p)]
+
+
+def _encode_lib():
+    L = N.lib()
+    if not getattr(L, "_nested_enc_ready", False):
+        P, U64, I32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32
+        L.sb_encode_nested_column.argtypes = [ctypes.POINTER(NestedDescC), ctypes.POINTER(NestInC), P, P, U64, P, U64,
+                                              ctypes.POINTER(N.WriteOptionsC), U64, I32,
+                                              ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(U64),
+                                              ctypes.POINTER(ctypes.POINTER(N.PageMetaC)), ctypes.POINTER(U64)]
+        L.sb_encode_nested_column.restype = I32
+        L._nested_enc_ready = True
+    return L
+
+
+def _arrays_on_path(arr: HostArray, path):
+    out = [arr]
+    for d in range(len(path) - 1):
+        f, child = path[d], path[d + 1]
+        a = out[-1]
+        out.append(a.children[0] if f.kind in ("list", "large_list", "map") else a.children[f.children.index(child)])
+    return out
+
+
+def _bits(v):
+    return None if v is None else np.packbits(np.asarray(v, bool), bitorder="little")
+
+
+def encode_field(fld: Field, arr: HostArray, options=None, n_threads: int = 0):
+    """encode_chunk for one nested field (write/common.rs:60-115): one
+    column chunk per leaf, to_leaves order, each paged by
+    options.max_page_size top-level rows (slice_parquet_array) and written
+    by write_nested (serialize.rs:135-198) through the host encoder
+    (sb_encode_nested_column).  Returns [(chunk bytes, [PageMeta])]."""
+    from .write import WriteOptions, _take
+
+    if fld.kind == "leaf":
+        raise N.StrawboatError(N.E_ARG, "a primitive field is not nested: use encode_column")
+    L = _encode_lib()
+    options = options or WriteOptions()
+    opts = options.c()
+    out_cols = []
+    for path in fld.leaf_paths():
+        nulls, mask, leaf_null, large = init_chain(path)
+        depth = len(nulls)
+        if depth > MAX_NEST:
+            raise N.StrawboatError(N.E_NYI, f"nesting depth {depth} not supported")
+        arrs = _arrays_on_path(arr, path)
+        keep = []  # numpy buffers alive across the call
+        nests = (NestInC * MAX_NEST)()
+        for d in range(depth):
+            a = arrs[d]
+            if not (mask >> d) & 1:
+                o = np.ascontiguousarray(a.offsets, np.int64)
+                keep.append(o)
+                nests[d].h_offsets = o.ctypes.data
+            vb = _bits(a.validity)
+            if vb is not None:
+                keep.append(vb)
+                nests[d].h_validity = vb.ctypes.data
+        lf, la = path[-1], arrs[-1]
+        phys = lf.physical_type
+        lo = None
+        vlen = 0
+        if phys in (BINARY, UTF8, LARGE_BINARY, LARGE_UTF8):
+            lo_, data = la.values
+            lo = np.ascontiguousarray(lo_, np.int64)
+            vals = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+            vlen = len(data)
+        elif phys == N.BOOLEAN:
+            vals = _bits(la.values)
+            if len(vals) == 0:
+                vals = np.zeros(1, np.uint8)
+        else:
+            vals = np.ascontiguousarray(la.values)
+            if len(vals) == 0:
+                vals = np.zeros(1, vals.dtype)
+        lvb = _bits(la.validity)
+        ln = (ctypes.c_int32 * MAX_NEST)(*([int(x) for x in nulls] + [0] * (MAX_NEST - depth)))
+        desc = NestedDescC(phys, depth, ln, int(leaf_null), 8 if large else 4, mask)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        olen, npg = ctypes.c_uint64(), ctypes.c_uint64()
+        metas = ctypes.POINTER(N.PageMetaC)()
+        vp = lambda x: None if x is None else x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        st = L.sb_encode_nested_column(ctypes.byref(desc), nests, vp(vals), vp(lo), vlen, vp(lvb), arr.length,
+                                       ctypes.byref(opts), options.max_page_size or 0, n_threads, ctypes.byref(out),
+                                       ctypes.byref(olen), ctypes.byref(metas), ctypes.byref(npg))
+        if st:
+            raise N.StrawboatError(st, "encode_nested_column")
+        pm = [PageMeta(metas[i].length, metas[i].num_values) for i in range(npg.value)]
+        L.sb_free(metas)
+        out_cols.append((_take(out, olen.value), pm))
+    return out_cols
 
 
 def batch_read_field(fld: Field, columns, ctx: Optional[Context] = None) -> DeviceArray:

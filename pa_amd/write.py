@@ -261,8 +261,8 @@ def page_seed(seed: int, page: int) -> int:
 
 
 class NativeWriter:
-    """NativeWriter (writer.rs:42-167) over an in-memory buffer for flat
-    primitive columns: start() -> write(columns) once -> finish()."""
+    """NativeWriter (writer.rs:42-167) over an in-memory buffer: start() ->
+    write(columns) once -> finish(); flat, Binary / Utf8 and nested fields."""
 
     def __init__(self, options: Optional[WriteOptions] = None, schema_bytes: bytes = b""):
         self.options = options or WriteOptions()
@@ -277,16 +277,33 @@ class NativeWriter:
         self.buf += ARROW_MAGIC + b"\x00\x00"
         self.state = "started"
 
-    def write(self, columns: Sequence[Tuple[np.ndarray, Optional[np.ndarray], bool]]):
-        """columns: (values, validity|None, nullable) per leaf, equal lengths."""
+    def write(self, columns):
+        """columns: one entry per field of the chunk, equal lengths -- a flat
+        field as (values, validity|None, nullable), a Binary / Utf8 field as
+        (BinaryColumn-like (offsets, bytes) values, validity|None, nullable,
+        physical type), a nested field as (pa_amd.Field, pa_amd.HostArray):
+        encode_chunk writes every leaf of it, to_leaves order
+        (write/common.rs:60-115)."""
+        from .nested import Field, encode_field
+
         if self.state == "written":
             raise N.StrawboatError(N.E_OUT_OF_SPEC, "The strawboat file can only accept one RowGroup in a single file")
         if self.state != "started":
             raise N.StrawboatError(N.E_OUT_OF_SPEC, "The strawboat file must be started before it can be written to")
-        for values, validity, nullable in columns:
-            chunk, pages = encode_column(values, validity, nullable, self.options)
-            self.metas.append(ColumnMeta(len(self.buf), pages))
-            self.buf += chunk
+        for col in columns:
+            if isinstance(col[0], Field):
+                leaves = encode_field(col[0], col[1], self.options)
+            elif len(col) == 4:
+                from .binary import encode_binary_column
+
+                (offs, data), validity, nullable, phys = col
+                leaves = [encode_binary_column(data, offs, validity, nullable, self.options, phys)]
+            else:
+                values, validity, nullable = col
+                leaves = [encode_column(values, validity, nullable, self.options)]
+            for chunk, pages in leaves:
+                self.metas.append(ColumnMeta(len(self.buf), pages))
+                self.buf += chunk
         self.state = "written"
 
     def finish(self) -> bytes:

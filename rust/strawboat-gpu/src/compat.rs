@@ -358,6 +358,155 @@ impl Array {
         assert!(offset as u64 + length as u64 <= self.len, "the offset of the new array cannot exceed the existing length");
         Array { data_type: self.data_type.clone(), data: self.data.clone(), offset: self.offset + offset as u64, len: length as u64 }
     }
+
+    /// The array's rows as host Arrow buffers, shaped like the reference's
+    /// `Box<dyn Array>` (batch_read.rs:190-209 returns host arrays): values,
+    /// offsets rebased to start at 0, LSB-first bitmaps at bit 0 -- one D2H
+    /// copy per buffer range.  Lists / maps carry only the child slots their
+    /// rows reach; a struct's children its rows.
+    pub fn to_host(&self) -> Result<HostArray> {
+        let (b, e) = (self.offset, self.offset + self.len);
+        match self.data.as_ref() {
+            ColumnData::Primitive(p) => {
+                let ty = leaf_type(&self.data_type);
+                let values = if ty == PhysicalType::Boolean {
+                    bits_to_host(&p.values, b, self.len)?
+                } else {
+                    let w = ty.width();
+                    p.values.range_to_host(b as usize * w, self.len as usize * w)?
+                };
+                Ok(HostArray::Primitive { values, validity: opt_bits(&p.validity, b, self.len)?, len: self.len })
+            }
+            ColumnData::Binary(x) => {
+                let ty = leaf_type(&self.data_type);
+                binary_to_host(&x.offsets, ty.offset_width(), &x.values, &x.validity, b, e)
+            }
+            ColumnData::List(l) => {
+                let ow = if matches!(self.data_type, DataType::LargeList(_)) { 8 } else { 4 };
+                let offs = offsets_to_host(&l.offsets, ow, b, e)?;
+                let (c0, c1) = (offs[0] as u64, offs[offs.len() - 1] as u64);
+                let DataType::List(item) | DataType::LargeList(item) = &self.data_type else {
+                    unreachable!("a List column has a list type")
+                };
+                let w = leaf_type(&item.data_type).width();
+                let child = HostArray::Primitive {
+                    values: l.values.range_to_host(c0 as usize * w, (c1 - c0) as usize * w)?,
+                    validity: opt_bits(&l.leaf_validity, c0, c1 - c0)?,
+                    len: c1 - c0,
+                };
+                Ok(HostArray::List { offsets: rebase(offs), validity: opt_bits(&l.list_validity, b, self.len)?,
+                                     values: Box::new(child), len: self.len })
+            }
+            ColumnData::Nested(n) => chain_to_host(&self.data_type, n, 0, b, e),
+            ColumnData::Field(f) => node_to_host(f, b, e),
+        }
+    }
+}
+
+/// Bits [bit0, bit0 + n) of a device bitmap, re-based to bit 0.
+fn bits_to_host(buf: &DeviceBuffer, bit0: u64, n: u64) -> Result<Vec<u8>> {
+    let first = (bit0 / 8) as usize;
+    let raw = buf.range_to_host(first, ((bit0 % 8 + n + 7) / 8) as usize)?;
+    let sh = (bit0 % 8) as u32;
+    let mut out = vec![0u8; ((n + 7) / 8) as usize];
+    for (i, o) in out.iter_mut().enumerate() {
+        let lo = raw[i] >> sh;
+        let hi = if sh > 0 && i + 1 < raw.len() { raw[i + 1] << (8 - sh) } else { 0 };
+        *o = lo | hi;
+    }
+    if n % 8 != 0 {
+        let last = out.len() - 1;
+        out[last] &= (1u8 << (n % 8)) - 1;
+    }
+    Ok(out)
+}
+
+fn opt_bits(buf: &Option<DeviceBuffer>, bit0: u64, n: u64) -> Result<Option<Vec<u8>>> {
+    buf.as_ref().map(|b| bits_to_host(b, bit0, n)).transpose()
+}
+
+/// Offsets [b, e] (e - b + 1 entries of `width` bytes) as i64.
+fn offsets_to_host(buf: &DeviceBuffer, width: usize, b: u64, e: u64) -> Result<Vec<i64>> {
+    let raw = buf.range_to_host(b as usize * width, (e - b + 1) as usize * width)?;
+    Ok(raw
+        .chunks_exact(width)
+        .map(|c| if width == 8 { i64::from_le_bytes(c.try_into().unwrap()) } else { i32::from_le_bytes(c.try_into().unwrap()) as i64 })
+        .collect())
+}
+
+fn rebase(mut offs: Vec<i64>) -> Vec<i64> {
+    let o0 = offs[0];
+    offs.iter_mut().for_each(|x| *x -= o0);
+    offs
+}
+
+fn binary_to_host(offsets: &DeviceBuffer, width: usize, values: &DeviceBuffer, validity: &Option<DeviceBuffer>, b: u64,
+                  e: u64) -> Result<HostArray> {
+    let offs = offsets_to_host(offsets, width, b, e)?;
+    let (v0, v1) = (offs[0] as usize, offs[offs.len() - 1] as usize);
+    Ok(HostArray::Binary { values: values.range_to_host(v0, v1 - v0)?, offsets: rebase(offs),
+                           validity: opt_bits(validity, b, e - b)?, len: e - b })
+}
+
+/// A leaf of a nested decode, slots [b, e).
+fn leaf_to_host(ty: PhysicalType, n: &Nested, b: u64, e: u64) -> Result<HostArray> {
+    if ty.is_binary() {
+        let lo = n.leaf_offsets.as_ref().ok_or_else(|| Error::OutOfSpec("binary leaf without offsets".into()))?;
+        return binary_to_host(lo, ty.offset_width(), &n.values, &n.leaf_validity, b, e);
+    }
+    let values = if ty == PhysicalType::Boolean {
+        bits_to_host(&n.values, b, e - b)?
+    } else {
+        n.values.range_to_host(b as usize * ty.width(), (e - b) as usize * ty.width())?
+    };
+    Ok(HostArray::Primitive { values, validity: opt_bits(&n.leaf_validity, b, e - b)?, len: e - b })
+}
+
+/// Nest `depth` of a list-only chain decode, entries [b, e).
+fn chain_to_host(dt: &DataType, n: &Nested, depth: usize, b: u64, e: u64) -> Result<HostArray> {
+    match dt {
+        DataType::List(c) | DataType::LargeList(c) | DataType::Map(c, _) => {
+            let buf = n.offsets[depth].as_ref().ok_or_else(|| Error::OutOfSpec("list nest without offsets".into()))?;
+            let width = buf.len() / (n.counts[depth] as usize + 1);
+            let offs = offsets_to_host(buf, width, b, e)?;
+            let (c0, c1) = (offs[0] as u64, offs[offs.len() - 1] as u64);
+            let child = Box::new(chain_to_host(&c.data_type, n, depth + 1, c0, c1)?);
+            let validity = opt_bits(&n.validity[depth], b, e - b)?;
+            Ok(if matches!(dt, DataType::Map(_, _)) {
+                HostArray::Map { offsets: rebase(offs), validity, field: child, len: e - b }
+            } else {
+                HostArray::List { offsets: rebase(offs), validity, values: child, len: e - b }
+            })
+        }
+        DataType::Struct(_) => Err(Error::OutOfSpec("a struct nest in a one-leaf chain".into())),
+        leaf => leaf_to_host(leaf_type(leaf), n, b, e),
+    }
+}
+
+/// A node of a Struct / Map field decode, entries [b, e).
+fn node_to_host(node: &FieldNode, b: u64, e: u64) -> Result<HostArray> {
+    let validity = || node.validity().map(|v| bits_to_host(v, b, e - b)).transpose();
+    match &node.data_type {
+        DataType::Struct(_) => {
+            let validity = validity()?;
+            let values = node.children.iter().map(|c| node_to_host(c, b, e)).collect::<Result<Vec<_>>>()?;
+            Ok(HostArray::Struct { values, validity, len: e - b })
+        }
+        DataType::List(_) | DataType::LargeList(_) | DataType::Map(_, _) => {
+            let buf = node.offsets().ok_or_else(|| Error::OutOfSpec("list nest without offsets".into()))?;
+            let width = buf.len() / (node.len as usize + 1);
+            let offs = offsets_to_host(buf, width, b, e)?;
+            let (c0, c1) = (offs[0] as u64, offs[offs.len() - 1] as u64);
+            let child = Box::new(node_to_host(&node.children[0], c0, c1)?);
+            let validity = validity()?;
+            Ok(if matches!(node.data_type, DataType::Map(_, _)) {
+                HostArray::Map { offsets: rebase(offs), validity, field: child, len: e - b }
+            } else {
+                HostArray::List { offsets: rebase(offs), validity, values: child, len: e - b }
+            })
+        }
+        leaf => leaf_to_host(leaf_type(leaf), &node.source, b, e),
+    }
 }
 
 /// `read::ArrayIter` (src/read/deserialize.rs): the arrays of a column, one
@@ -593,60 +742,141 @@ fn nested_page_rows(page: &[u8]) -> Result<u64> {
     Ok(u32::from_le_bytes([page[0], page[1], page[2], page[3]]) as u64)
 }
 
-/// The iterator `column_iter_to_arrays` returns.  On the first call it
-/// drains the page readers (handing every page buffer back through
-/// `swap_buffer`), stages each leaf chunk into HBM with one copy and plans
-/// and decodes the field once; each page then becomes the row range of the
-/// decoded field it covers.  A read or decode error of any page is returned
-/// by that first call -- a deviation from the reference's page-at-a-time
-/// iterator, which returns the arrays of the pages before a bad page first
-/// and holds one page in memory at a time ("Streaming").
+/// Pages decoded per launch by the streaming iterator: enough to fill the
+/// chip (one workgroup per page), few enough that memory stays bounded by the
+/// range, not the chunk.
+const RANGE_PAGES: usize = 64;
+
+/// The iterator `column_iter_to_arrays` returns: page-at-a-time semantics
+/// (read/deserialize.rs:237-253 yields one array per page) decoded in ranges
+/// of [`RANGE_PAGES`] pages.  Each `next()` that finds no decoded page left
+/// reads the next range from every leaf reader (handing each page buffer
+/// back through `swap_buffer`), stages it into HBM with one copy per leaf,
+/// decodes it in one launch and queues one array per page.  A bad page k of a
+/// range is found by decoding the range's pages one by one: the arrays of
+/// the pages before it come back first, then its error -- the order the
+/// reference's page iterator returns them in.
 struct PageArrays<I> {
-    readers: Option<Vec<I>>,
+    readers: Vec<I>,
     field: Field,
     is_nested: bool,
-    pages: VecDeque<(u64, u64)>,
-    data: Option<Arc<ColumnData>>,
+    ready: VecDeque<Result<Array>>,
+    done: bool,
+}
+
+/// One range of pages of every leaf column: bytes, metas, rows per page.
+struct PageRange {
+    chunks: Vec<Vec<u8>>,
+    metas: Vec<Vec<PageMeta>>,
+    rows: Vec<u64>,
 }
 
 impl<I> PageArrays<I>
 where
     I: Iterator<Item = Result<(u64, Vec<u8>)>> + PageIterator,
 {
-    fn load(&mut self, readers: Vec<I>) -> Result<()> {
-        let (mut chunks, mut all_metas, mut rows) = (Vec::new(), Vec::new(), Vec::new());
-        for (k, mut reader) in readers.into_iter().enumerate() {
-            let (mut bytes, mut metas, mut r) = (Vec::new(), Vec::new(), Vec::new());
-            while let Some(page) = reader.next() {
-                let (num_values, mut buf) = page?;
-                r.push(if self.is_nested { nested_page_rows(&buf)? } else { num_values });
+    /// Up to RANGE_PAGES pages of every reader; the error of a page that
+    /// could not be read comes back after the pages before it.
+    fn read_range(&mut self) -> (PageRange, Option<Error>) {
+        let mut r = PageRange { chunks: Vec::new(), metas: Vec::new(), rows: Vec::new() };
+        let mut err = None;
+        let mut n_pages = RANGE_PAGES;
+        for (k, reader) in self.readers.iter_mut().enumerate() {
+            let (mut bytes, mut metas, mut rows) = (Vec::new(), Vec::new(), Vec::new());
+            while metas.len() < n_pages {
+                let Some(page) = reader.next() else { break };
+                let (num_values, mut buf) = match page {
+                    Ok(p) => p,
+                    Err(e) => {
+                        err = Some(e);
+                        break;
+                    }
+                };
+                let rows_here = if self.is_nested {
+                    match nested_page_rows(&buf) {
+                        Ok(x) => x,
+                        Err(e) => {
+                            err = Some(e);
+                            break;
+                        }
+                    }
+                } else {
+                    num_values
+                };
+                rows.push(rows_here);
                 metas.push(PageMeta { length: buf.len() as u64, num_values });
                 bytes.extend_from_slice(&buf);
-                reader.swap_buffer(&mut buf);  // the page buffer back to the reader for reuse
+                reader.swap_buffer(&mut buf); // the page buffer back to the reader for reuse
             }
             if k == 0 {
-                rows = r;
-            } else if r != rows {
+                n_pages = metas.len();
+                r.rows = rows;
+            } else if rows.len() < n_pages && err.is_none() {
                 // StructIterator zips page k of every child (struct_.rs:63-85)
-                return Err(Error::OutOfSpec(format!("{}: its leaf columns page different rows", self.field.name)));
+                err = Some(Error::OutOfSpec(format!("{}: its leaf columns hold different pages", self.field.name)));
+            } else if rows[..n_pages.min(rows.len())] != r.rows[..n_pages.min(rows.len())] {
+                err = Some(Error::OutOfSpec(format!("{}: its leaf columns page different rows", self.field.name)));
             }
-            chunks.push(bytes);
-            all_metas.push(metas);
+            if err.is_some() {
+                n_pages = n_pages.min(metas.len());
+            }
+            r.chunks.push(bytes);
+            r.metas.push(metas);
         }
-        if rows.is_empty() {
-            return Ok(());
+        // every leaf keeps the pages all leaves could read
+        for (c, m) in r.chunks.iter_mut().zip(r.metas.iter_mut()) {
+            m.truncate(n_pages);
+            let len: u64 = m.iter().map(|p| p.length).sum();
+            c.truncate(len as usize);
         }
-        let data = decode_host_chunks(&chunks, &all_metas, &self.field)?;
+        r.rows.truncate(n_pages);
+        (r, err)
+    }
+
+    /// The arrays of one decoded range, one per page.
+    fn queue(&mut self, data: ColumnData, rows: &[u64]) -> Result<()> {
+        let total: u64 = rows.iter().sum();
+        if total != data.rows() {
+            return Err(Error::OutOfSpec(format!("pages hold {total} rows, the decoded range {}", data.rows())));
+        }
+        let data = Arc::new(data);
         let mut first = 0u64;
-        for r in rows {
-            self.pages.push_back((first, r));
+        for &r in rows {
+            self.ready.push_back(Ok(Array { data_type: self.field.data_type.clone(), data: data.clone(), offset: first, len: r }));
             first += r;
         }
-        if first != data.rows() {
-            return Err(Error::OutOfSpec(format!("pages hold {first} rows, the decoded column {}", data.rows())));
-        }
-        self.data = Some(Arc::new(data));
         Ok(())
+    }
+
+    fn fill(&mut self) {
+        let (r, read_err) = self.read_range();
+        let n = r.rows.len();
+        if n > 0 {
+            let res = decode_host_chunks(&r.chunks, &r.metas, &self.field).and_then(|d| self.queue(d, &r.rows));
+            if res.is_err() {
+                // find the bad page: the pages before it decode one by one
+                for p in 0..n {
+                    let one = |x: &Vec<u8>, m: &Vec<PageMeta>| {
+                        let start: u64 = m[..p].iter().map(|q| q.length).sum();
+                        x[start as usize..(start + m[p].length) as usize].to_vec()
+                    };
+                    let chunks: Vec<Vec<u8>> = r.chunks.iter().zip(&r.metas).map(|(x, m)| one(x, m)).collect();
+                    let metas: Vec<Vec<PageMeta>> = r.metas.iter().map(|m| vec![m[p]]).collect();
+                    let page = decode_host_chunks(&chunks, &metas, &self.field).and_then(|d| self.queue(d, &r.rows[p..p + 1]));
+                    if let Err(e) = page {
+                        self.ready.push_back(Err(e));
+                        self.done = true;
+                        return;
+                    }
+                }
+            }
+        }
+        if let Some(e) = read_err {
+            self.ready.push_back(Err(e));
+            self.done = true;
+        } else if n < RANGE_PAGES {
+            self.done = true;
+        }
     }
 }
 
@@ -657,20 +887,16 @@ where
     type Item = Result<Array>;
 
     fn next(&mut self) -> Option<Self::Item> {
-        if let Some(readers) = self.readers.take() {
-            if let Err(e) = self.load(readers) {
-                self.pages.clear();
-                return Some(Err(e));
-            }
+        if self.ready.is_empty() && !self.done {
+            self.fill();
         }
-        let (offset, len) = self.pages.pop_front()?;
-        let data = self.data.as_ref()?.clone();
-        Some(Ok(Array { data_type: self.field.data_type.clone(), data, offset, len }))
+        self.ready.pop_front()
     }
 }
 
 /// `column_iter_to_arrays` (src/read/deserialize.rs:237-253): one array per
-/// page of the field (one reader per leaf column, to_leaves order).
+/// page of the field (one reader per leaf column, to_leaves order), decoded
+/// lazily in ranges of [`RANGE_PAGES`] pages.
 pub fn column_iter_to_arrays<'a, I: 'a>(
     readers: Vec<I>,
     leaves: Vec<ColumnDescriptor>,
@@ -685,7 +911,7 @@ where
     if readers.len() != leaves.len() {
         return Err(Error::Argument(format!("{}: {} readers for {} leaves", field.name, readers.len(), leaves.len())));
     }
-    Ok(Box::new(PageArrays { readers: Some(readers), field, is_nested, pages: VecDeque::new(), data: None }))
+    Ok(Box::new(PageArrays { readers, field, is_nested, ready: VecDeque::new(), done: false }))
 }
 
 /// `compression::Compression` (src/compression/mod.rs:37-108).
@@ -809,11 +1035,45 @@ pub struct Schema {
     pub ipc_bytes: Vec<u8>,
 }
 
-/// One column of a [`Chunk`]: host Arrow buffers (LSB-first bitmaps).
+/// One array of a [`Chunk`]: host Arrow buffers (LSB-first bitmaps), shaped
+/// like arrow2's arrays so a nested field's array is a tree of them.
 pub enum HostArray {
+    /// `PrimitiveArray<T>`: `len` values of the field's type (a
+    /// `BooleanArray`: the LSB-first values bitmap).
     Primitive { values: Vec<u8>, validity: Option<Vec<u8>>, len: u64 },
+    /// `BinaryArray<O>` / `Utf8Array<O>`: `len + 1` absolute offsets into
+    /// `values` (the whole buffer: the stats and Extend header use its length).
     Binary { values: Vec<u8>, offsets: Vec<i64>, validity: Option<Vec<u8>>, len: u64 },
-    List { offsets: Vec<i64>, validity: Option<Vec<u8>>, values: Vec<u8>, child_validity: Option<Vec<u8>>, len: u64 },
+    /// `ListArray<O>`: `len + 1` absolute offsets into `values`.
+    List { offsets: Vec<i64>, validity: Option<Vec<u8>>, values: Box<HostArray>, len: u64 },
+    /// `StructArray`: one child per field, each `len` slots long.
+    Struct { values: Vec<HostArray>, validity: Option<Vec<u8>>, len: u64 },
+    /// `MapArray`: `len + 1` absolute offsets into `field`, the entries struct.
+    Map { offsets: Vec<i64>, validity: Option<Vec<u8>>, field: Box<HostArray>, len: u64 },
+}
+
+impl HostArray {
+    pub fn len(&self) -> u64 {
+        match self {
+            HostArray::Primitive { len, .. }
+            | HostArray::Binary { len, .. }
+            | HostArray::List { len, .. }
+            | HostArray::Struct { len, .. }
+            | HostArray::Map { len, .. } => *len,
+        }
+    }
+    pub fn is_empty(&self) -> bool {
+        self.len() == 0
+    }
+    fn validity(&self) -> &Option<Vec<u8>> {
+        match self {
+            HostArray::Primitive { validity, .. }
+            | HostArray::Binary { validity, .. }
+            | HostArray::List { validity, .. }
+            | HostArray::Struct { validity, .. }
+            | HostArray::Map { validity, .. } => validity,
+        }
+    }
 }
 
 /// arrow2 `Chunk<Box<dyn Array>>`: one array per schema field.
@@ -890,8 +1150,10 @@ impl<W: Write> NativeWriter<W> {
         Ok(())
     }
 
-    /// The chunk's columns, each paged and encoded by the engine's writer
-    /// (write/common.rs:49-119); one chunk per file (writer.rs:106-123).
+    /// The chunk's fields, each paged and encoded by the engine's writer leaf
+    /// by leaf (write/common.rs:49-119: a Struct / Map / nested List field is
+    /// one column per leaf, to_leaves order); one chunk per file
+    /// (writer.rs:106-123).
     /// Every column is encoded before any byte is written, so a column that
     /// fails to encode leaves the writer as it was.
     pub fn write(&mut self, chunk: &Chunk) -> Result<()> {
@@ -913,7 +1175,7 @@ impl<W: Write> NativeWriter<W> {
             .zip(self.schema.fields.iter())
             .map(|(a, f)| encode_array(a, f, &self.options))
             .collect::<Result<Vec<_>>>()?;
-        for (bytes, pages) in encoded {
+        for (bytes, pages) in encoded.into_iter().flatten() {
             let offset = self.offset;
             self.put(&bytes)?;
             self.metas.push(ColumnMeta { offset, pages });
@@ -992,12 +1254,171 @@ fn check_offsets(offsets: &[i64], n: u64, limit: u64) -> Result<()> {
     Ok(())
 }
 
-/// One column through sb_encode_column / sb_encode_binary_column /
-/// sb_encode_list_column (the host writer, every codec of the cascade).
-/// The buffers are checked against `len` first: the C encoder reads exactly
-/// what the lengths and offsets promise.
-fn encode_array(a: &HostArray, f: &Field, o: &WriteOptions) -> Result<(Vec<u8>, Vec<PageMeta>)> {
-    let (ty, lists, _, leaf_nullable) = leaf_path(f)?;
+/// One leaf of a nested array: the arrays on its path (outermost first,
+/// each with its nest), the leaf array and its field.
+struct LeafArrays<'a> {
+    nests: Vec<(&'a HostArray, Nest)>,
+    leaf: &'a HostArray,
+    field: &'a Field,
+}
+
+/// to_leaves / to_nested (write/common.rs:60-71) over a host array: the
+/// leaves of `a` in to_leaves order, each with its path.  The array must
+/// have the field's shape.
+fn leaf_arrays<'a>(f: &'a Field, a: &'a HostArray, nests: &mut Vec<(&'a HostArray, Nest)>,
+                   out: &mut Vec<LeafArrays<'a>>) -> Result<()> {
+    let shape = || arg(format!("{}: the array does not have the field's shape", f.name));
+    match (&f.data_type, a) {
+        (DataType::List(c) | DataType::LargeList(c), HostArray::List { values, .. }) => {
+            let large = matches!(f.data_type, DataType::LargeList(_));
+            nests.push((a, Nest { is_struct: false, nullable: f.is_nullable, large }));
+            leaf_arrays(c, values, nests, out)?;
+            nests.pop();
+        }
+        (DataType::Map(c, _), HostArray::Map { field, .. }) => {
+            nests.push((a, Nest { is_struct: false, nullable: f.is_nullable, large: false }));
+            leaf_arrays(c, field, nests, out)?;
+            nests.pop();
+        }
+        (DataType::Struct(fields), HostArray::Struct { values, .. }) => {
+            if fields.len() != values.len() {
+                return Err(shape());
+            }
+            nests.push((a, Nest { is_struct: true, nullable: f.is_nullable, large: false }));
+            for (c, v) in fields.iter().zip(values) {
+                leaf_arrays(c, v, nests, out)?;
+            }
+            nests.pop();
+        }
+        (DataType::List(_) | DataType::LargeList(_) | DataType::Map(_, _) | DataType::Struct(_), _) => {
+            return Err(shape())
+        }
+        (dt, HostArray::Binary { .. }) if leaf_type(dt).is_binary() => {
+            out.push(LeafArrays { nests: nests.clone(), leaf: a, field: f })
+        }
+        (dt, HostArray::Primitive { .. }) if !leaf_type(dt).is_binary() => {
+            out.push(LeafArrays { nests: nests.clone(), leaf: a, field: f })
+        }
+        _ => return Err(shape()),
+    }
+    Ok(())
+}
+
+/// The C encoder's chunk and page metas, freed from the engine's heap.
+fn take_encoded(out: *mut u8, len: u64, metas: *mut PageMeta, np: u64) -> (Vec<u8>, Vec<PageMeta>) {
+    let bytes = if len == 0 { Vec::new() } else { unsafe { std::slice::from_raw_parts(out, len as usize) }.to_vec() };
+    let pages = if np == 0 { Vec::new() } else { unsafe { std::slice::from_raw_parts(metas, np as usize) }.to_vec() };
+    unsafe {
+        ffi::sb_free(out as *mut c_void);
+        ffi::sb_free(metas as *mut c_void);
+    }
+    (bytes, pages)
+}
+
+/// One leaf column of a nested field through sb_encode_nested_column
+/// (write_nested, serialize.rs:135-198).  Every buffer on the path is checked
+/// against the lengths first: the encoder reads what the offsets promise.
+fn encode_nested_leaf(top_len: u64, l: &LeafArrays, o: &WriteOptions) -> Result<(Vec<u8>, Vec<PageMeta>)> {
+    let name = &l.field.name;
+    if l.nests.len() > ffi::SB_MAX_NEST {
+        return Err(Error::NotYetImplemented(format!("{name}: more than {} nests", ffi::SB_MAX_NEST)));
+    }
+    let ty = leaf_type(&l.field.data_type);
+    let mut desc = ffi::sb_nested_desc {
+        physical_type: ty as i32,
+        depth: l.nests.len() as i32,
+        list_nullable: [0; 4],
+        item_nullable: l.field.is_nullable as i32,
+        offset_width: 4,
+        struct_mask: 0,
+    };
+    let mut nests = [ffi::sb_nest_in { h_offsets: ptr::null(), h_validity: ptr::null() }; ffi::SB_MAX_NEST];
+    let mut count = top_len;  // entries of the current nest
+    for (d, (a, n)) in l.nests.iter().enumerate() {
+        if a.len() != count {
+            return Err(arg(format!("{name}: nest {d} holds {} entries, its parent reaches {count}", a.len())));
+        }
+        check_bitmap(a.validity(), count, "nest validity")?;
+        desc.list_nullable[d] = n.nullable as i32;
+        nests[d].h_validity = a.validity().as_ref().map_or(ptr::null(), |b| b.as_ptr());
+        if n.large {
+            desc.offset_width = 8;
+        }
+        match a {
+            HostArray::Struct { .. } => desc.struct_mask |= 1 << d,
+            HostArray::List { offsets, values: child, .. } | HostArray::Map { offsets, field: child, .. } => {
+                check_offsets(offsets, count, child.len())?;
+                nests[d].h_offsets = offsets.as_ptr();
+                count = child.len();
+            }
+            _ => unreachable!("leaf_arrays pushes nests only"),
+        }
+    }
+    if l.leaf.len() != count {
+        return Err(arg(format!("{name}: the leaf holds {} slots, its parent reaches {count}", l.leaf.len())));
+    }
+    check_bitmap(l.leaf.validity(), count, "leaf validity")?;
+    let (values, leaf_offsets, values_len) = match l.leaf {
+        HostArray::Primitive { values, .. } => {
+            check_values(values, count, ty)?;
+            (values.as_ptr(), ptr::null(), 0u64)
+        }
+        HostArray::Binary { values, offsets, .. } => {
+            check_offsets(offsets, count, values.len() as u64)?;
+            (values.as_ptr(), offsets.as_ptr(), values.len() as u64)
+        }
+        _ => unreachable!("leaf_arrays pushes leaves only"),
+    };
+    let eo = o.engine(ty);
+    let opts = eo.raw();
+    let (mut out, mut len, mut metas, mut np) = (ptr::null_mut(), 0u64, ptr::null_mut(), 0u64);
+    let st = unsafe {
+        ffi::sb_encode_nested_column(&desc, nests.as_ptr(), values as *const c_void, leaf_offsets, values_len,
+                                     l.leaf.validity().as_ref().map_or(ptr::null(), |b| b.as_ptr()), top_len, &opts,
+                                     eo.max_page_size.unwrap_or(0), 0, &mut out, &mut len, &mut metas, &mut np)
+    };
+    status(st, || format!("encoding {name}"))?;
+    Ok(take_encoded(out, len, metas as *mut PageMeta, np))
+}
+
+/// One field of the chunk: a flat leaf through sb_encode_column /
+/// sb_encode_binary_column, a `List<primitive>` through sb_encode_list_column,
+/// any other nesting leaf by leaf through sb_encode_nested_column (the host
+/// writer, every codec of the cascade).  Returns one (chunk, pages) per leaf
+/// column, to_leaves order (encode_chunk, write/common.rs:60-115).  The
+/// buffers are checked against `len` first: the C encoder reads exactly what
+/// the lengths and offsets promise.
+fn encode_array(a: &HostArray, f: &Field, o: &WriteOptions) -> Result<Vec<(Vec<u8>, Vec<PageMeta>)>> {
+    if !is_primitive(&f.data_type) {
+        if let (Ok((ty, lists, _, leaf_nullable)), HostArray::List { offsets, validity, values: child, len: n }) =
+            (leaf_path(f), a)
+        {
+            if let HostArray::Primitive { values, validity: child_validity, len: nc } = child.as_ref() {
+                if lists.len() == 1 && !ty.is_binary() && ty != PhysicalType::Boolean {
+                    check_offsets(offsets, *n, *nc)?;
+                    check_values(values, *nc, ty)?;
+                    check_bitmap(validity, *n, "list validity")?;
+                    check_bitmap(child_validity, *nc, "item validity")?;
+                    let eo = o.engine(ty);
+                    let opts = eo.raw();
+                    let bm = |v: &Option<Vec<u8>>| v.as_ref().map_or(ptr::null(), |b| b.as_ptr());
+                    let (mut out, mut len, mut metas, mut np) = (ptr::null_mut(), 0u64, ptr::null_mut(), 0u64);
+                    let st = unsafe {
+                        ffi::sb_encode_list_column(ty as i32, offsets.as_ptr(), bm(validity), lists[0] as i32,
+                                                   values.as_ptr() as *const c_void, bm(child_validity),
+                                                   leaf_nullable as i32, *n, &opts, eo.max_page_size.unwrap_or(0), 0,
+                                                   &mut out, &mut len, &mut metas, &mut np)
+                    };
+                    status(st, || format!("encoding {}", f.name))?;
+                    return Ok(vec![take_encoded(out, len, metas as *mut PageMeta, np)]);
+                }
+            }
+        }
+        let mut leaves = Vec::new();
+        leaf_arrays(f, a, &mut Vec::new(), &mut leaves)?;
+        return leaves.iter().map(|l| encode_nested_leaf(a.len(), l, o)).collect();
+    }
+    let ty = leaf_type(&f.data_type);
     let eo = o.engine(ty);
     let opts = eo.raw();
     let page = eo.max_page_size.unwrap_or(0);
@@ -1007,7 +1428,7 @@ fn encode_array(a: &HostArray, f: &Field, o: &WriteOptions) -> Result<(Vec<u8>, 
     let mut np = 0u64;
     let bm = |v: &Option<Vec<u8>>| v.as_ref().map_or(ptr::null(), |b| b.as_ptr());
     let st = match a {
-        HostArray::Primitive { values, validity, len: n } if lists.is_empty() && !ty.is_binary() => {
+        HostArray::Primitive { values, validity, len: n } if !ty.is_binary() => {
             check_values(values, *n, ty)?;
             check_bitmap(validity, *n, "validity")?;
             unsafe {
@@ -1015,7 +1436,7 @@ fn encode_array(a: &HostArray, f: &Field, o: &WriteOptions) -> Result<(Vec<u8>, 
                                       f.is_nullable as i32, &opts, page, 0, &mut out, &mut len, &mut metas, &mut np)
             }
         }
-        HostArray::Binary { values, offsets, validity, len: n } if lists.is_empty() && ty.is_binary() => {
+        HostArray::Binary { values, offsets, validity, len: n } if ty.is_binary() => {
             check_offsets(offsets, *n, values.len() as u64)?;
             check_bitmap(validity, *n, "validity")?;
             unsafe {
@@ -1024,30 +1445,10 @@ fn encode_array(a: &HostArray, f: &Field, o: &WriteOptions) -> Result<(Vec<u8>, 
                                              &mut len, &mut metas, &mut np)
             }
         }
-        HostArray::List { offsets, validity, values, child_validity, len: n }
-            if lists.len() == 1 && !ty.is_binary() && ty != PhysicalType::Boolean =>
-        {
-            let children = values.len() as u64 / ty.width() as u64;
-            check_offsets(offsets, *n, children)?;
-            check_bitmap(validity, *n, "list validity")?;
-            check_bitmap(child_validity, offsets[offsets.len() - 1] as u64, "item validity")?;
-            unsafe {
-                ffi::sb_encode_list_column(ty as i32, offsets.as_ptr(), bm(validity), lists[0] as i32,
-                                           values.as_ptr() as *const c_void, bm(child_validity),
-                                           leaf_nullable as i32, *n, &opts, page, 0, &mut out, &mut len, &mut metas,
-                                           &mut np)
-            }
-        }
-        _ => return Err(Error::NotYetImplemented(format!("{}: no writer path for this array / field", f.name))),
+        _ => return Err(arg(format!("{}: the array does not have the field's shape", f.name))),
     };
     status(st, || format!("encoding {}", f.name))?;
-    let bytes = unsafe { std::slice::from_raw_parts(out, len as usize) }.to_vec();
-    let pages = if np == 0 { Vec::new() } else { unsafe { std::slice::from_raw_parts(metas, np as usize) }.to_vec() };
-    unsafe {
-        ffi::sb_free(out as *mut c_void);
-        ffi::sb_free(metas as *mut c_void);
-    }
-    Ok((bytes, pages))
+    Ok(vec![take_encoded(out, len, metas, np)])
 }
 
 #[cfg(test)]
@@ -1144,6 +1545,40 @@ mod tests {
         assert!(matches!(encode_array(&past, &s, &o), Err(Error::Argument(_))));
         let down = HostArray::Binary { values: b"ab".to_vec(), offsets: vec![0, 2, 1], validity: None, len: 2 };
         assert!(matches!(encode_array(&down, &s, &o), Err(Error::Argument(_))));
+    }
+
+    #[test]
+    fn nested_arrays_follow_the_field() {
+        // io.rs:256-278 test_struct_list: Struct { name: LargeBinary, age: List<Int32> }
+        let age = Field::new("age", DataType::List(Box::new(Field::new("item", DataType::Int32, true))), true);
+        let f = Field::new("s", DataType::Struct(vec![Field::new("name", DataType::LargeBinary, true), age]), false);
+        let name = HostArray::Binary { values: b"ab".to_vec(), offsets: vec![0, 1, 2], validity: None, len: 2 };
+        let ages = HostArray::List {
+            offsets: vec![0, 2, 3],
+            validity: Some(vec![0b11]),
+            values: Box::new(HostArray::Primitive { values: vec![0; 12], validity: None, len: 3 }),
+            len: 2,
+        };
+        let a = HostArray::Struct { values: vec![name, ages], validity: None, len: 2 };
+        let mut leaves = Vec::new();
+        leaf_arrays(&f, &a, &mut Vec::new(), &mut leaves).unwrap();
+        assert_eq!(leaves.len(), 2);
+        assert_eq!(leaves[0].nests.len(), 1);
+        assert!(leaves[0].nests[0].1.is_struct);
+        assert_eq!(leaves[1].nests.len(), 2);
+        assert!(!leaves[1].nests[1].1.is_struct && leaves[1].nests[1].1.nullable);
+        // a struct child shorter than the struct, and a field / array mismatch, are argument errors
+        let short = HostArray::Struct {
+            values: vec![HostArray::Binary { values: b"a".to_vec(), offsets: vec![0, 1], validity: None, len: 1 },
+                         HostArray::List { offsets: vec![0, 0, 0], validity: None,
+                                           values: Box::new(HostArray::Primitive { values: vec![], validity: None, len: 0 }),
+                                           len: 2 }],
+            validity: None,
+            len: 2,
+        };
+        assert!(matches!(encode_array(&short, &f, &WriteOptions::default()), Err(Error::Argument(_))));
+        let flat = HostArray::Primitive { values: vec![0; 8], validity: None, len: 2 };
+        assert!(matches!(encode_array(&flat, &f, &WriteOptions::default()), Err(Error::Argument(_))));
     }
 
     #[test]

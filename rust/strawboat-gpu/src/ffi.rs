@@ -48,6 +48,9 @@ pub struct sb_nested_out { pub d_offsets: [*mut c_void; 4], pub d_validity: [*mu
                           pub d_leaf_offsets: *mut c_void, pub values_capacity: u64 }
 
 #[repr(C)] #[derive(Clone, Copy)]
+pub struct sb_nest_in { pub h_offsets: *const i64, pub h_validity: *const u8 }
+
+#[repr(C)] #[derive(Clone, Copy)]
 pub struct sb_write_options {
     pub default_codec: i32, pub has_ratio: i32, pub ratio: f64,
     pub forbidden_mask: u32, pub forced_codec: i32, pub seed: u64,
@@ -94,6 +97,11 @@ extern "C" {
                                  item_nullable: i32, n_rows: u64, opts: *const sb_write_options,
                                  max_page_rows: u64, n_threads: i32, out: *mut *mut u8, out_len: *mut u64,
                                  metas: *mut *mut sb_page_meta, n_pages: *mut u64) -> i32;
+    pub fn sb_encode_nested_column(desc: *const sb_nested_desc, nests: *const sb_nest_in, values: *const c_void,
+                                   leaf_offsets: *const i64, values_len: u64, leaf_validity: *const u8, n_rows: u64,
+                                   opts: *const sb_write_options, max_page_rows: u64, n_threads: i32,
+                                   out: *mut *mut u8, out_len: *mut u64, metas: *mut *mut sb_page_meta,
+                                   n_pages: *mut u64) -> i32;
     pub fn sb_encode_device_bound(physical_type: i32, n_rows: u64, nullable: i32, max_page_rows: u64) -> u64;
     pub fn sb_encode_column_device(ctx: *mut sb_ctx, physical_type: i32, d_values: *const c_void,
                                    d_validity: *const u8, n_rows: u64, nullable: i32,

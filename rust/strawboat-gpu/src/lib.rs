@@ -162,6 +162,24 @@ impl DeviceBuffer {
         }
         Ok(v)
     }
+    /// Bytes [offset, offset + len) of the buffer, one D2H copy (clipped to
+    /// the allocation).
+    pub fn range_to_host(&self, offset: usize, len: usize) -> Result<Vec<u8>> {
+        let off = offset.min(self.len);
+        let n = len.min(self.len - off);
+        let mut v = vec![0u8; len];
+        if n == 0 {
+            return Ok(v);
+        }
+        let e = unsafe {
+            ffi::hipMemcpy(v.as_mut_ptr() as *mut c_void, (self.ptr as *const u8).add(off) as *const c_void, n,
+                           ffi::HIP_MEMCPY_DEVICE_TO_HOST)
+        };
+        if e != 0 {
+            return Err(Error::Device(format!("hipMemcpy D2H failed: {e}")));
+        }
+        Ok(v)
+    }
     pub fn as_ptr(&self) -> *mut c_void {
         self.ptr
     }

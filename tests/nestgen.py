@@ -180,3 +180,118 @@ def device_to_host(f: F, d) -> A:
         return A("struct", n, validity, children=[device_to_host(c, x) for c, x in zip(f.children, d.children)])
     offs = d.offsets.cpu().numpy().astype(np.int64)[: n + 1]
     return A(f.kind, n, validity, offsets=offs, children=[device_to_host(f.children[0], d.children[0])])
+
+
+# ---- the reference's integration chunks as io.rs builds them ---------------
+def _rand_index(n, null_density, uniq, rng, dtype=np.int32):
+    """create_random_index (io.rs:357-369): Some(v in [0, uniq)) or None (0)."""
+    valid = rng.random(n) > null_density
+    v = np.where(valid, rng.integers(0, max(uniq, 1), n), 0).astype(dtype)
+    return A("leaf", n, valid, values=v)
+
+
+def _rand_string(n, null_density, uniq, rng):
+    """create_random_string (io.rs:385-397): decimal strings or None (empty)."""
+    valid = rng.random(n) > null_density
+    vals = rng.integers(0, max(uniq, 1), n)
+    strs = [str(int(x)).encode() if ok else b"" for x, ok in zip(vals, valid)]
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum([len(s) for s in strs])
+    return A("leaf", n, valid, values=(offs, b"".join(strs)))
+
+
+def _rand_bool(n, null_density, rng):
+    valid = rng.random(n) > null_density
+    return A("leaf", n, valid, values=(rng.random(n) < 0.5) & valid)
+
+
+def _rand_offsets(n, null_density, rng):
+    """create_random_offsets (io.rs:399-415): lengths {0, 1, 2}, null lists empty."""
+    valid = rng.random(n) > null_density
+    lens = np.where(valid, rng.integers(0, 3, n), 0)
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    return offs, valid
+
+
+def _create_list(n, null_density, rng, item=None):
+    offs, valid = _rand_offsets(n, 0.1, rng)
+    m = int(offs[-1])
+    child = item(m) if item else _rand_index(m, null_density, m, rng)
+    return A("list", n, valid, offsets=offs, children=[child])
+
+
+def _create_struct(n, null_density, uniq, rng):
+    return A("struct", n, None, children=[_rand_string(n, null_density, uniq, rng),
+                                          _rand_index(n, null_density, uniq, rng)])
+
+
+def _create_map(n, null_density, rng):
+    offs, valid = _rand_offsets(n, 0.1, rng)
+    m = int(offs[-1])
+    entries = A("struct", m, None, children=[_rand_index(m, 0.0, m, rng), _rand_string(m, null_density, m, rng)])
+    return A("map", n, valid, offsets=offs, children=[entries])
+
+
+def _stride2(child, rows=500):
+    """io.rs:199-205: ListArray over offsets 0, 2, .., 2 * rows of a longer child."""
+    return A("list", rows, None, offsets=np.arange(0, 2 * rows + 1, 2, dtype=np.int64), children=[child])
+
+
+def io_rs_cases(rng):
+    """name -> (field, array): test_struct, test_map, test_list_list,
+    test_list_struct, test_list_map, test_struct_list (io.rs:167-278) as
+    test_write_read_with_options declares them (top field nullable iff the
+    array has a validity, :444-452), plus List<Utf8>, List<Boolean> and
+    List<List<Boolean>> leaves."""
+    name_age = struct([leaf("binary", True, "name", large=True), leaf("i32", True, "age")], False)
+    name_age_item = struct([leaf("binary", True, "name", large=True), leaf("i32", True, "age")], True, "item")
+    kv = lambda n: map_(leaf("i32", False, "key"), leaf("binary", True, "value", large=True), n)  # noqa: E731
+    int_list = lambda n, name="": lst(leaf("i32", True, "item"), n, name)  # noqa: E731
+    cases = {
+        "test_struct": (name_age, _create_struct(1000, 0.2, 1000, rng)),
+        "test_map": (kv(True), _create_map(1000, 0.2, rng)),
+        "test_list_list": (lst(int_list(True, "item"), False), _stride2(_create_list(2000, 0.2, rng))),
+        "test_list_struct": (lst(name_age_item, False), _stride2(_create_struct(2000, 0.2, 2000, rng))),
+        "test_list_map": (lst(kv(True), False), _stride2(_create_map(2000, 0.2, rng))),
+        "test_struct_list": (struct([leaf("binary", True, "name", large=True), int_list(True, "age")], False),
+                             A("struct", 10000, None, children=[_rand_string(10000, 0.2, 10000, rng),
+                                                               _create_list(10000, 0.2, rng)])),
+        "list_utf8": (lst(leaf("utf8", True, "item"), True),
+                      _create_list(3000, 0.2, rng, lambda m: _rand_string(m, 0.2, 50, rng))),
+        "list_bool": (lst(leaf("bool", True, "item"), True),
+                      _create_list(3000, 0.2, rng, lambda m: _rand_bool(m, 0.2, rng))),
+        "list_list_bool": (lst(lst(leaf("bool", False, "item"), True, "item"), True),
+                           _create_list(1500, 0.2, rng, lambda m: _create_list(
+                               m, 0.2, rng, lambda k: A("leaf", k, None, values=rng.random(k) < 0.3)))),
+    }
+    return cases
+
+
+def host_array(a: A):
+    """oracle.nest.A -> pa_amd.HostArray (the product writer's input)."""
+    import pa_amd
+
+    return pa_amd.HostArray(a.kind, a.length, a.validity, a.offsets, [host_array(c) for c in a.children], a.values)
+
+
+def _slice(a: A, b: int, e: int) -> A:
+    """Slots [b, e) of an array (children compacted to the slots they reach)."""
+    v = None if a.validity is None else np.asarray(a.validity)[b:e]
+    if a.kind == "leaf":
+        if isinstance(a.values, tuple):
+            offs, data = a.values
+            o = np.asarray(offs[b:e + 1], np.int64)
+            return A("leaf", e - b, v, values=(o - o[0], data[int(o[0]):int(o[-1])]))
+        return A("leaf", e - b, v, values=np.asarray(a.values)[b:e])
+    if a.kind == "struct":
+        return A("struct", e - b, v, children=[_slice(c, b, e) for c in a.children])
+    o = np.asarray(a.offsets[b:e + 1], np.int64)
+    return A(a.kind, e - b, v, offsets=o - o[0], children=[_slice(a.children[0], int(o[0]), int(o[-1]))])
+
+
+def compact(a: A) -> A:
+    """The array with every child cut to the slots its parent reaches (what
+    Arrow logical equality compares, e.g. io.rs's ListArray over the first
+    half of a longer child)."""
+    return _slice(a, 0, a.length)

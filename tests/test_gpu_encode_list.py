@@ -113,3 +113,30 @@ def test_device_list_encode_decodes(ctx):
     vals = gv.cpu().numpy().view(np.int32)[: len(child)]
     assert (vals[cv] == child[cv]).all()
     dec.close()
+
+
+def test_device_list_encode_largest_page_step(ctx):
+    """The largest page step the device List encoder takes (16384 rows):
+    k_enc_list_levels' row-prefix table is 65540 B of dynamic LDS, past
+    64 KiB."""
+    rng = np.random.default_rng(16384)
+    offs, lv, child, cv = make_lists(40000, rng)
+    check(ctx, offs, lv, child, cv, True, True, opts_for("adaptive", 16384))
+    check(ctx, offs, lv, child, cv, False, False, opts_for("lz4", 16384))
+
+
+def test_device_list_encode_refuses_decreasing_offsets(ctx):
+    """A decreasing offset pair -- at a page boundary or inside a page -- is an
+    argument error, as in the host writer, not a wrapped slot size."""
+    import pa_amd
+
+    rng = np.random.default_rng(3)
+    offs, lv, child, cv = make_lists(3000, rng)
+    for at in (1000, 1234):  # page boundary (page 1000) and inside a page
+        bad = offs.copy()
+        bad[at] = bad[at + 1] + 1
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        with pytest.raises(pa_amd.StrawboatError) as e:
+            pa_amd.encode_list_column_device(dev(bad), dev(child), dev(lv), dev(cv), True, True,
+                                             opts_for("plain", 1000), ctx)
+        assert e.value.status == 6

@@ -110,10 +110,27 @@ def test_rust_compat_keeps_the_reference_signatures():
 
 
 def test_rust_compat_checks_host_buffers_before_ffi():
-    """encode_array validates lengths, bitmaps and offsets before the unsafe
-    calls into the C encoder."""
+    """Every unsafe call into the C encoder is preceded (since the previous
+    FFI call) by checks of the lengths, bitmaps and offsets it will read
+    (ADVICE r03)."""
     src = open(COMPAT).read()
-    body = src[src.index("fn encode_array"):]
-    for call in ("sb_encode_column(", "sb_encode_binary_column(", "sb_encode_list_column("):
-        head = body[:body.index(call)]
-        assert "check_" in head[head.rfind("=>"):], call
+    for call in ("sb_encode_column(", "sb_encode_binary_column(", "sb_encode_list_column(",
+                 "sb_encode_nested_column("):
+        i = src.index("ffi::" + call)
+        prev = src.rfind("ffi::sb_", 0, i)
+        assert "check_" in src[prev + 1:i], call
+
+
+def test_rust_compat_host_array_is_arrow2_shaped():
+    """HostArray mirrors arrow2's array tree (PrimitiveArray / BooleanArray,
+    BinaryArray / Utf8Array, ListArray, StructArray, MapArray), so
+    NativeWriter::write takes the reference's nested chunks (io.rs:167-278);
+    a nested field goes leaf by leaf through sb_encode_nested_column."""
+    src = open(COMPAT).read()
+    enum = src[src.index("pub enum HostArray {"):]
+    enum = enum[:enum.index("\n}\n")]
+    for v in ("Primitive {", "Binary {", "List { offsets: Vec<i64>, validity: Option<Vec<u8>>, values: Box<HostArray>",
+              "Struct { values: Vec<HostArray>", "Map { offsets: Vec<i64>, validity: Option<Vec<u8>>, field: Box<HostArray>"):
+        assert v in enum, v
+    assert "fn leaf_arrays" in src and "ffi::sb_encode_nested_column(" in src
+    assert "encoded.into_iter().flatten()" in src  # one ColumnMeta per leaf column
