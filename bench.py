@@ -1044,7 +1044,7 @@ class WorkloadC5:
         return ok
 
 
-TRAFFIC_FILE = "r05_pmc_traffic.json"  # tools/pmc_r03.sh -> tools/publish_traffic.py
+TRAFFIC_FILE = "r05_pmc_traffic.json"  # tools/pmc_traffic.sh -> tools/publish_traffic.py
 
 
 def load_traffic(workload: str):

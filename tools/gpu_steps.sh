@@ -1,4 +1,4 @@
-# Round-4 GPU session steps: bash tools/gpu_r04.sh <step> ...
+# GPU session steps: bash tools/gpu_steps.sh <step> ...
 #   tests "<pytest -k expr>" <files...>  : pytest subset (-m gpu), log under gpurun_out/
 #   c3ab "<lib ...>" [rows]              : tools/c3bench.py per library (PA_AMD_LIB)
 #   phases [rows]                        : tools/infphases.py on pa_amd/variants/libsb_phases.so
@@ -9,8 +9,8 @@ step=$1; shift
 case $step in
   tests)
     k=$1; shift
-    timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -k "$k" "$@" > gpurun_out/r04_tests.log 2>&1
-    rc=$?; tail -4 gpurun_out/r04_tests.log; exit $rc ;;
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -k "$k" "$@" > gpurun_out/steps_tests.log 2>&1
+    rc=$?; tail -4 gpurun_out/steps_tests.log; exit $rc ;;
   c3ab)
     for L in $1; do
       echo "== $L"

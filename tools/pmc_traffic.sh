@@ -1,8 +1,8 @@
-# Round-3 HBM traffic evidence: FETCH_SIZE / WRITE_SIZE per kernel (separate
+# HBM traffic evidence: FETCH_SIZE / WRITE_SIZE per kernel (separate
 # --pmc passes) and a kernel trace of the C2 headline, C3, C4 and C5 decodes
-# of this tree.  Outputs: gpurun_out/r03pmc/ (summaries: <wl>_traffic.json).
+# of this tree.  Outputs: $OUT (default gpurun_out/pmc/) (summaries: <wl>_traffic.json).
 set -o pipefail
-out=${OUT:-gpurun_out/r03pmc}
+out=${OUT:-gpurun_out/pmc}
 mkdir -p $out
 commit=${COMMIT:-unknown}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

@@ -1,4 +1,4 @@
-"""Publish one PMC run (tools/pmc_r03.sh output directory) into profiles/:
+"""Publish one PMC run (tools/pmc_traffic.sh output directory) into profiles/:
 python tools/publish_traffic.py <gpurun_out/r03pmc> <tag>.
 
 Writes profiles/<tag>_pmc_traffic.json -- one entry per bench.py workload
