@@ -772,7 +772,11 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 #ifndef SB_INF_WPB
 #define SB_INF_WPB 4
 #endif
+#ifdef SB_INF_RING2K  // 2 KiB rings, 512-byte chunks: 4.5 KiB of LDS a wave, eight waves a SIMD
+constexpr uint32_t kRing = 2048, kChunk = 512;
+#else
 constexpr uint32_t kRing = 4096, kChunk = 1024;
+#endif
 constexpr uint32_t kInfWaves = SB_INF_WPB;  // waves (jobs in flight) per k_inflate workgroup
 
 // Far-history reads re-read bytes this wave stored and waited for (vmcnt(0))
@@ -904,18 +908,21 @@ struct WaveOut {
         if (!skip0 || (c0 | w)) d32[w] = r32[slot(c0 + 4 * w) >> 2] + xadd;
       return;
     }
-    if (len == kChunk) {
-      const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(ring + slot(c0 + 16 * lane));
-      hib |= __ballot(((v.x | v.y | v.z | v.w) & 0x80808080u) != 0) != 0;
+    if (len == kChunk) {  // 16 bytes a lane (kChunk / 16 lanes)
+      const bool on = 16 * lane < kChunk;
+      const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(ring + slot(c0 + (on ? 16 * lane : 0)));
+      hib |= __ballot(on && ((v.x | v.y | v.z | v.w) & 0x80808080u) != 0) != 0;
       const uintptr_t al = (uintptr_t)d;
       if ((al & 15) == 0) {
-        ((u32x4*)d)[lane] = v;
+        if (on) ((u32x4*)d)[lane] = v;
       } else if ((al & 3) == 0) {
-        uint32_t* q = (uint32_t*)(d + 16 * lane);
-        q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
+        if (on) {
+          uint32_t* q = (uint32_t*)(d + 16 * lane);
+          q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
+        }
       } else {
 #pragma unroll
-        for (uint32_t j = 0; j < 16; j++) d[j * 64 + lane] = ring[slot(c0 + j * 64 + lane)];
+        for (uint32_t j = 0; j < kChunk / 64; j++) d[j * 64 + lane] = ring[slot(c0 + j * 64 + lane)];
       }
       return;
     }
@@ -965,20 +972,22 @@ struct WaveOut {
     gmem_u32* s32 = (gmem_u32*)((uintptr_t)src - sh);
     const uint32_t dal = (uint32_t)((uintptr_t)d & 15);
     if (xf && pos == 0) w0 = __builtin_amdgcn_alignbyte(s32[1], s32[0], sh);
-    for (uint32_t c = 0; c < n; c += 2 * kChunk) {
+    constexpr uint32_t B = 1024;  // 16 bytes a lane; n is a multiple of kChunk (<= B)
+    for (uint32_t c = 0; c < n; c += 2 * B) {
       uint32_t w[2][5];
 #pragma unroll
       for (uint32_t h = 0; h < 2; h++) {
-        const uint32_t x = c + h * kChunk + 16 * lane, i = (sh + x) >> 2;
-        const bool on = c + h * kChunk < n;
+        const uint32_t x = c + h * B + 16 * lane, i = (sh + x) >> 2;
+        const bool on = x < n;
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) w[h][k] = on ? s32[i + k] : 0u;
         w[h][4] = on && sh ? s32[i + 4] : 0u;  // the dword past byte x + 15 only when x is unaligned
       }
 #pragma unroll
       for (uint32_t h = 0; h < 2; h++) {
-        if (c + h * kChunk >= n) break;
-        const uint32_t x = c + h * kChunk + 16 * lane;
+        if (c + h * B >= n) break;
+        const uint32_t x = c + h * B + 16 * lane;
+        if (x >= n) continue;
         u32x4 v;
         v.x = __builtin_amdgcn_alignbyte(w[h][1], w[h][0], sh);
         v.y = __builtin_amdgcn_alignbyte(w[h][2], w[h][1], sh);
@@ -1525,8 +1534,13 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     INF_T(1);
     // 2. the chain of sequence starts from p, wave-parallel (wave_chain): a
     //    candidate that needs the serial path ends it
+#ifdef SB_INF_BPCHAIN  // the chain by ds_bpermute doubling: no LDS tables (k_inflate_lz4's 5 KiB a wave)
+    const uint32_t cx = wave_chain(t1);
+    const uint32_t j = (uint32_t)__popcll(__ballot(cx < kChainEnd && tab_at(t1, cx) != kChainStop));
+#else
     const uint32_t cx = lds_chain(in.ct, t1);
     const uint32_t j = (uint32_t)__popcll(__ballot(cx < kChainEnd && in.ct[cx] != kChainStop));
+#endif
     INF_T(2);
     const uint32_t starts = p + cx;
     // 3. decode and place
@@ -1564,6 +1578,26 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
 #ifdef SB_V_NOLIT
     if (v) s.lit = 0;
 #endif
+#ifdef SB_INF_EARLYFAR
+    // The free matches' sources are final before the batch (below d_first), and
+    // those below farlim are in HBM: their first dwords are loaded now, so the
+    // loads' latency passes under the literal copies.
+    const uint32_t d_first = __builtin_amdgcn_readfirstlane(dm);
+    const uint32_t src = dm - s.off;
+    const bool hazard = v && (src + s.ml > d_first || s.ml > kMatchFast);
+    const bool freel = v && !hazard;
+    const uint32_t farlim = o.far_limit();
+    const bool mfar = src + s.ml <= farlim, mnear = src >= farlim;
+    const bool fw = freel && (mfar || mnear);
+    const uint32_t fa = mfar ? src + o.dal : src, fsh = fa & 3, fa0 = fa - fsh, fneed = fw ? fsh + s.ml : 0u;
+    constexpr uint32_t kEarly = 3;
+    uint32_t pw[kEarly];
+#pragma unroll
+    for (uint32_t t = 0; t < kEarly; t++) {
+      const bool need = fw && mfar && 4 * t < fneed;
+      pw[t] = __ballot(need) ? o.far32(fa0 + 4 * t, need) : 0u;
+    }
+#endif
     // literals, 16 bytes per lane per step: source dwords from the input ring,
     // one masked dword store per destination word
     for (uint32_t c = 0; __ballot(v && c < s.lit); c += 16) {
@@ -1576,6 +1610,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
       }
     }
     INF_T(4);
+#ifndef SB_INF_EARLYFAR
     const uint32_t d_first = __builtin_amdgcn_readfirstlane(dm);
     const uint32_t src = dm - s.off;
 #ifdef SB_V_NOHAZ
@@ -1596,6 +1631,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     const bool mfar = src + s.ml <= farlim, mnear = src >= farlim;
     const bool fw = freel && (mfar || mnear);
     const uint32_t fa = mfar ? src + o.dal : src, fsh = fa & 3, fa0 = fa - fsh, fneed = fw ? fsh + s.ml : 0u;
+#endif
     if (__ballot(fw)) {
       constexpr uint32_t NW = kMatchFast / 4 + 1;
       uint32_t w[NW];
@@ -1603,8 +1639,22 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
       for (uint32_t t = 0; t < NW; t++) {
         w[t] = 0;
         if (!__ballot(4 * t < fneed)) continue;
+#ifdef SB_INF_EARLYFAR
+        // ring sources now (this batch's literals are in); far dwords past the
+        // early ones loaded here, only when some lane needs them
+        const bool nr = !mfar && 4 * t < fneed;
+        const uint32_t r = __ballot(nr) ? r32[((fa0 + 4 * t) & (kRing - 1)) >> 2] : 0u;
+        uint32_t g;
+        if (t < kEarly) {
+          g = pw[t < kEarly ? t : 0];
+        } else {
+          const bool nf = mfar && 4 * t < fneed;
+          g = __ballot(nf) ? o.far32(fa0 + 4 * t, nf) : 0u;
+        }
+#else
         const uint32_t g = o.far32(fa0 + 4 * t, mfar && 4 * t < fneed);
         const uint32_t r = r32[((fa0 + 4 * t) & (kRing - 1)) >> 2];
+#endif
         w[t] = mfar ? g : r;
       }
       if (fw) ring_put<NW>(o.ring, dm, s.ml, fsh, w);
@@ -1623,6 +1673,44 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
     // the ring, <= 64 bytes) is one byte a lane; its ring positions and
     // length are packed per lane beforehand, so each takes one v_readlane.
     const bool hfast = hazard && s.ml <= 64 && s.off >= s.ml && src >= farlim;
+#ifdef SB_INF_HAZGROUP
+    // Consecutive fast hazards go as one group, one byte a lane: a member joins
+    // while the group's bytes fit the wave and its source lies outside the
+    // span of the group's destinations (every earlier byte it reads is then
+    // final), so a group costs one LDS read and one store instead of a pair
+    // per hazard.  Positions are packed relative to op - kRing (13 bits each:
+    // sources reach back at most the ring, destinations a chunk ahead).
+    const uint32_t rel0 = o.op - kRing;
+    const uint32_t hpack = hfast ? ((src - rel0) << 19) | ((dm - rel0) << 6) | (s.ml - 1) : 0u;
+    const uint64_t fastm = __ballot(hfast);
+    for (uint64_t hm = __ballot(hazard); hm;) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(hm);
+      if ((fastm >> l) & 1) {
+        uint32_t base = 0, gd0 = 0, gend = 0, rs = 0, rd = 0;
+        bool act = false;
+        while (hm && ((fastm >> __builtin_ctzll(hm)) & 1)) {
+          const uint32_t h = __builtin_amdgcn_readlane(hpack, (uint32_t)__builtin_ctzll(hm));
+          const uint32_t m = (h & 63u) + 1u, hs = h >> 19, hd = (h >> 6) & 0x1FFFu;
+          if (base) {
+            if (base + m > 64u || !(hs + m <= gd0 || hs >= gend)) break;
+          } else {
+            gd0 = hd;
+          }
+          if (lane >= base && lane < base + m) {
+            rs = hs + lane - base;
+            rd = hd + lane - base;
+            act = true;
+          }
+          base += m;
+          gend = hd + m;
+          hm &= hm - 1;
+        }
+        const uint32_t b = act ? (uint32_t)o.ring[(rs + rel0) & (kRing - 1)] : 0u;
+        if (act) o.ring[(rd + rel0) & (kRing - 1)] = (uint8_t)b;
+        continue;
+      }
+      hm &= hm - 1;
+#else
     const uint32_t hpack = ((src & (kRing - 1)) << 20) | ((dm & (kRing - 1)) << 8) | (hfast ? s.ml : 0u);
     const uint64_t fastm = __ballot(hfast);
     for (uint64_t hm = __ballot(hazard); hm; hm &= hm - 1) {
@@ -1633,6 +1721,7 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
           o.ring[((h >> 8) + lane) & (kRing - 1)] = o.ring[((h >> 20) + lane) & (kRing - 1)];
         continue;
       }
+#endif
       const uint32_t D = __builtin_amdgcn_readlane(dm, l), O = __builtin_amdgcn_readlane(s.off, l),
                      M = __builtin_amdgcn_readlane(s.ml, l);
       for (uint32_t c = 0; c < M; c += 64) {
@@ -2527,12 +2616,20 @@ static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
 // workgroup, so 8 waves per SIMD can be resident and the serial token streams
 // of many pages overlap.
 #ifndef SB_INF_BLOCKS
+#ifdef SB_INF_RING2K
+#define SB_INF_BLOCKS 8  // 4-wave workgroups: 8 waves per SIMD (4.5 KiB of LDS and <= 64 VGPRs a wave)
+#else
 #define SB_INF_BLOCKS 6  // 4-wave workgroups: 6 waves per SIMD (6.5 KiB of LDS and <= 80 VGPRs a wave)
+#endif
 #endif
 __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(InflateLaunch a) {
   __shared__ u32x4 rings[kInfWaves][kRing / 16];
   __shared__ u32x4 ibufs[kInfWaves][kIb / 16];
+#ifdef SB_INF_BPCHAIN
+  u32x4* const ctabs[kInfWaves] = {};
+#else
   __shared__ u32x4 ctabs[kInfWaves][kChainTabs * 256 / 16];
+#endif
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = a.count ? *a.count : a.n_jobs;

@@ -734,6 +734,7 @@ __device__ __forceinline__ uint32_t zstd_frame_wave(const uint8_t* src, uint32_t
   uint32_t op = 0;
   if (len == 0 && lane == 0) op = sbz::zstd_empty(frame);
   if (len && lane == 0) op = sbz::zstd_frame_header(frame, len);
+  sbz::ZRep rep{{1, 4, 8}};  // (lane 0's)
   for (uint32_t off = 0; off < len; off += sbz::kZChunk) {
     const uint32_t cl = min(len - off, sbz::kZChunk);
     for (uint32_t i = lane; i < 4096; i += 64) ((uint32_t*)tab)[i] = 0;
@@ -741,7 +742,7 @@ __device__ __forceinline__ uint32_t zstd_frame_wave(const uint8_t* src, uint32_t
     __builtin_amdgcn_wave_barrier();
     const uint32_t r = sbc::lz4_compress_wave(sbc::Lz4GSrc{src + off}, cl, tmp, tab);
     __threadfence();  // the parse's stores, visible to lane 0
-    if (lane == 0) op += sbz::zstd_transcode(tmp, r, src + off, cl, frame + op, (uint64_t*)tab, off + cl == len);
+    if (lane == 0) op += sbz::zstd_transcode(tmp, r, src + off, cl, frame + op, (uint64_t*)tab, off + cl == len, rep);
     __threadfence();
     __builtin_amdgcn_wave_barrier();
   }

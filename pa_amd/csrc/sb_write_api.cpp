@@ -57,11 +57,12 @@ uint64_t sb_zstd_compress_host(const uint8_t* src, uint64_t n, uint8_t* dst) {
   std::vector<uint8_t> table(sbc::kLz4TableBytes), lz(sbc::lz4_bound(sbz::kZChunk));
   std::vector<uint64_t> recs(sbz::kZScratchU64);
   uint64_t op = sbz::zstd_frame_header(dst, (uint32_t)n);
+  sbz::ZRep rep{{1, 4, 8}};
   for (uint64_t off = 0; off < n; off += sbz::kZChunk) {
     const uint32_t cl = (uint32_t)std::min<uint64_t>(sbz::kZChunk, n - off);
     std::fill(table.begin(), table.end(), 0);
     const uint32_t ll = sbc::lz4_compress(src + off, cl, lz.data(), table.data());
-    op += sbz::zstd_transcode(lz.data(), ll, src + off, cl, dst + op, recs.data(), off + cl == n);
+    op += sbz::zstd_transcode(lz.data(), ll, src + off, cl, dst + op, recs.data(), off + cl == n, rep);
   }
   return op;
 }
