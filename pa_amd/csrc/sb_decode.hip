@@ -1522,25 +1522,31 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
   uint64_t tph = __builtin_amdgcn_s_memtime();
   INF_N(13, 1);
 #endif
-  while (p < pend && !ended) {
-    in.slide(p);
-    INF_T(0);
+  // the chain of the batch at p: found at the loop's top, or (SB_INF_PIPE)
+  // by the previous batch while its far loads were in flight
+  uint32_t cx = 0, j = 0;
+  bool have = false;
+  // 1. successor distances of the candidate starts x = p + 4 lane + k, from
+  //    the token and at most one extension byte per length: the tokens are
+  //    one unaligned dword of the ring, the literal extensions the next
+  //    bytes; only a match-length extension needs its own byte read;
+  // 2. the chain of sequence starts from p, wave-parallel: a candidate that
+  //    needs the serial path ends it
+  auto chain_at = [&](uint32_t q) {
+    in.slide(q);
     const uint32_t lim = min(in.base + kIb, pend);
-    // 1. successor distances of the candidate starts x = p + 4 lane + k, from
-    //    the token and at most one extension byte per length: the tokens are
-    //    one unaligned dword of the ring, the literal extensions the next
-    //    bytes; only a match-length extension needs its own byte read
-    const uint32_t t1 = cand_steps(in.ib, p, lim, pend);
-    INF_T(1);
-    // 2. the chain of sequence starts from p, wave-parallel (wave_chain): a
-    //    candidate that needs the serial path ends it
-#ifdef SB_INF_BPCHAIN  // the chain by ds_bpermute doubling: no LDS tables (k_inflate_lz4's 5 KiB a wave)
-    const uint32_t cx = wave_chain(t1);
-    const uint32_t j = (uint32_t)__popcll(__ballot(cx < kChainEnd && tab_at(t1, cx) != kChainStop));
+    const uint32_t t1 = cand_steps(in.ib, q, lim, pend);
+#ifdef SB_INF_BPCHAIN  // the chain by ds_bpermute doubling: no LDS tables
+    cx = wave_chain(t1);
+    j = (uint32_t)__popcll(__ballot(cx < kChainEnd && tab_at(t1, cx) != kChainStop));
 #else
-    const uint32_t cx = lds_chain(in.ct, t1);
-    const uint32_t j = (uint32_t)__popcll(__ballot(cx < kChainEnd && in.ct[cx] != kChainStop));
+    cx = lds_chain(in.ct, t1);
+    j = (uint32_t)__popcll(__ballot(cx < kChainEnd && in.ct[cx] != kChainStop));
 #endif
+  };
+  while (p < pend && !ended) {
+    if (!have) chain_at(p);
+    have = false;
     INF_T(2);
     const uint32_t starts = p + cx;
     // 3. decode and place
@@ -1609,6 +1615,14 @@ __device__ uint32_t lz4_inflate(InRing& in, uint32_t p, uint32_t pend, WaveOut<t
         ring_put<5>(o.ring, dl + c, n, sh, w);
       }
     }
+#ifdef SB_INF_PIPE
+    // the next batch's candidates and chain, under the far loads' latency (the
+    // literals are in the output ring: the input ring may slide)
+    if (pnext < pend) {
+      chain_at(pnext);
+      have = true;
+    }
+#endif
     INF_T(4);
 #ifndef SB_INF_EARLYFAR
     const uint32_t d_first = __builtin_amdgcn_readfirstlane(dm);
@@ -2085,7 +2099,11 @@ __device__ __forceinline__ void decode_values(const Src& s, const LSrc& ls, Shar
   const uint32_t tid = threadIdx.x;
   const uint32_t n = pd.num_values;
   uint8_t* obase = a.out_values + pd.row_off * W;
+#ifdef SB_VEC_DWORD  // quads of 4- and 8-byte values as one 16-byte store at any dword alignment
+  GSink<W> out{obase, W >= 4 ? ((uintptr_t)obase & 3) == 0 : ((uintptr_t)obase & (uintptr_t)(4 * W - 1)) == 0};
+#else
   GSink<W> out{obase, ((uintptr_t)obase & (uintptr_t)(W == 8 ? 15 : 4 * W - 1)) == 0};
+#endif
   const uint32_t chain = sh.chain;
   const Stream leaf = sh.sub;
   const uint32_t k = sh.dict_k, doff = sh.dict_off;
