@@ -218,23 +218,29 @@ def timed(torch, dist, wl: Workload, steps: int, warmup: int):
         wl.step(k)
     torch.cuda.synchronize()
     ok = wl.verify(torch)
-    # HIP events on the launch stream (the context launches on torch's current
-    # stream) between the steps: one device-clock duration per step (the
-    # median is reported); the host wall clock brackets all of
-    # them for ms_per_step
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    # The timed region: `steps` steps back to back, bracketed by a barrier and
+    # a device synchronize (ms_per_step).  Then the same number of steps with a
+    # HIP event on the launch stream (the context launches on torch's current
+    # stream) after each: one device-clock duration per step, whose median is
+    # reported.  The events are kept out of the timed region: an
+    # event between two steps is a barrier on the queue, 3-5 us a step on the
+    # device (tools/evgap.py), which no decode pays.
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    for k in range(steps):
+        wl.step(k)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     evs[0].record()
     for k in range(steps):
         wl.step(k)
         evs[k + 1].record()
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
     for d in wl.decs:
         d.check()
     kern_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(steps)]
@@ -464,13 +470,16 @@ class StreamSet:
     """Independent columns decode concurrently (the reference decodes columns
     independently too, read/deserialize.rs:237-253): each column's context
     launches on one of `n` side streams, forked from and joined back into the
-    current stream every step, so the HIP events of timed() span all of them."""
+    current stream every step, so the HIP events of timed() span all of them.
+    mode "own": each context on a HIP stream of its own (pa.Context.use_own_stream),
+    each on a hardware queue of its own; "torch": torch's pooled side streams,
+    which may share one hardware queue -- then the columns run one after
+    the other (C3: 4.46 vs 3.96 ms/step, tools/wlstreams.py)."""
 
-    def __init__(self, torch, pa, device, n):
+    def __init__(self, torch, pa, device, n, mode="torch"):
         self.torch = torch
         self.ctxs = [pa.Context(device) for _ in range(n)]
-        if os.environ.get("SB_BENCH_STREAMS", "torch") == "own":
-            # each context on its own HIP stream (pa.Context.use_own_stream):
+        if os.environ.get("SB_BENCH_STREAMS", mode) == "own":
             # measured slower for C5 (3.39 vs 2.74 ms/step) -- the four
             # streams then run on four hardware queues at once and the LZ4 /
             # Patas units contend with the rest
@@ -559,7 +568,10 @@ class WorkloadC3:
         dev = f"cuda:{device}"
         fh = torch.from_numpy(np.frombuffer(self.fchunk, np.uint8).copy())
         sh = torch.from_numpy(np.frombuffer(self.schunk, np.uint8).copy())
-        self.ss = StreamSet(torch, pa, device, 2)  # Float64 and Utf8 columns on their own streams
+        # Float64 and Utf8 columns on streams of their own: the second column's
+        # k_inflate waves take the wave slots the first one's leave as its
+        # job queue drains
+        self.ss = StreamSet(torch, pa, device, 2, mode="own")
         fd, sd = [fh.to(dev) for _ in range(2)], [sh.to(dev) for _ in range(2)]
         torch.cuda.synchronize()
         self.fdec = [pa.ColumnDecoder.for_shard(fd[i], self.fmetas, self.fcol.shard, np.float64, True, ctx=self.ss.ctxs[0])

@@ -92,6 +92,7 @@ struct sb_plan {
   sb_list_desc ldesc{};
   uint8_t* d_lc = nullptr;  // list state, see list_state_bytes
   bool list_peek = false;   // sizes from the page headers (checked against the levels at plan time)
+  uint16_t list_epoch = 0;  // tag of the last decode's block totals (k_list_bases)
   sb_plan* inner = nullptr;
   uint64_t n_leaves = 0;
   int offset_width = 0;
@@ -859,6 +860,7 @@ static sb_status list_launch(sb_ctx* ctx, sb_plan* p, const sb_list_out* out, in
                    out ? (uint32_t*)out->d_leaf_validity : nullptr, p->d_status};
   if (out && p->ldesc.list_nullable) L.zw_list = (p->n_rows + 31) / 32;
   if (out && p->ldesc.item_nullable) L.zw_leaf = (p->n_leaves + 31) / 32;
+  L.epoch = p->list_epoch;
   if (sb::launch_list(stage, L, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "list launch failed: %s", hipGetErrorString(hipGetLastError()));
   return SB_OK;
@@ -978,8 +980,10 @@ sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* p, const sb_list_out* out
     // stream, 242 vs 214 us, the kernels contend for the same CUs; a walk
     // with one wave per 2048-level step, 113-119 vs 108 us.)
     sb_status lst = p->list_peek ? SB_OK : list_launch(ctx, p, out, 0, false);
-    if (!lst) lst = list_launch(ctx, p, out, 1, p->list_peek);
-    if (!lst) lst = list_launch(ctx, p, out, 3, p->list_peek);
+    if (!lst) {  // sizes + bases in one launch, this decode's tag on the block totals
+      p->list_epoch = (uint16_t)(p->list_epoch + 1) ? (uint16_t)(p->list_epoch + 1) : 1;
+      lst = list_launch(ctx, p, out, 4, p->list_peek);
+    }
     if (!lst) lst = list_launch(ctx, p, out, 2, p->list_peek);
     if (lst) return lst;
     sb_primitive_out vo{out->d_values ? out->d_values : out->d_offsets, nullptr};  // (no leaves: nothing written)

@@ -4637,7 +4637,8 @@ struct ListArgs {
   uint32_t* out_list_validity;
   uint32_t* out_leaf_validity;
   uint32_t* status;
-  uint64_t zw_list, zw_leaf;  // k_list_vbase: bitmap words to zero
+  uint64_t zw_list, zw_leaf;  // k_list_vbase / k_list_bases: bitmap words to zero
+  uint32_t epoch;             // k_list_bases: tag of this decode's block totals
 };
 
 // Header + run tables (one lane).
@@ -5191,6 +5192,97 @@ __global__ __launch_bounds__(NT) void k_list_vbase(ListArgs a) {
   }
 }
 
+// k_list_bscan + k_list_vbase in one launch (a decode's sizing, one kernel
+// boundary less).  Block b < nblk scans its NT pages' counts, publishes its
+// row / leaf totals as two words of blk tagged with a.epoch (top 16 bits),
+// and sums the totals of blocks 0..b-1 -- every predecessor's own total, no
+// inclusive prefixes, so no block waits on another's wait: the lower blocks
+// were dispatched first (workgroups launch in order on each XCD), each
+// publishes as soon as its scan is done.  A stale word (an earlier decode's
+// tag, or the plan's zeroed state) reads as not yet published.  Every block
+// zeroes its share of the bitmaps first.
+__global__ __launch_bounds__(NT) void k_list_bases(ListArgs a) {
+  __shared__ Shared sh;
+  __shared__ uint64_t red[2][NW];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  {  // zero the bitmaps, 16 B a thread per step
+    const uint64_t nt = (uint64_t)gridDim.x * NT, g = (uint64_t)blockIdx.x * NT + tid;
+    for (int m = 0; m < 2; m++) {
+      uint32_t* bm = m ? a.out_leaf_validity : a.out_list_validity;
+      const uint64_t nw = m ? a.zw_leaf : a.zw_list;
+      if (!bm || !nw) continue;
+      const uint64_t n4 = nw / 4;
+      for (uint64_t i = g; i < n4; i += nt) ((u32x4*)bm)[i] = u32x4{0, 0, 0, 0};
+      if (g < nw - 4 * n4) bm[4 * n4 + g] = 0;
+    }
+  }
+  const uint32_t nblk = (a.n_pages + NT - 1) / NT;
+  if (blockIdx.x >= nblk) return;
+  const uint32_t p = blockIdx.x * NT + tid;
+  uint64_t c = 0;
+  uint64_t vpos = ~0ull;
+  PageDesc pd{};
+  if (p < a.n_pages) {
+    if (a.peek) {
+      pd = a.pages[p];
+      const GlbSrc g{a.chunk + pd.byte_off};
+      if (pd.byte_len >= 12) {
+        vpos = 12ull + g.u32(4) + g.u32(8);
+        if (vpos + 9 <= pd.byte_len) c = ((uint64_t)g.u32(0) << 32) | (g.u32((uint32_t)vpos + 5) / a.width);
+      }
+      a.counts[p] = c;
+    } else {
+      c = a.counts[p];
+    }
+  }
+  uint64_t tr, tl;
+  const uint64_t er = block_excl_scan<uint64_t>(c >> 32, sh, &tr);
+  const uint64_t el = block_excl_scan<uint64_t>(c & 0xFFFFFFFFull, sh, &tl);
+  constexpr uint64_t kVal = (1ull << 48) - 1;
+  const uint64_t tag = (uint64_t)a.epoch << 48;
+  if (tid == 0) {
+    __hip_atomic_store(&a.blk[2 * blockIdx.x], tag | tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.blk[2 * blockIdx.x + 1], tag | tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (wv == 0) {  // the totals of blocks 0..b-1, 64 blocks a probe
+    uint64_t br = 0, bl = 0;
+    for (uint32_t b0 = 0; b0 < blockIdx.x; b0 += 64) {
+      const uint32_t b = b0 + lane;
+      const bool need = b < blockIdx.x;
+      uint64_t r = 0, l = 0;
+      for (;;) {
+        if (need) {
+          r = __hip_atomic_load(&a.blk[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          l = __hip_atomic_load(&a.blk[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!__ballot(need && ((r & ~kVal) != tag || (l & ~kVal) != tag))) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (need) {
+        br += r & kVal;
+        bl += l & kVal;
+      }
+    }
+    br = wave_sum64(br);
+    bl = wave_sum64(bl);
+    if (lane == 0) {
+      red[0][0] = br;
+      red[1][0] = bl;
+    }
+  }
+  __syncthreads();
+  if (p < a.n_pages) {
+    const uint64_t rbase = red[0][0] + er, lbase = red[1][0] + el;
+    a.local[2 * p] = rbase;
+    a.local[2 * p + 1] = lbase;
+    if (a.peek) {
+      const bool ok = vpos + 9 <= pd.byte_len;
+      a.vpages[p] = PageDesc{pd.byte_off + (ok ? vpos : 0), lbase, ok ? pd.byte_len - (uint32_t)vpos : 0,
+                             ok ? (uint32_t)c : 0, a.vpages[p].reserved};
+    }
+  }
+}
+
 // Levels pass: one wave per page, at the global bases k_list_vbase wrote.
 // Writes offsets and both bitmaps, its status, and (unless the values
 // descriptors came from the headers) the page's values-stream descriptor;
@@ -5687,7 +5779,7 @@ namespace sb {
 int launch_list(int stage, const ListLaunch& L, void* stream) {
   sbk::ListArgs a{L.chunk, L.pages, L.n_pages, L.list_nullable, L.item_nullable, L.offset_width, L.width, L.peek,
                   L.counts, L.local, L.blk, L.totals, (uint4*)L.lvdesc, L.vpages, L.out_offsets, L.out_list_validity,
-                  L.out_leaf_validity, L.status, L.zw_list, L.zw_leaf};
+                  L.out_leaf_validity, L.status, L.zw_list, L.zw_leaf, L.epoch};
   if (L.n_pages == 0) return 0;
   const uint32_t grid = std::min<uint32_t>((L.n_pages + sbk::NW - 1) / sbk::NW, kListGrid);
   const uint32_t nblk = (L.n_pages + sbk::NT - 1) / sbk::NT;
@@ -5696,10 +5788,11 @@ int launch_list(int stage, const ListLaunch& L, void* stream) {
     hipLaunchKernelGGL(sbk::k_list_size, dim3(grid), dim3(sbk::NT), 0, st, a);
   } else if (stage == 1) {  // block bases (+ header sizing when peek)
     hipLaunchKernelGGL(sbk::k_list_bscan, dim3(nblk), dim3(sbk::NT), 0, st, a);
-  } else if (stage == 3) {  // global bases, values descriptors (peek), zeroed bitmaps
+  } else if (stage == 3 || stage == 4) {  // global bases, values descriptors (peek), zeroed bitmaps
     const uint64_t zw = std::max(L.zw_list, L.zw_leaf);
     const uint32_t zg = (uint32_t)std::min<uint64_t>((zw / 4 + sbk::NT - 1) / sbk::NT, 1024);
-    hipLaunchKernelGGL(sbk::k_list_vbase, dim3(std::max(nblk, zg)), dim3(sbk::NT), 0, st, a);
+    if (stage == 3) hipLaunchKernelGGL(sbk::k_list_vbase, dim3(std::max(nblk, zg)), dim3(sbk::NT), 0, st, a);
+    else hipLaunchKernelGGL(sbk::k_list_bases, dim3(std::max(nblk, zg)), dim3(sbk::NT), 0, st, a);
   } else {
     hipLaunchKernelGGL(sbk::k_list_levels, dim3(grid), dim3(sbk::NT), 0, st, a);
   }

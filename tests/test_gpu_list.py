@@ -90,6 +90,26 @@ def test_list_ragged_pages(ctx, page_rows):
     check(ctx, offs, lv, child, cv, True, True, page_rows, O.WriteOptions.make(ratio=1.2))
 
 
+def test_list_repeated_decodes_multi_block(ctx):
+    """k_list_bases tags each decode's block totals: one plan of 1 250 pages
+    (five blocks exchanging totals) decoded again and again gives the
+    oracle's arrays every time."""
+    import pa_amd
+
+    rng = np.random.default_rng(12)
+    offs, lv, child, cv = make_lists(20000, rng)
+    chunk, metas, _ = O.write_list_column(offs, lv, child, cv, True, True, 16, O.WriteOptions.make(ratio=1.2))
+    eo, el, ev, ef = O.read_list_column(chunk, metas, child.dtype, True, True)
+    dec = pa_amd.ListColumnDecoder(chunk, [pa_amd.PageMeta(l, n) for l, n in metas], np.int32, True, True, ctx)
+    unpack = lambda b, n: np.unpackbits(b.cpu().numpy(), bitorder="little")[:n].astype(bool)  # noqa: E731
+    for _ in range(5):
+        go, gl, gv, gf = dec.decode()
+        assert (go.cpu().numpy().astype(np.int64) == eo).all()
+        assert (unpack(gl, dec.num_rows) == el).all() and (unpack(gf, dec.num_leaves) == ef).all()
+        assert gv.cpu().numpy().view(np.uint8)[: 4 * dec.num_leaves].tobytes() == ev.tobytes()
+    dec.close()
+
+
 def test_list_long_lists_multi_tile(ctx):
     """Pages with many levels per row: several level tiles per page; the
     level streams exceed the LDS stage and are read from HBM."""

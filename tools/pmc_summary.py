@@ -56,7 +56,7 @@ def tag(names):
 
 def main():
     wl, fcsv, wcsv, bjson, out, commit = sys.argv[1:7]
-    rnd = int(sys.argv[7]) if len(sys.argv) > 7 else int(os.environ.get("SB_ROUND", "5"))
+    rnd = int(sys.argv[7]) if len(sys.argv) > 7 else int(os.environ.get("SB_ROUND", "6"))
     by = json.load(open(bjson))
     f, fn = per_dispatch(fcsv, "FETCH_SIZE")
     w, wn = per_dispatch(wcsv, "WRITE_SIZE")
