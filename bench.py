@@ -198,13 +198,13 @@ class Workload:
 
 def step_clocks(wall_s: float, kern_ms, step_bytes: int) -> dict:
     """A workload's step time on both clocks: the host wall clock over the
-    timed steps (ms_per_step) and the median of the per-step HIP-event
-    durations (kernel_ms_median), each with the roofline fraction of the
+    timed steps (ms_per_step) and the HIP-event span of the same steps per
+    step (kernel_ms_per_step), each with the roofline fraction of the
     step's algorithmic bytes on that clock."""
     km = float(np.median(kern_ms))
     return {
         "ms_per_step": round(wall_s * 1e3, 3),
-        "kernel_ms_median": round(km, 4),
+        "kernel_ms_per_step": round(km, 4),
         "step_traffic_GBps": round(step_bytes / (km / 1e3) / 1e9, 1),
         "roofline_frac": round(step_bytes / (km / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
         "roofline_frac_wall": round(step_bytes / wall_s / 1e9 / HBM_PEAK_GBPS, 4),
@@ -219,31 +219,28 @@ def timed(torch, dist, wl: Workload, steps: int, warmup: int):
     torch.cuda.synchronize()
     ok = wl.verify(torch)
     # The timed region: `steps` steps back to back, bracketed by a barrier and
-    # a device synchronize (ms_per_step).  Then the same number of steps with a
-    # HIP event on the launch stream (the context launches on torch's current
-    # stream) after each: one device-clock duration per step, whose median is
-    # reported.  The events are kept out of the timed region: an
-    # event between two steps is a barrier on the queue, 3-5 us a step on the
-    # device (tools/evgap.py), which no decode pays.
+    # a device synchronize (ms_per_step), with a HIP event on the launch
+    # stream (the context launches on torch's current stream) before the first
+    # and after the last step: their device-clock span / steps is the step's
+    # device time.  No event between steps: each one is a barrier on the
+    # queue, 3-10 us a step on the device (tools/evgap.py), which no decode
+    # pays.
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record()
     for k in range(steps):
         wl.step(k)
+    e1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
-    evs[0].record()
-    for k in range(steps):
-        wl.step(k)
-        evs[k + 1].record()
-    torch.cuda.synchronize()
     for d in wl.decs:
         d.check()
-    kern_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(steps)]
+    kern_ms = [e0.elapsed_time(e1) / steps]
     return t1 - t0, kern_ms, ok
 
 
@@ -471,15 +468,26 @@ class StreamSet:
     independently too, read/deserialize.rs:237-253): each column's context
     launches on one of `n` side streams, forked from and joined back into the
     current stream every step, so the HIP events of timed() span all of them.
-    mode "own": each context on a HIP stream of its own (pa.Context.use_own_stream),
-    each on a hardware queue of its own; "torch": torch's pooled side streams,
-    which may share one hardware queue -- then the columns run one after
-    the other (C3: 4.46 vs 3.96 ms/step, tools/wlstreams.py)."""
+    mode "torch": torch's pooled side streams; "own": each context on a HIP
+    stream of its own (pa.Context.use_own_stream); "prio": torch side streams,
+    the last at high priority.  Streams of equal priority may share one
+    hardware queue, and then the columns run one after the other: C3 took
+    4.46 ms/step on torch streams and 3.96 on its own ones in one process
+    (tools/wlstreams.py), 4.0 and 4.5 in the bench's, after other workloads had
+    created their streams."""
 
     def __init__(self, torch, pa, device, n, mode="torch"):
         self.torch = torch
         self.ctxs = [pa.Context(device) for _ in range(n)]
-        if os.environ.get("SB_BENCH_STREAMS", mode) == "own":
+        mode = os.environ.get("SB_BENCH_STREAMS", mode)
+        if mode == "prio":
+            # torch side streams, the last one at high priority: a queue of its
+            # own (priority is a property of the hardware queue), and its
+            # column's small kernels dispatch ahead of the other's inflate waves
+            self.streams = [torch.cuda.Stream(device=device, priority=-1 if i == n - 1 else 0) for i in range(n)]
+            for c, st in zip(self.ctxs, self.streams):
+                c.use_stream(st)
+        elif mode == "own":
             # measured slower for C5 (3.39 vs 2.74 ms/step) -- the four
             # streams then run on four hardware queues at once and the LZ4 /
             # Patas units contend with the rest
@@ -571,7 +579,7 @@ class WorkloadC3:
         # Float64 and Utf8 columns on streams of their own: the second column's
         # k_inflate waves take the wave slots the first one's leave as its
         # job queue drains
-        self.ss = StreamSet(torch, pa, device, 2, mode="own")
+        self.ss = StreamSet(torch, pa, device, 2, mode="prio")
         fd, sd = [fh.to(dev) for _ in range(2)], [sh.to(dev) for _ in range(2)]
         torch.cuda.synchronize()
         self.fdec = [pa.ColumnDecoder.for_shard(fd[i], self.fmetas, self.fcol.shard, np.float64, True, ctx=self.ss.ctxs[0])
@@ -1056,7 +1064,7 @@ class WorkloadC5:
         return ok
 
 
-TRAFFIC_FILE = "r05_pmc_traffic.json"  # tools/pmc_traffic.sh -> tools/publish_traffic.py
+TRAFFIC_FILE = "r06_pmc_traffic.json"  # tools/pmc_traffic.sh -> tools/publish_traffic.py
 
 
 def load_traffic(workload: str):
@@ -1239,7 +1247,7 @@ def main():
 
     if not args.no_c4:
         wl4 = WorkloadC4(torch, pa_amd, args.c4_rows, 99, local, threads, dist, world, rank)
-        steps4 = max(3, args.steps // 2)
+        steps4 = max(3, 2 * args.steps)  # 0.15 ms steps: the timed region's fixed costs spread over more of them
         w4, k4, ok4 = timed(torch, dist, wl4, steps4, args.warmup)
         w4m = reduce(w4, MAX)
         extra["c4_list_int32_nested"] = {
@@ -1335,7 +1343,7 @@ def main():
                 "traffic": load_traffic("c2_int32_adaptive_bitpack_dict"),
                 "kernel": "k_decode_staged<4,false>",
                 "kernel_ms": round(kavg, 4),
-                "kernel_clock": "median of the per-step HIP-event durations on the launch stream",
+                "kernel_clock": "HIP events on the launch stream before the first and after the last timed step, span / steps",
                 "frac_wall": round((wl.in_bytes + wl.out_bytes) / (wall_max / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
                 "bytes_per_launch": wl.in_bytes + wl.out_bytes,
             },
