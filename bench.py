@@ -1262,7 +1262,7 @@ def main():
             "parallelism": f"page-shard x{world} of one column (shard_pages / for_shard); leaf base {wl4.leaf_base} "
                            f"from the all-gathered leaf counts",
             "traffic": load_traffic("c4_list_int32_nested"),
-            "kernels": "k_list_bscan + k_list_vbase + k_list_levels + k_decode_staged<4,false>",
+            "kernels": "k_list_bases + k_list_levels + k_decode_staged<4,false>",
         }
         if do_cpu:
             extra["c4_list_int32_nested"]["cpu_baseline"] = wl4.cpu_baseline()

@@ -772,10 +772,10 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 #ifndef SB_INF_WPB
 #define SB_INF_WPB 4
 #endif
-#ifdef SB_INF_RING2K  // 2 KiB rings, 512-byte chunks: 4.5 KiB of LDS a wave, eight waves a SIMD
-constexpr uint32_t kRing = 2048, kChunk = 512;
-#else
+#ifdef SB_INF_RING4K  // (before round 6) 4 KiB rings, 1 KiB chunks: 6.5 KiB of LDS a wave, six waves a SIMD
 constexpr uint32_t kRing = 4096, kChunk = 1024;
+#else  // 2 KiB rings, 512-byte chunks: 4.5 KiB of LDS a wave, eight waves a SIMD
+constexpr uint32_t kRing = 2048, kChunk = 512;
 #endif
 constexpr uint32_t kInfWaves = SB_INF_WPB;  // waves (jobs in flight) per k_inflate workgroup
 
@@ -2626,10 +2626,10 @@ static int launch(int kind, const LaunchArgs& a, hipStream_t stream) {
 // workgroup, so 8 waves per SIMD can be resident and the serial token streams
 // of many pages overlap.
 #ifndef SB_INF_BLOCKS
-#ifdef SB_INF_RING2K
-#define SB_INF_BLOCKS 8  // 4-wave workgroups: 8 waves per SIMD (4.5 KiB of LDS and <= 64 VGPRs a wave)
-#else
+#ifdef SB_INF_RING4K
 #define SB_INF_BLOCKS 6  // 4-wave workgroups: 6 waves per SIMD (6.5 KiB of LDS and <= 80 VGPRs a wave)
+#else
+#define SB_INF_BLOCKS 8  // 4-wave workgroups: 8 waves per SIMD (4.5 KiB of LDS and <= 64 VGPRs a wave)
 #endif
 #endif
 __global__ __launch_bounds__(64 * kInfWaves, SB_INF_BLOCKS) void k_inflate(InflateLaunch a) {
