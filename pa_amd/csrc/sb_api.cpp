@@ -858,8 +858,6 @@ static sb_status list_launch(sb_ctx* ctx, sb_plan* p, const sb_list_out* out, in
                    peek ? 1u : 0u, b, b + n, b + 3 * n, tot, tot + 2, p->inner->d_pages,
                    out ? (uint8_t*)out->d_offsets : nullptr, out ? (uint32_t*)out->d_list_validity : nullptr,
                    out ? (uint32_t*)out->d_leaf_validity : nullptr, p->d_status};
-  if (out && p->ldesc.list_nullable) L.zw_list = (p->n_rows + 31) / 32;
-  if (out && p->ldesc.item_nullable) L.zw_leaf = (p->n_leaves + 31) / 32;
   L.epoch = p->list_epoch;
   if (sb::launch_list(stage, L, ctx->stream))
     return fail(ctx, SB_E_DEVICE, "list launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -974,7 +972,7 @@ sb_status sb_decode_list_planned(sb_ctx* ctx, sb_plan* p, const sb_list_out* out
   if (!p->n_pages) {
     HIP_TRY(ctx, hipMemsetAsync(out->d_offsets, 0, (size_t)p->ldesc.offset_width, ctx->stream));
   } else {
-    // sizes (exact pass, or the headers), global bases + zeroed bitmaps, the
+    // sizes (exact pass, or the headers) and global bases in one launch, the
     // levels walk, then the values streams at their leaf bases.  (Measured
     // on C4 and not kept: the values decode beside the walk on a second
     // stream, 242 vs 214 us, the kernels contend for the same CUs; a walk

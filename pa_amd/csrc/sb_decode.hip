@@ -4637,7 +4637,6 @@ struct ListArgs {
   uint32_t* out_list_validity;
   uint32_t* out_leaf_validity;
   uint32_t* status;
-  uint64_t zw_list, zw_leaf;  // k_list_vbase / k_list_bases: bitmap words to zero
   uint32_t epoch;             // k_list_bases: tag of this decode's block totals
 };
 
@@ -4748,37 +4747,27 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 
-// n bits of an LDS bitmap (bit 0 at word 0) to global bit position row_off,
-// one wave: whole words stored, edge words merged with atomicOr (zeroed bitmap).
-__device__ void wave_write_bits(const uint32_t* bm, uint32_t n, uint64_t row_off, uint32_t* out) {
-  if (n == 0) return;
-  const LdsSrc s{bm, 0};
-  const uint64_t fw = row_off >> 5, lw = (row_off + n - 1) >> 5;
-  for (uint64_t w = fw + (threadIdx.x & 63); w <= lw; w += 64) {
-    const int64_t pb = (int64_t)(w * 32) - (int64_t)row_off;
-    uint32_t v = pb >= 0 ? (uint32_t)(s.u64((uint32_t)(pb >> 3)) >> (pb & 7)) : s.u32(0) << (uint32_t)(-pb);
-    const uint32_t lo = pb < 0 ? (uint32_t)(-pb) : 0u;
-    const int64_t hi_ex = (int64_t)n - pb;
-    const uint32_t hi = hi_ex >= 32 ? 32u : (uint32_t)hi_ex;
-    const uint32_t m = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1)) & (0xFFFFFFFFu << lo);
-    if (m == 0xFFFFFFFFu) out[w] = v;
-    else if (v & m) atomicOr(&out[w], v & m);
-  }
-}
-
 // n bits of an LDS bitmap (bit 0 at word 0, zero past n, one spare zero word
 // before it at bm[-1]) to global bit position g0: the shift is uniform over
 // the wave, so output word i is a funnel of bm[i - 1] and bm[i]; interior
-// words are stored, the two edge words merged with atomicOr.
+// words are stored.  An edge word, shared with the neighbouring range, gets
+// its own bits cleared (atomicAnd) and then set (atomicOr): the neighbour's
+// bits are never touched, so the bitmap needs no zeroing first.
 __device__ __forceinline__ void wave_put_bits(const uint32_t* bm, uint32_t n, uint64_t g0, uint32_t* out) {
   if (n == 0) return;
-  const uint32_t sh = (uint32_t)(g0 & 31), nw = (sh + n + 31) >> 5;
+  const uint32_t sh = (uint32_t)(g0 & 31), nw = (sh + n + 31) >> 5, eb = (sh + n) & 31;
   uint32_t* o = out + (g0 >> 5);
   for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {
     const uint32_t v = sh ? __builtin_amdgcn_alignbit(bm[i], bm[(int)i - 1], 32 - sh) : bm[i];
-    const bool edge = (i == 0 && sh) || (i == nw - 1 && ((sh + n) & 31));
-    if (edge) { if (v) atomicOr(&o[i], v); }
-    else o[i] = v;
+    const bool lo_edge = i == 0 && sh, hi_edge = i == nw - 1 && eb;
+    if (lo_edge || hi_edge) {
+      uint32_t m = lo_edge ? ~0u << sh : ~0u;
+      if (hi_edge) m &= (1u << eb) - 1;
+      atomicAnd(&o[i], ~m);
+      if (v) atomicOr(&o[i], v);
+    } else {
+      o[i] = v;
+    }
   }
 }
 
@@ -4794,15 +4783,11 @@ constexpr uint32_t kLvStep = 64 * kLvK;  // levels per wave step (2048)
 #ifndef SB_LV_ACC_BITS
 #define SB_LV_ACC_BITS 8192
 #endif
-#ifdef SB_LV_STEPBITS
-constexpr uint32_t kLvBitsW = kLvStep / 32 + 4;  // a step's bits, written out every step
-#else
 // The page's validity bits accumulate over its steps and go out once per
 // kLvAccBits (a C4 page: once), as whole words with two edge merges,
 // instead of a short partial-line write and two atomics every step.
 constexpr uint32_t kLvAccBits = SB_LV_ACC_BITS;
 constexpr uint32_t kLvBitsW = kLvAccBits / 32 + 2;
-#endif
 
 struct ListWave {
   ListShared ls;
@@ -4852,7 +4837,6 @@ __device__ __forceinline__ uint32_t compress32(uint32_t x, uint32_t m) {
 
 // The held validity bits to the bitmaps; the buffers zeroed again.
 __device__ __forceinline__ void lv_flush(ListWave& w, const ListArgs& a, LvAcc& acc) {
-#ifndef SB_LV_STEPBITS
   const uint32_t lane = threadIdx.x & 63;
 #ifndef SB_V_LV_NOBITS
   if (a.nl) wave_put_bits(w.lbits + 1, acc.r, acc.g0, a.out_list_validity);
@@ -4865,7 +4849,6 @@ __device__ __forceinline__ void lv_flush(ListWave& w, const ListArgs& a, LvAcc& 
   acc.g0 += acc.r;
   acc.v0 += acc.l;
   acc.r = acc.l = 0;
-#endif
 }
 
 // One step of kLvStep levels [t0, t0 + kLvStep) of a page, one wave, rows
@@ -4897,14 +4880,8 @@ __device__ uint32_t lv_step_m(const LvMasks m, WV& w, uint32_t rows, const ListA
     const uint32_t s_r0 = carry_r, s_l0 = carry_l;
     const uint64_t g0 = rbase + s_r0, v0 = lbase + s_l0;
     const uint32_t al = a.ow == 4 ? (uint32_t)(g0 & 3) : (uint32_t)(g0 & 1);  // obuf index of row 0
-#ifdef SB_LV_STEPBITS
-    for (uint32_t i = lane; i < kLvBitsW; i += 64) w.lbits[i] = w.fbits[i] = 0;
-    wave_sync();
-    const uint32_t pr = rb - s_r0, pf = lb - s_l0;
-#else
     if (acc.r + (tot >> 16) > kLvAccBits || acc.l + (tot & 0xFFFFu) > kLvAccBits) lv_flush(w, a, acc);
     const uint32_t pr = acc.r + rb - s_r0, pf = acc.l + lb - s_l0;
-#endif
     const uint32_t nr = __popc(rsm), nf = __popc(lfm);
     uint16_t* ob = w.obuf + al + (rb - s_r0);
     const uint32_t lrel = lb - s_l0;
@@ -4955,13 +4932,8 @@ __device__ uint32_t lv_step_m(const LvMasks m, WV& w, uint32_t rows, const ListA
         }
       }
     }
-#ifdef SB_LV_STEPBITS
-    if (a.nl) wave_put_bits(w.lbits + 1, tr, g0, a.out_list_validity);
-    if (a.ni) wave_put_bits(w.fbits + 1, tl, v0, a.out_leaf_validity);
-#else
     acc.r += tr;
     acc.l += tl;
-#endif
     wave_sync();
   }
   *step_r = tot >> 16;
@@ -4984,12 +4956,10 @@ __device__ void wave_levels(const Src& s, ListWave& w, const ListArgs& a, uint32
   const uint32_t lane = threadIdx.x & 63, rows = w.ls.rows;
   uint32_t carry_r = 0, carry_l = 0, leaves = 0;
   LvAcc acc{0, 0, rbase, lbase};
-#ifndef SB_LV_STEPBITS
   if constexpr (WRITE) {
     for (uint32_t i = lane; i < kLvBitsW; i += 64) w.lbits[i] = w.fbits[i] = 0;
     wave_sync();
   }
-#endif
   for (uint32_t t0 = 0; t0 < L; t0 += kLvStep) {
     uint32_t sr, sl;
     leaves += lv_step<WRITE>(s, w, w.ls, a, t0, L, rbase, lbase, carry_r, carry_l, &sr, &sl, acc);
@@ -4997,9 +4967,7 @@ __device__ void wave_levels(const Src& s, ListWave& w, const ListArgs& a, uint32
     carry_l += sl;
     if (carry_r > rows) break;  // uniform: every later level is past the last row
   }
-#ifndef SB_LV_STEPBITS
   if constexpr (WRITE) lv_flush(w, a, acc);
-#endif
   const uint32_t rc = min(carry_r, rows);
   if (lane == 0 && rc != rows) put_err(&w.err, ST_OUT_OF_SPEC);  // levels ended before `rows` rows
   *rows_c = rc;
@@ -5137,87 +5105,23 @@ __global__ __launch_bounds__(NT) void k_list_bscan(ListArgs a) {
   }
 }
 
-// Global bases: the page's in-block bases + the totals of the blocks before
-// it, written back over a.local.  With a.peek the page's values-stream
-// descriptor too (its header gives the stream's position, bscan the leaf
-// count), so the values decode needs nothing from k_list_levels and runs
-// beside it on another stream.  Every thread of the grid also zeroes its
-// share of the two validity bitmaps, which k_list_levels ORs into.
-__global__ __launch_bounds__(NT) void k_list_vbase(ListArgs a) {
-  __shared__ uint64_t red[2][NW];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint32_t nblk = (a.n_pages + NT - 1) / NT;
-  if (blockIdx.x < nblk) {
-    uint64_t br = 0, bl = 0;
-    for (uint32_t b = tid; b < blockIdx.x; b += NT) {
-      br += a.blk[2 * b];
-      bl += a.blk[2 * b + 1];
-    }
-    br = wave_sum64(br);
-    bl = wave_sum64(bl);
-    if (lane == 0) {
-      red[0][wv] = br;
-      red[1][wv] = bl;
-    }
-    __syncthreads();
-    br = bl = 0;
-    for (uint32_t k = 0; k < NW; k++) {
-      br += red[0][k];
-      bl += red[1][k];
-    }
-    const uint32_t p = blockIdx.x * NT + tid;
-    if (p < a.n_pages) {
-      const uint64_t rbase = br + a.local[2 * p], lbase = bl + a.local[2 * p + 1];
-      a.local[2 * p] = rbase;
-      a.local[2 * p + 1] = lbase;
-      if (a.peek) {
-        const PageDesc pd = a.pages[p];
-        const GlbSrc g{a.chunk + pd.byte_off};
-        const uint64_t vpos = pd.byte_len >= 12 ? 12ull + g.u32(4) + g.u32(8) : ~0ull;
-        const bool ok = vpos + 9 <= pd.byte_len;
-        a.vpages[p] = PageDesc{pd.byte_off + (ok ? vpos : 0), lbase, ok ? pd.byte_len - (uint32_t)vpos : 0,
-                               ok ? (uint32_t)a.counts[p] : 0, a.vpages[p].reserved};
-      }
-    }
-  }
-  // zero the bitmaps, 16 B a thread per step
-  const uint64_t nt = (uint64_t)gridDim.x * NT, g = (uint64_t)blockIdx.x * NT + tid;
-  for (int m = 0; m < 2; m++) {
-    uint32_t* bm = m ? a.out_leaf_validity : a.out_list_validity;
-    const uint64_t nw = m ? a.zw_leaf : a.zw_list;
-    if (!bm || !nw) continue;
-    const uint64_t n4 = nw / 4;
-    for (uint64_t i = g; i < n4; i += nt) ((u32x4*)bm)[i] = u32x4{0, 0, 0, 0};
-    if (g < nw - 4 * n4) bm[4 * n4 + g] = 0;
-  }
-}
-
-// k_list_bscan + k_list_vbase in one launch (a decode's sizing, one kernel
-// boundary less).  Block b < nblk scans its NT pages' counts, publishes its
+// A decode's sizing in one launch: page counts (from the headers with
+// a.peek, else the exact pass's), block scans and global bases, and each
+// page's values-stream descriptor (a.peek), so the values decode needs
+// nothing from k_list_levels.  Block b < nblk scans its NT pages' counts, publishes its
 // row / leaf totals as two words of blk tagged with a.epoch (top 16 bits),
 // and sums the totals of blocks 0..b-1 -- every predecessor's own total, no
 // inclusive prefixes, so no block waits on another's wait: the lower blocks
 // were dispatched first (workgroups launch in order on each XCD), each
 // publishes as soon as its scan is done.  A stale word (an earlier decode's
-// tag, or the plan's zeroed state) reads as not yet published.  Every block
-// zeroes its share of the bitmaps first.
+// tag, or the plan's zeroed state) reads as not yet published.  The bitmaps
+// need no zeroing (k_list_levels clears and sets only the bits it owns), but
+// for the bits past the column's last row / leaf: the last page's thread
+// zeroes the final word of each bitmap before k_list_levels runs.
 __global__ __launch_bounds__(NT) void k_list_bases(ListArgs a) {
   __shared__ Shared sh;
   __shared__ uint64_t red[2][NW];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  {  // zero the bitmaps, 16 B a thread per step
-    const uint64_t nt = (uint64_t)gridDim.x * NT, g = (uint64_t)blockIdx.x * NT + tid;
-    for (int m = 0; m < 2; m++) {
-      uint32_t* bm = m ? a.out_leaf_validity : a.out_list_validity;
-      const uint64_t nw = m ? a.zw_leaf : a.zw_list;
-      if (!bm || !nw) continue;
-      const uint64_t n4 = nw / 4;
-      for (uint64_t i = g; i < n4; i += nt) ((u32x4*)bm)[i] = u32x4{0, 0, 0, 0};
-      if (g < nw - 4 * n4) bm[4 * n4 + g] = 0;
-    }
-  }
-  const uint32_t nblk = (a.n_pages + NT - 1) / NT;
-  if (blockIdx.x >= nblk) return;
   const uint32_t p = blockIdx.x * NT + tid;
   uint64_t c = 0;
   uint64_t vpos = ~0ull;
@@ -5275,6 +5179,11 @@ __global__ __launch_bounds__(NT) void k_list_bases(ListArgs a) {
     const uint64_t rbase = red[0][0] + er, lbase = red[1][0] + el;
     a.local[2 * p] = rbase;
     a.local[2 * p + 1] = lbase;
+    if (p == a.n_pages - 1) {
+      const uint64_t tr_all = rbase + (c >> 32), tl_all = lbase + (c & 0xFFFFFFFFull);
+      if (a.nl && a.out_list_validity && (tr_all & 31)) a.out_list_validity[tr_all >> 5] = 0;
+      if (a.ni && a.out_leaf_validity && (tl_all & 31)) a.out_leaf_validity[tl_all >> 5] = 0;
+    }
     if (a.peek) {
       const bool ok = vpos + 9 <= pd.byte_len;
       a.vpages[p] = PageDesc{pd.byte_off + (ok ? vpos : 0), lbase, ok ? pd.byte_len - (uint32_t)vpos : 0,
@@ -5283,7 +5192,7 @@ __global__ __launch_bounds__(NT) void k_list_bases(ListArgs a) {
   }
 }
 
-// Levels pass: one wave per page, at the global bases k_list_vbase wrote.
+// Levels pass: one wave per page, at the global bases k_list_bases wrote.
 // Writes offsets and both bitmaps, its status, and (unless the values
 // descriptors came from the headers) the page's values-stream descriptor;
 // the last page also the totals and the final offset.
@@ -5779,7 +5688,7 @@ namespace sb {
 int launch_list(int stage, const ListLaunch& L, void* stream) {
   sbk::ListArgs a{L.chunk, L.pages, L.n_pages, L.list_nullable, L.item_nullable, L.offset_width, L.width, L.peek,
                   L.counts, L.local, L.blk, L.totals, (uint4*)L.lvdesc, L.vpages, L.out_offsets, L.out_list_validity,
-                  L.out_leaf_validity, L.status, L.zw_list, L.zw_leaf, L.epoch};
+                  L.out_leaf_validity, L.status, L.epoch};
   if (L.n_pages == 0) return 0;
   const uint32_t grid = std::min<uint32_t>((L.n_pages + sbk::NW - 1) / sbk::NW, kListGrid);
   const uint32_t nblk = (L.n_pages + sbk::NT - 1) / sbk::NT;
@@ -5788,11 +5697,8 @@ int launch_list(int stage, const ListLaunch& L, void* stream) {
     hipLaunchKernelGGL(sbk::k_list_size, dim3(grid), dim3(sbk::NT), 0, st, a);
   } else if (stage == 1) {  // block bases (+ header sizing when peek)
     hipLaunchKernelGGL(sbk::k_list_bscan, dim3(nblk), dim3(sbk::NT), 0, st, a);
-  } else if (stage == 3 || stage == 4) {  // global bases, values descriptors (peek), zeroed bitmaps
-    const uint64_t zw = std::max(L.zw_list, L.zw_leaf);
-    const uint32_t zg = (uint32_t)std::min<uint64_t>((zw / 4 + sbk::NT - 1) / sbk::NT, 1024);
-    if (stage == 3) hipLaunchKernelGGL(sbk::k_list_vbase, dim3(std::max(nblk, zg)), dim3(sbk::NT), 0, st, a);
-    else hipLaunchKernelGGL(sbk::k_list_bases, dim3(std::max(nblk, zg)), dim3(sbk::NT), 0, st, a);
+  } else if (stage == 4) {  // counts, global bases, values descriptors (peek)
+    hipLaunchKernelGGL(sbk::k_list_bases, dim3(nblk), dim3(sbk::NT), 0, st, a);
   } else {
     hipLaunchKernelGGL(sbk::k_list_levels, dim3(grid), dim3(sbk::NT), 0, st, a);
   }

@@ -238,10 +238,10 @@ int launch_utf8_check(int offset_width, const Utf8Launch& a, void* stream);
 
 // List<primitive> columns: stage 0 = exact sizing pass (one wave per page,
 // walks the levels); stage 1 = block bases (peek = 1: counts from the page
-// headers instead); stage 3 = global bases + values descriptors + zeroed
-// bitmaps; stage 4 = stages 1 and 3 in one launch (blocks exchange their
-// totals through `blk`, tagged with `epoch`); stage 2 = offsets + bitmaps +
-// values-stream descriptors.
+// headers instead; the plan's check of the headers); stage 4 = counts +
+// global bases + values descriptors (blocks exchange their totals through
+// `blk`, tagged with `epoch`); stage 2 = offsets + bitmaps (+ values
+// descriptors without peek).
 struct ListLaunch {
   const uint8_t* chunk;
   const PageDesc* pages;
@@ -258,7 +258,6 @@ struct ListLaunch {
   uint32_t* out_list_validity;
   uint32_t* out_leaf_validity;
   uint32_t* status;
-  uint64_t zw_list, zw_leaf;  // stages 3 / 4: validity bitmap words to zero (0: none)
   uint32_t epoch;             // stage 4: this decode's tag (1..65535) on the block totals
 };
 constexpr uint32_t kListGrid = 2048;
