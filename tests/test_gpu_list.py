@@ -110,6 +110,14 @@ def test_list_repeated_decodes_multi_block(ctx):
     dec.close()
 
 
+def test_list_9000_one_row_pages(ctx):
+    """9 000 pages: k_list_bases' 36 workgroups exchange their totals, and
+    k_list_levels walks more pages than it has waves."""
+    rng = np.random.default_rng(9)
+    offs, lv, child, cv = make_lists(9000, rng)
+    check(ctx, offs, lv, child, cv, True, True, 1, O.WriteOptions.make())
+
+
 def test_list_long_lists_multi_tile(ctx):
     """Pages with many levels per row: several level tiles per page; the
     level streams exceed the LDS stage and are read from HBM."""
