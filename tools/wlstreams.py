@@ -25,7 +25,7 @@ def main():
     else:
         wl = bench.WorkloadC5(torch, pa_amd, 8_388_608, 555, 0, thr)
     wall, k, ok = bench.timed(torch, None, wl, steps, 3)
-    print(f"{name} streams={os.environ.get('SB_BENCH_STREAMS', 'torch')}: ok={ok} wall {wall / steps * 1e3:.3f} ms/step, "
+    print(f"{name} streams={os.environ.get('SB_BENCH_STREAMS', 'default')}: ok={ok} wall {wall / steps * 1e3:.3f} ms/step, "
           f"event median {float(np.median(k)):.3f} ms", flush=True)
 
 
