@@ -885,7 +885,7 @@ class WorkloadC5:
         names = {0: "none", 1: "lz4", 2: "zstd", 3: "snappy", 10: "rle", 11: "dict", 12: "one_value", 13: "freq",
                  14: "bitpacking", 15: "delta_bitpacking", 16: "patas"}
         nb = (rows + 7) // 8
-        self.ss = StreamSet(torch, pa, device, 4)
+        self.ss = StreamSet(torch, pa, device, int(os.environ.get("SB_C5_STREAMS", "4")))
         enc = []  # device encode inputs: (dt, opts, nullable, device tensors)
         for ci, (dt, kind) in zip(self.col_ids, specs):
             v, valid, nullable, opts, chunk, metas, enc_s = self.host_column(pa, dt, kind, ci, rows, seed, threads)
