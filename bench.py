@@ -480,11 +480,12 @@ class StreamSet:
         self.torch = torch
         self.ctxs = [pa.Context(device) for _ in range(n)]
         mode = os.environ.get("SB_BENCH_STREAMS", mode)
-        if mode == "prio":
-            # torch side streams, the last one at high priority: a queue of its
-            # own (priority is a property of the hardware queue), and its
-            # column's small kernels dispatch ahead of the other's inflate waves
-            self.streams = [torch.cuda.Stream(device=device, priority=-1 if i == n - 1 else 0) for i in range(n)]
+        if mode in ("prio", "prio0"):
+            # torch side streams, the last one (prio0: the first) at high
+            # priority: a queue of its own (priority is a property of the
+            # hardware queue), and its column's kernels dispatch first
+            hi = 0 if mode == "prio0" else n - 1
+            self.streams = [torch.cuda.Stream(device=device, priority=-1 if i == hi else 0) for i in range(n)]
             for c, st in zip(self.ctxs, self.streams):
                 c.use_stream(st)
         elif mode == "own":
@@ -579,7 +580,7 @@ class WorkloadC3:
         # Float64 and Utf8 columns on streams of their own: the second column's
         # k_inflate waves take the wave slots the first one's leave as its
         # job queue drains
-        self.ss = StreamSet(torch, pa, device, 2, mode="prio")
+        self.ss = StreamSet(torch, pa, device, 2, mode="prio0")
         fd, sd = [fh.to(dev) for _ in range(2)], [sh.to(dev) for _ in range(2)]
         torch.cuda.synchronize()
         self.fdec = [pa.ColumnDecoder.for_shard(fd[i], self.fmetas, self.fcol.shard, np.float64, True, ctx=self.ss.ctxs[0])
