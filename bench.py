@@ -1065,7 +1065,7 @@ class WorkloadC5:
         return ok
 
 
-TRAFFIC_FILE = "r06b_pmc_traffic.json"  # tools/pmc_traffic.sh -> tools/publish_traffic.py
+TRAFFIC_FILE = "r06c_pmc_traffic.json"  # tools/pmc_traffic.sh -> tools/publish_traffic.py
 
 
 def load_traffic(workload: str):
