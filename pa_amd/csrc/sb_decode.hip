@@ -1256,7 +1256,12 @@ __device__ __forceinline__ uint32_t lds_chain(lds_u8* tab, uint32_t t1) {
 #ifndef SB_INF_MATCHFAST
 #define SB_INF_MATCHFAST 24  // longer matches go the hazard way (C3 3.64 -> 3.59 ms, C5 2.36 -> 2.33 against 32)
 #endif
-constexpr uint32_t kIb = 1024, kIbHalf = kIb / 2, kLitFast = 64, kMatchFast = SB_INF_MATCHFAST;
+#ifndef SB_INF_LITFAST
+#define SB_INF_LITFAST 64
+#endif
+constexpr uint32_t kIb = 1024, kIbHalf = kIb / 2, kLitFast = SB_INF_LITFAST, kMatchFast = SB_INF_MATCHFAST;
+// (a batch's bytes, <= p + 261 + kLitFast, stay inside the staged input window)
+static_assert(kIbHalf + 261 + kLitFast + 20 <= kIb, "kLitFast too large for the input ring");
 constexpr uint32_t kChainTabs = 6;  // T1..T32: batches of up to 64 sequences
 constexpr uint32_t kChainEnd = 0xFE, kChainStop = 0xFF;  // chain sentinels (see cand_steps)
 
@@ -1400,7 +1405,7 @@ __device__ __forceinline__ uint32_t cand_steps(const lds_u8* ib, uint32_t p, uin
   const uint32_t nxt = __builtin_amdgcn_alignbyte(w2, w1, sh);   // bytes x0 + 4 .. x0 + 7
   const uint32_t ext = __builtin_amdgcn_alignbyte(nxt, tok, 1);  // bytes x0 + 1 .. x0 + 4
   uint32_t t1 = 0;
-  if (lim - p >= 325) {  // every candidate's bytes (<= p + 324) are staged: no bounds checks
+  if (lim - p >= 261 + kLitFast) {  // every candidate's bytes (<= p + 260 + kLitFast) are staged: no bounds checks
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
       const uint32_t x = x0 + k, t = (tok >> (8 * k)) & 0xFFu, e = (ext >> (8 * k)) & 0xFFu;
